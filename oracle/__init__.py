@@ -1,0 +1,6 @@
+"""CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline
+leg may import this package, and only as the checker / CPU baseline.  The
+product package never imports it.
+"""

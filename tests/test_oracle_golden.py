@@ -1,0 +1,161 @@
+"""Pin the CPU oracle against golden vectors produced by the reference itself
+(tests/golden/gen_golden.py imports /root/reference in the build container).
+
+Tolerances: forward/loss/gradients on identical weights are fp32-exact up to
+summation order (rtol 1e-4, the north-star bar).  Adam is compared from the
+reference's own gradients (it turns g into ~sign(g)*lr, so a trajectory
+comparison would amplify summation noise in near-zero gradients).
+Scoring is compared on the reference's trained weights.  NAP is compared with
+the reference's own fit (the synthetic diffs are rank-deficient, so an
+independently fitted SVD is noise-dominated in its null directions) and its
+fit separately on a well-conditioned case."""
+import numpy as np
+import pytest
+
+from oracle import ae_oracle as O
+from oracle.model_io import model_from_state_dict, state_dict_from_model, grads_to_flat
+from icra2021_multimodal_ad_amd.common_utils import init_state_dict, get_hidden_layer_sizes
+
+CASES = ["c1_ft64", "mm192"]
+
+
+def _sd(g, prefix):
+    return {k[len(prefix):]: g[k] for k in g.files if k.startswith(prefix)}
+
+
+def _rel(a, r):
+    return float(np.abs(np.asarray(a, np.float64) - r).max() / (np.abs(r).max() + 1e-30))
+
+
+def test_hidden_layer_sizes_match_reference_probe():
+    # SURVEY §8 a1 probe values
+    assert get_hidden_layer_sizes(1728, 100, 4) == [1402, 1076, 751, 425]
+    assert get_hidden_layer_sizes(2048, 100, 4) == [1658, 1268, 879, 489]
+    assert get_hidden_layer_sizes(64, 100, 4) == [71, 78, 85, 92]
+    assert get_hidden_layer_sizes(1728, 200, 4) == [1422, 1116, 811, 505]
+    assert O.get_hidden_layer_sizes(100, 1728, 4) == get_hidden_layer_sizes(100, 1728, 4)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_forward_loss_grads(golden, name):
+    g = golden(name)
+    m = model_from_state_dict(_sd(g, "init/"))
+    loss, xh, grads = O.ae_train_grads(g["x/0"], m)
+    assert abs(loss - g["step1/loss"]) <= 1e-5 * g["step1/loss"]
+    assert _rel(xh, g["step1/x_hat"]) < 1e-5
+    for k, v in grads_to_flat(grads).items():
+        assert _rel(v, g["step1/grad/" + k]) < 1e-4, k
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_bn_running_stats_after_step(golden, name):
+    g = golden(name)
+    m = model_from_state_dict(_sd(g, "init/"))
+    O.ae_forward(g["x/0"], m, train=True)
+    sd = state_dict_from_model(m)
+    for k, v in sd.items():
+        if "running" in k:
+            assert _rel(v, g["after0/" + k]) < 1e-5, k
+        if "num_batches" in k:
+            assert int(v) == int(g["after0/" + k])
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_adam_from_reference_grads(golden, name):
+    g = golden(name)
+    m = model_from_state_dict(_sd(g, "init/"))
+    grads = {"enc": [], "dec": []}
+    for side, nm in (("enc", "encoder"), ("dec", "decoder")):
+        for i, layer in enumerate(m[side]):
+            p = f"step1/grad/{nm}.net.{i}."
+            d = {"W": g[p + "layer.weight"], "b": g[p + "layer.bias"]}
+            if layer["bn"] is not None:
+                d["gamma"], d["beta"] = g[p + "bn.weight"], g[p + "bn.bias"]
+            grads[side].append(d)
+    O.adam_step(m, grads, {})
+    for k, v in state_dict_from_model(m).items():
+        if "running" in k or "num_batches" in k:
+            continue
+        assert np.abs(np.asarray(v, np.float64) - g["after0/" + k]).max() < 1e-7, k
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_first_step_loss_trajectory(golden, name):
+    g = golden(name)
+    m = model_from_state_dict(_sd(g, "init/"))
+    st = {}
+    l0 = O.train_step(g["x/0"], m, st)
+    assert abs(l0 - g["loss/0"]) <= 1e-5 * g["loss/0"]
+    l1 = O.train_step(g["x/1"], m, st)
+    # second step sees post-Adam weights: sign(g) amplification of summation noise
+    assert abs(l1 - g["loss/1"]) <= 5e-3 * g["loss/1"]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_eval_forward_and_scoring(golden, name):
+    g = golden(name)
+    steps = int(g["meta_steps"])
+    m = model_from_state_dict(_sd(g, f"after{steps - 1}/"))
+    xe, _ = O.ae_forward(g["x/0"], m, train=False)
+    assert _rel(xe, g["eval/x_hat"]) < 1e-5
+    diffs = O.get_diffs(g["score/test_x"], m)
+    for i, d in enumerate(diffs):
+        assert np.abs(d - g[f"score/test_diff{i}"]).max() < 1e-4
+    lab = g["score/test_label"]
+    b, s = O.base_score(diffs), O.sap_score(diffs)
+    assert _rel(b, g["score/base"]) < 1e-4
+    assert _rel(s, g["score/sap"]) < 1e-4
+    assert abs(O.auroc(b, lab) - g["score/base_auroc"]) < 1e-9
+    assert abs(O.auroc(s, lab) - g["score/sap_auroc"]) < 1e-9
+    fit = {"mu_r": g["score/nap_mu_r"], "v": g["score/nap_v"], "mu_s": g["score/nap_mu_s"],
+           "var": g["score/nap_var"]}
+    n = O.nap_score(np.concatenate(diffs, axis=1), fit)
+    assert _rel(n, g["score/nap"]) < 1e-4
+    assert abs(O.auroc(n, lab) - g["score/nap_auroc"]) < 2e-3
+
+
+def test_nap_fit_well_conditioned(golden):
+    g = golden("nap")
+    fit = O.nap_fit(g["train"])
+    assert _rel(fit["var"], g["var"]) < 1e-4
+    assert _rel(fit["mu_r"], g["mu_r"]) < 1e-4
+    assert _rel(O.nap_score(g["test"], fit), g["score"]) < 1e-4
+
+
+def test_d1728_reference_width(golden):
+    g = golden("d1728")
+    m = model_from_state_dict(init_state_dict(1728, 100, 5, seed=2))
+    loss, xh, grads = O.ae_train_grads(g["x/0"], m)
+    assert abs(loss - g["step1/loss"]) <= 1e-5 * g["step1/loss"]
+    assert _rel(xh[:8], g["step1/x_hat"]) < 1e-5
+    for k, v in grads_to_flat(grads).items():
+        v = v.astype(np.float64)
+        sq = g["step1/gradsq/" + k]
+        assert abs((v ** 2).sum() - sq) <= 1e-4 * sq, k
+        assert abs(v.sum() - g["step1/gradsum/" + k]) <= 1e-3 * np.sqrt(sq * v.size), k
+
+
+def test_vib_reparam_and_k_expanded_decoder(golden):
+    g = golden("vib")
+    sd_e = {"encoder." + k[4:]: g[k] for k in g.files if k.startswith("enc/")}
+    sd_d = {"decoder." + k[4:]: g[k] for k in g.files if k.startswith("dec/")}
+    m = model_from_state_dict({**sd_e, **sd_d})
+    out, _ = O.module_forward(g["x"], m["enc"], train=True)
+    mu, lv = O.vib_split(out)
+    assert _rel(mu, g["mu"]) < 1e-5 and _rel(lv, g["logvar"]) < 1e-5
+    z = O.vib_reparam(mu, lv, g["eps"])
+    assert _rel(z, g["z"]) < 1e-5
+    xh, _ = O.module_forward(z, m["dec"], train=True)     # [k,B,D], BN over k*B rows
+    assert xh.shape == g["x_hat"].shape
+    assert _rel(xh, g["x_hat"]) < 1e-4
+    assert bool(g["k0_raises"])
+    assert g["det_z"].shape[0] == 2
+
+
+def test_auroc_matches_sklearn():
+    from sklearn import metrics
+    rng = np.random.default_rng(0)
+    s = np.round(rng.normal(size=500), 1)            # with ties
+    lab = rng.random(500) < 0.3
+    fpr, tpr, _ = metrics.roc_curve(lab, s)
+    assert abs(O.auroc(s, lab) - metrics.auc(fpr, tpr)) < 1e-12
