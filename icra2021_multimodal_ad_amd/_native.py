@@ -1,0 +1,126 @@
+"""ctypes binding of libmmad.so (the C-ABI declared in include/mmad.h).
+
+There is no fallback: if the library is missing or no GPU is visible, calls
+raise ``NativeUnavailable``.  Loading the library itself needs no GPU (the CPU
+test-suite checks the exported symbols).
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MMAD_LIB", os.path.join(HERE, "libmmad.so"))
+
+MMAD_OK = 0
+F32, BF16 = 0, 1
+ACT = {None: 0, "leakyrelu": 1, "relu": 2, "sigmoid": 3, "tanh": 4}
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_I64 = ctypes.c_int64
+_U64 = ctypes.c_uint64
+
+# name -> (restype, argtypes); mirrors include/mmad.h one-to-one
+SIGNATURES = {
+    "mmad_last_error_string": (ctypes.c_char_p, []),
+    "mmad_abi_version": (_I, []),
+    "mmad_pad_granule": (_I, []),
+    "mmad_fc_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P, _P, _P, _P, _P]),
+    "mmad_fc_fwd_mse": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _F, _P, _P, _P]),
+    "mmad_fc_fwd_score": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P, _P, _P, _P,
+                               _P, _P, _I, _P]),
+    "mmad_bn_eval_affine": (_I, [_I, _I, _P, _P, _P, _P, _F, _P, _P, _P]),
+    "mmad_bn_train_apply": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P,
+                                 _P]),
+    "mmad_fc_bwd_data": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "mmad_fc_bwd_weight": (_I, [_I, _I, _I, _I, _P, _P, _P, _P]),
+    "mmad_bn_act_bwd_ws": (ctypes.c_size_t, [_I, _I]),
+    "mmad_bn_act_bwd": (_I, [_I, _I, _F, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                             _P]),
+    "mmad_colsum": (_I, [_I, _I, _I, _P, _I, _F, _P, _P]),
+    "mmad_sum": (_I, [_I64, _P, _F, _P, _I, _P]),
+    "mmad_pack_input": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _P]),
+    "mmad_unpack_output": (_I, [_I, _I, _I, _I, _P, _P, _I, _P]),
+    "mmad_adam": (_I, [_I64, _P, _P, _P, _P, _F, _F, _F, _F, _F, _P, _I64, _P]),
+    "mmad_vib_reparam_fwd": (_I, [_I, _I, _I, _I, _P, _I, _P, _P, _U64, _U64, _I, _P, _I, _P, _P]),
+    "mmad_vib_reparam_bwd": (_I, [_I, _I, _I, _I, _P, _I, _P, _P, _I, _F, _P, _I, _P, _P]),
+    "mmad_ae_create": (_I, [ctypes.POINTER(_P), _I, _I, ctypes.POINTER(_I), _I,
+                            ctypes.POINTER(_I), _I, _F, _F, _F]),
+    "mmad_ae_destroy": (None, [_P]),
+    "mmad_ae_layout": (_I, [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
+    "mmad_ae_workspace_bytes": (_I64, [_P, _I, _I]),
+    "mmad_ae_bind": (_I, [_P, _P, _P, _P, _P, _P, _P]),
+    "mmad_ae_sync_shadow": (_I, [_P, _P]),
+    "mmad_ae_train_fwd_bwd": (_I, [_P, _P, _I, _I, _I, _P, _U64, _U64, _F, _P, _P, _I64, _P]),
+    "mmad_ae_backward": (_I, [_P, _P, _I, _I, _P, _I64, _P]),
+    "mmad_ae_adam": (_I, [_P, _F, _F, _F, _F, _I, _P]),
+    "mmad_ae_forward": (_I, [_P, _P, _I, _I, _I, _P, _I, _P, _P, _I64, _P]),
+    "mmad_ae_score": (_I, [_P, _P, _I, _I, _P, _P, _P, _I64, _P]),
+}
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load libmmad.so (no GPU needed).  Raises NativeUnavailable if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeUnavailable(
+            f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (or `make -C icra2021_multimodal_ad_amd/csrc`)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status, what=""):
+    if status != MMAD_OK:
+        msg = load().mmad_last_error_string().decode(errors="replace")
+        raise NativeError(f"{what}: status {status}: {msg}")
+
+
+def call(name, *args):
+    """Call an mmad_* entry point and raise on a non-zero status."""
+    fn = getattr(load(), name)
+    check(fn(*args), name)
+
+
+def require_gpu(t=None):
+    """Fail loudly unless the HIP path can run (no CPU fallback exists)."""
+    import torch
+    load()
+    if not torch.cuda.is_available():
+        raise NativeUnavailable("icra2021_multimodal_ad_amd needs a ROCm GPU (MI355X); "
+                                "torch.cuda.is_available() is False")
+    if t is not None and not t.is_cuda:
+        raise NativeUnavailable("tensor must live on the GPU (call model.cuda() / get_model with "
+                                "gpu_id >= 0)")
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def stream_ptr(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def pad(n, g=128):
+    return (int(n) + g - 1) // g * g

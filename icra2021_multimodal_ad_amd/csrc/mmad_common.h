@@ -1,0 +1,77 @@
+// Shared device/host helpers for the MI355X (gfx950) autoencoder hot path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/mmad.h"
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned int uint4v __attribute__((ext_vector_type(4)));
+
+#define MMAD_LDS __attribute__((address_space(3)))
+
+// Padding granule for every feature / batch dimension of the packed layouts
+// (see DESIGN.md "Data layout in HBM"): GEMM tiles never need K/N masking.
+#define MMAD_PAD 128
+// Rows per BatchNorm / column-sum partial written by GEMM epilogues.
+#define MMAD_PART_ROWS 32
+
+static inline int mmad_roundup(int x, int g) { return (x + g - 1) / g * g; }
+
+// ---- error reporting (thread-local, no exceptions across the ABI) -------
+void mmad_set_error(const char* fmt, ...);
+#define MMAD_CHECK_ARG(cond, ...)                                      \
+  do {                                                                 \
+    if (!(cond)) { mmad_set_error(__VA_ARGS__); return MMAD_EINVAL; }  \
+  } while (0)
+#define MMAD_HIP_CHECK(expr)                                                   \
+  do {                                                                         \
+    hipError_t e_ = (expr);                                                    \
+    if (e_ != hipSuccess) {                                                    \
+      mmad_set_error("HIP error %s at %s:%d", hipGetErrorString(e_), __FILE__, \
+                     __LINE__);                                                \
+      return MMAD_EHIP;                                                        \
+    }                                                                          \
+  } while (0)
+#define MMAD_LAUNCH_CHECK() MMAD_HIP_CHECK(hipGetLastError())
+
+// ---- element conversion ---------------------------------------------------
+template <typename T> __device__ __forceinline__ float to_f32(T v);
+template <> __device__ __forceinline__ float to_f32<float>(float v) { return v; }
+template <> __device__ __forceinline__ float to_f32<bf16>(bf16 v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T from_f32(float v);
+template <> __device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float v) { return (bf16)v; }
+
+// activation enum shared with the ABI (modules/activation.py:20-45)
+__device__ __forceinline__ float apply_act(float z, int act, float slope) {
+  switch (act) {
+    case MMAD_ACT_LEAKYRELU: return z > 0.f ? z : z * slope;
+    case MMAD_ACT_RELU: return z > 0.f ? z : 0.f;
+    case MMAD_ACT_SIGMOID: return 1.f / (1.f + __expf(-z));
+    case MMAD_ACT_TANH: return tanhf(z);
+    default: return z;
+  }
+}
+// derivative expressed through the activation OUTPUT a (all supported acts
+// are monotone so the output determines the branch / value)
+__device__ __forceinline__ float act_grad_from_out(float a, int act, float slope) {
+  switch (act) {
+    case MMAD_ACT_LEAKYRELU: return a > 0.f ? 1.f : slope;
+    case MMAD_ACT_RELU: return a > 0.f ? 1.f : 0.f;
+    case MMAD_ACT_SIGMOID: return a * (1.f - a);
+    case MMAD_ACT_TANH: return 1.f - a * a;
+    default: return 1.f;
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}

@@ -1,0 +1,41 @@
+// Internal GEMM interface (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+enum GemmEpiKind {
+  GEMM_EPI_FWD = 0,         // y = BNaffine(act(acc + bias)); optional Welford partials
+  GEMM_EPI_MSE = 1,         // dz = gscale*(acc + bias - target); partials (sum dz, sum d^2)
+  GEMM_EPI_BWD_DATA = 2,    // dx = acc; optional column-sum partials
+  GEMM_EPI_BWD_WEIGHT = 3,  // dW = acc (fp32 out)
+  GEMM_EPI_SCORE = 4,       // as FWD (eval) + row-sum of (y - ref)^2, optional diff out
+};
+
+struct GemmEpi {
+  int M, N;              // valid rows / cols of the output
+  void* out;             // output, ld = ldo elements
+  int ldo;
+  const float* bias;     // [Np]
+  int act;
+  float slope;
+  const float* bn_scale; // eval-mode BN affine (nullable)
+  const float* bn_shift;
+  float* part;           // partials [Mp/32][2][ldpart]
+  int ldpart;
+  const float* target;   // MSE target (fp32 user input), ld = ldt
+  int ldt;
+  int tmod;              // MSE target row = row % tmod (k-expanded VIB decoder)
+  float gscale;          // MSE gradient scale (2 for sum-MSE, 2/k for VIB)
+  const void* ref;       // SCORE reference activations (same dtype as out)
+  int ldref;
+  float* rowsq;          // SCORE row partials [Np/BN][ldrow]
+  int ldrow;
+  float* diff;           // SCORE optional fp32 diff output
+  int lddiff;
+};
+
+int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,
+                       int Np, int K, const GemmEpi& ep, hipStream_t s);
+int mmad_pick_tile(int Mp, int Np, int epi);
+int mmad_tile_override();
+// width (columns) of the tile the score epilogue will use for an Np-wide output
+static inline int mmad_score_tile_n() { return 128; }

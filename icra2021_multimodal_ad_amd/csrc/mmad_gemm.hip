@@ -1,0 +1,411 @@
+// MFMA GEMM for the fc_module encoder/decoder stack on gfx950 (CDNA4).
+//
+// One kernel template covers the three contractions of an FCLayer
+// (layers/fc_layer.py:37-48 forward; its autograd backward):
+//   forward      y  = x  . W^T  (+bias, act, BN-eval affine | BN-train stats
+//                                 | MSE grad/loss | score-diff epilogues)
+//   backward-dx  dx = dz . W     (B operand is MN-major: W stored [out][in])
+//   backward-dW  dW = dz^T . x   (both operands MN-major: K = batch)
+// Operands stay in the caller's row-major packed layout; an MN-major operand
+// is transposed on the LDS read side with ds_read_b64_tr_b16 (bf16) or plain
+// per-k reads (f32), so no transposed copies are ever materialised in HBM.
+//
+// Tile: BM x BN = (32*MI) x (32*NI), 256 threads = 4 waves in 2x2, each wave
+// (16*MI) x (16*NI) built from 16x16 MFMA tiles (bf16: v_mfma_f32_16x16x32_bf16,
+// f32: v_mfma_f32_16x16x4_f32, exact f32 for the parity path).  K stage =
+// 128 bytes of K per row (BK = 64 bf16 / 32 f32), register-staged global
+// loads (16 B/lane), double-buffered LDS, one barrier per stage.
+//
+// LDS images:
+//  * K-major operand: [rows][128 B], 16-byte chunk j stored at j ^ ((row>>1)&7)
+//    -> the two ds_read_b64 (bf16) / one ds_read_b128 (f32) fragment reads of
+//    a wave are bank-conflict free.
+//  * MN-major operand: [BK][rows*esize + pad], pad = 32 B (bf16) / 16 B (f32):
+//    tr-reads of 8 consecutive k-rows hit disjoint banks.
+// bf16 k-slot order inside one 32-deep MFMA step: lane group g (= lane>>4)
+// owns k = {4g..4g+3} U {16+4g..16+4g+3}; A and B use the same permutation,
+// so the contraction is exact.
+#include "mmad_common.h"
+#include "mmad_gemm.h"
+
+namespace {
+
+template <typename T> struct Esz { static constexpr int v = sizeof(T); };
+
+template <typename T, bool KMAJ, int ROWS>
+struct Img {
+  static constexpr int ES = sizeof(T);
+  static constexpr int BK = 128 / ES;                       // K per stage
+  static constexpr int PADB = (ES == 2) ? 32 : 16;
+  static constexpr int STRIDE = KMAJ ? 128 : ROWS * ES + PADB;  // bytes per LDS row
+  static constexpr int BYTES = KMAJ ? ROWS * 128 : BK * (ROWS * ES + PADB);
+  static constexpr int CHUNKS = ROWS * 8 / 256;              // 16 B chunks per thread
+  static constexpr int CPR = ROWS * ES / 16;                 // MN-major: chunks per k-row
+};
+
+// global -> registers for one stage of one operand
+template <typename T, bool KMAJ, int ROWS>
+__device__ __forceinline__ void stage_load(uint4v* r,
+                                           const T* __restrict__ G, int ld, int r0, int k0, int tid) {
+  using I = Img<T, KMAJ, ROWS>;
+  constexpr int EPC = 16 / sizeof(T);  // elements per chunk
+#pragma unroll
+  for (int i = 0; i < I::CHUNKS; ++i) {
+    int c = tid + 256 * i;
+    const T* p;
+    if (KMAJ) {
+      int row = c >> 3, j = c & 7;
+      p = G + (size_t)(r0 + row) * ld + k0 + j * EPC;
+    } else {
+      int kr = c / I::CPR, j = c % I::CPR;
+      p = G + (size_t)(k0 + kr) * ld + r0 + j * EPC;
+    }
+    r[i] = *(const uint4v*)p;
+  }
+}
+
+template <typename T, bool KMAJ, int ROWS>
+__device__ __forceinline__ void stage_store(char* img, const uint4v* r,
+                                            int tid) {
+  using I = Img<T, KMAJ, ROWS>;
+#pragma unroll
+  for (int i = 0; i < I::CHUNKS; ++i) {
+    int c = tid + 256 * i;
+    int off;
+    if (KMAJ) {
+      int row = c >> 3, j = c & 7;
+      off = row * 128 + ((j ^ ((row >> 1) & 7)) << 4);
+    } else {
+      int kr = c / I::CPR, j = c % I::CPR;
+      off = kr * I::STRIDE + (j << 4);
+    }
+    *(uint4v*)(img + off) = r[i];
+  }
+}
+
+// ---- bf16 fragment reads (16x16x32 MFMA operand, permuted k slots) ------
+template <bool KMAJ, int ROWS>
+__device__ __forceinline__ bf16x8 frag_bf16(const char* img, int rbase, int kk, int lane) {
+  using I = Img<bf16, KMAJ, ROWS>;
+  const int g = lane >> 4;
+  if (KMAJ) {
+    const int m = rbase + (lane & 15);
+    const int f = ((m >> 1) & 7) << 1;        // swizzle in 8-byte units
+    const int c1 = (kk * 8 + g) ^ f;
+    const int c2 = (kk * 8 + 4 + g) ^ f;
+    bf16x4 lo = *(const bf16x4*)(img + m * 128 + c1 * 8);
+    bf16x4 hi = *(const bf16x4*)(img + m * 128 + c2 * 8);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  } else {
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    const int k1 = kk * 32 + 4 * g + q;
+    const int col = rbase + 4 * p;
+    const MMAD_LDS char* base = (const MMAD_LDS char*)img;
+    short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (MMAD_LDS short4v*)(base + k1 * I::STRIDE + col * 2));
+    short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (MMAD_LDS short4v*)(base + (k1 + 16) * I::STRIDE + col * 2));
+    bf16x4 l4 = __builtin_bit_cast(bf16x4, lo);
+    bf16x4 h4 = __builtin_bit_cast(bf16x4, hi);
+    return __builtin_shufflevector(l4, h4, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+}
+
+// ---- f32 fragment reads (16x16x4 MFMA, 4 steps per 16-deep chunk) -------
+template <bool KMAJ, int ROWS>
+__device__ __forceinline__ floatx4 frag_f32(const char* img, int rbase, int kc, int lane) {
+  using I = Img<float, KMAJ, ROWS>;
+  const int g = lane >> 4;
+  if (KMAJ) {
+    const int m = rbase + (lane & 15);
+    const int j = (kc * 4 + g) ^ ((m >> 1) & 7);
+    return *(const floatx4*)(img + m * 128 + j * 16);
+  } else {
+    const int col = rbase + (lane & 15);
+    floatx4 r;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) r[s] = *(const float*)(img + (kc * 16 + 4 * g + s) * I::STRIDE + col * 4);
+    return r;
+  }
+}
+
+}  // namespace
+
+// -------------------------------------------------------------------------
+template <typename T, typename TO, bool AK, bool BK_, int MI, int NI, int EPI>
+__global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__ A, int lda,
+                                                            const T* __restrict__ B, int ldb, int K,
+                                                            GemmEpi ep) {
+  constexpr int BM = 32 * MI, BN = 32 * NI;
+  using IA = Img<T, AK, BM>;
+  using IB = Img<T, BK_, BN>;
+  constexpr int STAGE = IA::BYTES + IB::BYTES;
+  constexpr int OSTRIDE = BN * (int)sizeof(TO) + 16;
+  constexpr int OBYTES = BM * OSTRIDE;
+  constexpr int LDS_BYTES = (2 * STAGE > OBYTES) ? 2 * STAGE : OBYTES;
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int nt = K / IA::BK;
+
+  floatx4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  uint4v ra[IA::CHUNKS], rb[IB::CHUNKS];
+  stage_load<T, AK, BM>(ra, A, lda, m0, 0, tid);
+  stage_load<T, BK_, BN>(rb, B, ldb, n0, 0, tid);
+  stage_store<T, AK, BM>(smem, ra, tid);
+  stage_store<T, BK_, BN>(smem + IA::BYTES, rb, tid);
+  __syncthreads();
+
+  for (int t = 0; t < nt; ++t) {
+    char* sa = smem + (t & 1) * STAGE;
+    char* sb = sa + IA::BYTES;
+    if (t + 1 < nt) {
+      stage_load<T, AK, BM>(ra, A, lda, m0, (t + 1) * IA::BK, tid);
+      stage_load<T, BK_, BN>(rb, B, ldb, n0, (t + 1) * IA::BK, tid);
+    }
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 fa[MI], fb[NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) fa[i] = frag_bf16<AK, BM>(sa, wm * 16 * MI + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) fb[j] = frag_bf16<BK_, BN>(sb, wn * 16 * NI + j * 16, kk, lane);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int kc = 0; kc < 2; ++kc) {
+        floatx4 fa[MI], fb[NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) fa[i] = frag_f32<AK, BM>(sa, wm * 16 * MI + i * 16, kc, lane);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) fb[j] = frag_f32<BK_, BN>(sb, wn * 16 * NI + j * 16, kc, lane);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (t + 1 < nt) {
+      char* na = smem + ((t + 1) & 1) * STAGE;
+      stage_store<T, AK, BM>(na, ra, tid);
+      stage_store<T, BK_, BN>(na + IA::BYTES, rb, tid);
+    }
+    __syncthreads();
+  }
+
+  // ===================== epilogue, register phase ==========================
+  const int g = lane >> 4, c = lane & 15;
+  const int rw = m0 + wm * 16 * MI;  // first row of this wave
+  const int cw = n0 + wn * 16 * NI;  // first col of this wave
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int col = cw + j * 16 + c;
+    const bool cvalid = col < ep.N;
+    float bias = 0.f, sc = 1.f, sh = 0.f;
+    if (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_MSE || EPI == GEMM_EPI_SCORE) {
+      if (ep.bias) bias = ep.bias[col];
+      if (ep.bn_scale) { sc = ep.bn_scale[col]; sh = ep.bn_shift[col]; }
+    }
+    float s1[MI / 2], s2[MI / 2];
+#pragma unroll
+    for (int p = 0; p < MI / 2; ++p) { s1[p] = 0.f; s2[p] = 0.f; }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rw + i * 16 + 4 * g + r;
+        const bool valid = cvalid && row < ep.M;
+        float v = acc[i][j][r];
+        if (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_SCORE) {
+          v = apply_act(v + bias, ep.act, ep.slope) * sc + sh;
+          v = valid ? v : 0.f;
+          s1[i >> 1] += v;
+        } else if (EPI == GEMM_EPI_MSE) {
+          float d = 0.f;
+          if (valid) d = v + bias - ep.target[(size_t)(row % ep.tmod) * ep.ldt + col];
+          v = ep.gscale * d;
+          s1[i >> 1] += v;
+          s2[i >> 1] += d * d;
+        } else if (EPI == GEMM_EPI_BWD_DATA) {
+          v = valid ? v : 0.f;
+          s1[i >> 1] += v;
+        }
+        acc[i][j][r] = v;
+      }
+    }
+    if (ep.part) {
+#pragma unroll
+      for (int p = 0; p < MI / 2; ++p) {
+        float a1 = s1[p];
+        a1 += __shfl_xor(a1, 16);
+        a1 += __shfl_xor(a1, 32);
+        const int crow = rw + p * 32;
+        const int chunk = crow / MMAD_PART_ROWS;
+        float* part = ep.part + (size_t)chunk * 2 * ep.ldpart;
+        if (EPI == GEMM_EPI_FWD) {
+          // Welford partial: mean and M2 of the valid rows of this 32-row chunk
+          int cnt = ep.M - crow;
+          cnt = cnt < 0 ? 0 : (cnt > 32 ? 32 : cnt);
+          const float mean = cnt > 0 ? a1 / (float)cnt : 0.f;
+          float q = 0.f;
+#pragma unroll
+          for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int row = crow + ii * 16 + 4 * g + r;
+              const float dv = acc[2 * p + ii][j][r] - mean;
+              q += (row < ep.M) ? dv * dv : 0.f;
+            }
+          q += __shfl_xor(q, 16);
+          q += __shfl_xor(q, 32);
+          if (g == 0) { part[col] = mean; part[ep.ldpart + col] = q; }
+        } else if (EPI == GEMM_EPI_MSE) {
+          float a2 = s2[p];
+          a2 += __shfl_xor(a2, 16);
+          a2 += __shfl_xor(a2, 32);
+          if (g == 0) { part[col] = a1; part[ep.ldpart + col] = a2; }
+        } else if (EPI == GEMM_EPI_BWD_DATA) {
+          if (g == 0) part[col] = a1;
+        }
+      }
+    }
+  }
+
+  // ===================== epilogue, LDS-staged coalesced store ===============
+  __syncthreads();  // main-loop LDS no longer read
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = wm * 16 * MI + i * 16 + 4 * g + r;
+        const int cl = wn * 16 * NI + j * 16 + c;
+        *(TO*)(smem + rl * OSTRIDE + cl * (int)sizeof(TO)) = from_f32<TO>(acc[i][j][r]);
+      }
+  __syncthreads();
+  constexpr int CPR = BN * (int)sizeof(TO) / 16;  // 16-byte chunks per output row
+  constexpr int EPC = 16 / (int)sizeof(TO);
+  constexpr int ITERS = BM * CPR / 256;
+  TO* out = (TO*)ep.out;
+#pragma unroll
+  for (int it = 0; it < ITERS; ++it) {
+    const int idx = it * 256 + tid;
+    const int rl = idx / CPR, ch = idx % CPR;
+    const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
+    const int row = m0 + rl;
+    const int col = n0 + ch * EPC;
+    *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
+    if (EPI == GEMM_EPI_SCORE) {
+      const TO* ref = (const TO*)ep.ref + (size_t)row * ep.ldref + col;
+      const uint4v rv = *(const uint4v*)ref;
+      const TO* pv = (const TO*)&v;
+      const TO* pr = (const TO*)&rv;
+      float sq = 0.f;
+      float dd[EPC];
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        dd[e] = to_f32<TO>(pv[e]) - to_f32<TO>(pr[e]);
+        sq += dd[e] * dd[e];
+      }
+      if (ep.diff && row < ep.M) {
+        float* dp = ep.diff + (size_t)row * ep.lddiff + col;
+#pragma unroll
+        for (int e = 0; e < EPC; ++e)
+          if (col + e < ep.N) dp[e] = dd[e];
+      }
+#pragma unroll
+      for (int o = 1; o < CPR; o <<= 1) sq += __shfl_xor(sq, o);
+      if (ch == 0) ep.rowsq[(size_t)blockIdx.x * ep.ldrow + row] = sq;
+    }
+  }
+}
+
+// -------------------------------------------------------------------------
+// host-side launch
+// -------------------------------------------------------------------------
+template <typename T, typename TO, bool AK, bool BK_, int EPI>
+static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np, int K,
+                        const GemmEpi& ep, int tile, hipStream_t s) {
+  dim3 blk(256);
+  switch (tile) {
+    case 0: {  // 128 x 128
+      dim3 grd(Np / 128, Mp / 128);
+      mmad_gemm_kernel<T, TO, AK, BK_, 4, 4, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep);
+      break;
+    }
+    case 1: {  // 64 x 128
+      dim3 grd(Np / 128, Mp / 64);
+      mmad_gemm_kernel<T, TO, AK, BK_, 2, 4, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep);
+      break;
+    }
+    default: {  // 64 x 64
+      dim3 grd(Np / 64, Mp / 64);
+      mmad_gemm_kernel<T, TO, AK, BK_, 2, 2, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep);
+      break;
+    }
+  }
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_pick_tile(int Mp, int Np, int epi) {
+  const int env = mmad_tile_override();
+  if (env >= 0) return env;
+  // the score epilogue reduces rows over the tile width; keep it 128 wide
+  if ((Mp / 128) * (Np / 128) >= 240) return 0;
+  if (epi == GEMM_EPI_SCORE || (Mp / 64) * (Np / 128) >= 200) return 1;
+  return 2;
+}
+
+int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,
+                       int Np, int K, const GemmEpi& ep, hipStream_t s) {
+  MMAD_CHECK_ARG(Mp % 128 == 0 && Np % 128 == 0 && K % 128 == 0,
+                 "gemm: padded dims must be multiples of 128 (Mp=%d Np=%d K=%d)", Mp, Np, K);
+  MMAD_CHECK_ARG(Mp > 0 && Np > 0 && K > 0, "gemm: empty problem");
+  const int tile = mmad_pick_tile(Mp, Np, epi);
+  if (epi == GEMM_EPI_SCORE) MMAD_CHECK_ARG(tile != 2, "score epilogue needs a 128-wide tile");
+#define MMAD_DISPATCH_T(T)                                                                        \
+  switch (epi) {                                                                                  \
+    case GEMM_EPI_FWD:                                                                            \
+      return launch_tiled<T, T, true, true, GEMM_EPI_FWD>((const T*)A, lda, (const T*)B, ldb, Mp,  \
+                                                          Np, K, ep, tile, s);                    \
+    case GEMM_EPI_MSE:                                                                            \
+      return launch_tiled<T, T, true, true, GEMM_EPI_MSE>((const T*)A, lda, (const T*)B, ldb, Mp,  \
+                                                          Np, K, ep, tile, s);                    \
+    case GEMM_EPI_SCORE:                                                                          \
+      return launch_tiled<T, T, true, true, GEMM_EPI_SCORE>((const T*)A, lda, (const T*)B, ldb,    \
+                                                            Mp, Np, K, ep, tile, s);              \
+    case GEMM_EPI_BWD_DATA:                                                                       \
+      return launch_tiled<T, T, true, false, GEMM_EPI_BWD_DATA>((const T*)A, lda, (const T*)B,     \
+                                                                ldb, Mp, Np, K, ep, tile, s);     \
+    case GEMM_EPI_BWD_WEIGHT:                                                                     \
+      return launch_tiled<T, float, false, false, GEMM_EPI_BWD_WEIGHT>(                            \
+          (const T*)A, lda, (const T*)B, ldb, Mp, Np, K, ep, tile, s);                            \
+    default: mmad_set_error("gemm: bad epilogue %d", epi); return MMAD_EINVAL;                   \
+  }
+  if (dtype == MMAD_BF16) {
+    MMAD_DISPATCH_T(bf16)
+  } else if (dtype == MMAD_F32) {
+    MMAD_DISPATCH_T(float)
+  }
+#undef MMAD_DISPATCH_T
+  mmad_set_error("gemm: bad dtype %d", dtype);
+  return MMAD_EINVAL;
+}

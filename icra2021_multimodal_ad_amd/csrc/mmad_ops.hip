@@ -1,0 +1,695 @@
+// Column-slab kernels around the MFMA GEMMs: BatchNorm1d train/eval,
+// BN+activation backward, bias/loss reductions, input packing, Adam, and the
+// variational-information-bottleneck reparameterisation.  All HBM-bound:
+// 16-byte accesses per lane, one 64-column x 128-row slab per 256-thread
+// block (grid = Np/64 x Mp/128, thousands of blocks at the bench shapes).
+#include "mmad_common.h"
+#include "mmad_ops.h"
+
+#define SLAB_COLS 64
+#define SLAB_ROWS 128
+
+namespace {
+
+template <typename T> struct Vec { static constexpr int N = 16 / sizeof(T); };
+
+// ---------------------------------------------------------------------------
+// BN eval affine: scale = gamma/sqrt(rv+eps), shift = beta - rm*scale
+__global__ void bn_eval_affine_k(int N, int Np, const float* gamma, const float* beta,
+                                 const float* rm, const float* rv, float eps, float* scale,
+                                 float* shift) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= Np) return;
+  if (j < N) {
+    float s = gamma[j] * rsqrtf(rv[j] + eps);
+    scale[j] = s;
+    shift[j] = beta[j] - rm[j] * s;
+  } else {
+    scale[j] = 0.f;
+    shift[j] = 0.f;
+  }
+}
+
+// Merge the GEMM-epilogue Welford partials of 64 columns -> (mean, var) in LDS.
+__device__ void merge_welford(int M, int nparts, const float* stats, int Np, int n0, float* s_mean,
+                              float* s_var) {
+  __shared__ float pm[4][SLAB_COLS], pq[4][SLAB_COLS], pn[4][SLAB_COLS];
+  const int tid = threadIdx.x, c = tid & 63, grp = tid >> 6;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (int i = grp; i < nparts; i += 4) {
+    int cnt = M - i * MMAD_PART_ROWS;
+    cnt = cnt < 0 ? 0 : (cnt > MMAD_PART_ROWS ? MMAD_PART_ROWS : cnt);
+    if (cnt == 0) continue;
+    const float mb = stats[(size_t)i * 2 * Np + n0 + c];
+    const float qb = stats[((size_t)i * 2 + 1) * Np + n0 + c];
+    const float nb = (float)cnt;
+    const float nn = n + nb;
+    const float d = mb - mean;
+    mean += d * (nb / nn);
+    m2 += qb + d * d * (n * nb / nn);
+    n = nn;
+  }
+  pm[grp][c] = mean;
+  pq[grp][c] = m2;
+  pn[grp][c] = n;
+  __syncthreads();
+  if (tid < SLAB_COLS) {
+    float n1 = 0.f, mu = 0.f, q = 0.f;
+    for (int g = 0; g < 4; ++g) {
+      const float nb = pn[g][tid];
+      if (nb == 0.f) continue;
+      const float nn = n1 + nb;
+      const float d = pm[g][tid] - mu;
+      mu += d * (nb / nn);
+      q += pq[g][tid] + d * d * (n1 * nb / nn);
+      n1 = nn;
+    }
+    s_mean[tid] = mu;
+    s_var[tid] = n1 > 0.f ? q / n1 : 0.f;  // biased variance (normalisation)
+  }
+  __syncthreads();
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_train_apply_k(int M, int N, int Np, const T* __restrict__ a,
+                                                        const float* __restrict__ stats, int nparts,
+                                                        const float* gamma, const float* beta,
+                                                        float* rmean, float* rvar, float momentum,
+                                                        float eps, float* save_mean,
+                                                        float* save_rstd, T* __restrict__ y) {
+  __shared__ float s_mean[SLAB_COLS], s_var[SLAB_COLS], s_sc[SLAB_COLS], s_sh[SLAB_COLS];
+  const int n0 = blockIdx.x * SLAB_COLS, r0 = blockIdx.y * SLAB_ROWS, tid = threadIdx.x;
+  merge_welford(M, nparts, stats, Np, n0, s_mean, s_var);
+  if (tid < SLAB_COLS) {
+    const int col = n0 + tid;
+    float sc = 0.f, sh = 0.f;
+    if (col < N) {
+      const float rstd = rsqrtf(s_var[tid] + eps);
+      sc = gamma[col] * rstd;
+      sh = beta[col] - s_mean[tid] * sc;
+      if (blockIdx.y == 0) {
+        save_mean[col] = s_mean[tid];
+        save_rstd[col] = rstd;
+        const float unb = M > 1 ? s_var[tid] * (float)M / (float)(M - 1) : s_var[tid];
+        rmean[col] = (1.f - momentum) * rmean[col] + momentum * s_mean[tid];
+        rvar[col] = (1.f - momentum) * rvar[col] + momentum * unb;
+      }
+    } else if (blockIdx.y == 0) {
+      save_mean[col] = 0.f;
+      save_rstd[col] = 0.f;
+    }
+    s_sc[tid] = sc;
+    s_sh[tid] = sh;
+  }
+  __syncthreads();
+  constexpr int V = Vec<T>::N;
+  constexpr int CPR = SLAB_COLS / V;
+  for (int idx = tid; idx < SLAB_ROWS * CPR; idx += 256) {
+    const int rl = idx / CPR, ch = idx % CPR;
+    const int row = r0 + rl;
+    const size_t off = (size_t)row * Np + n0 + ch * V;
+    uint4v raw = *(const uint4v*)(a + off);
+    T* e = (T*)&raw;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float v = to_f32<T>(e[k]) * s_sc[ch * V + k] + s_sh[ch * V + k];
+      e[k] = from_f32<T>(row < M ? v : 0.f);
+    }
+    *(uint4v*)(y + off) = raw;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// BN(train) + activation backward.  Pass 1: per-slab partial sums of dy and
+// dy*xhat.  Pass 2: finalise dgamma/dbeta, dz, and db partials.
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_k(int M, int Np, const T* __restrict__ dy,
+                                                       const T* __restrict__ a,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd,
+                                                       float* __restrict__ part) {
+  constexpr int V = Vec<T>::N;
+  constexpr int CPR = SLAB_COLS / V;
+  constexpr int RG = 256 / CPR;  // row groups
+  __shared__ float s1[RG][SLAB_COLS], s2[RG][SLAB_COLS];
+  const int n0 = blockIdx.x * SLAB_COLS, r0 = blockIdx.y * SLAB_ROWS, tid = threadIdx.x;
+  const int ch = tid % CPR, rg = tid / CPR;
+  float acc1[V], acc2[V], mu[V], rs[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    acc1[k] = 0.f;
+    acc2[k] = 0.f;
+    mu[k] = mean[n0 + ch * V + k];
+    rs[k] = rstd[n0 + ch * V + k];
+  }
+  for (int rl = rg; rl < SLAB_ROWS; rl += RG) {
+    const int row = r0 + rl;
+    if (row >= M) break;
+    const size_t off = (size_t)row * Np + n0 + ch * V;
+    uint4v rd = *(const uint4v*)(dy + off);
+    uint4v ra = *(const uint4v*)(a + off);
+    const T* pd = (const T*)&rd;
+    const T* pa = (const T*)&ra;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float d = to_f32<T>(pd[k]);
+      acc1[k] += d;
+      acc2[k] += d * (to_f32<T>(pa[k]) - mu[k]) * rs[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    s1[rg][ch * V + k] = acc1[k];
+    s2[rg][ch * V + k] = acc2[k];
+  }
+  __syncthreads();
+  if (tid < SLAB_COLS) {
+    float t1 = 0.f, t2 = 0.f;
+    for (int g = 0; g < RG; ++g) { t1 += s1[g][tid]; t2 += s2[g][tid]; }
+    part[((size_t)blockIdx.y * 2) * Np + n0 + tid] = t1;
+    part[((size_t)blockIdx.y * 2 + 1) * Np + n0 + tid] = t2;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int M, int N, int Np,
+                                                      int nparts, const T* __restrict__ dy,
+                                                      const T* __restrict__ a,
+                                                      const float* __restrict__ mean,
+                                                      const float* __restrict__ rstd,
+                                                      const float* __restrict__ gamma,
+                                                      const float* __restrict__ part,
+                                                      T* __restrict__ dz, float* dgamma,
+                                                      float* dbeta, float* dbpart) {
+  constexpr int V = Vec<T>::N;
+  constexpr int CPR = SLAB_COLS / V;
+  constexpr int RG = 256 / CPR;
+  __shared__ float s_db[SLAB_COLS], s_dg[SLAB_COLS];
+  __shared__ float s_red[RG][SLAB_COLS];
+  const int n0 = blockIdx.x * SLAB_COLS, r0 = blockIdx.y * SLAB_ROWS, tid = threadIdx.x;
+  if (tid < SLAB_COLS) {
+    float t1 = 0.f, t2 = 0.f;
+    for (int i = 0; i < nparts; ++i) {
+      t1 += part[((size_t)i * 2) * Np + n0 + tid];
+      t2 += part[((size_t)i * 2 + 1) * Np + n0 + tid];
+    }
+    const int col = n0 + tid;
+    if (col >= N) { t1 = 0.f; t2 = 0.f; }
+    s_db[tid] = t1;
+    s_dg[tid] = t2;
+    if (blockIdx.y == 0) { dbeta[col] = t1; dgamma[col] = t2; }
+  }
+  __syncthreads();
+  const int ch = tid % CPR, rg = tid / CPR;
+  float mu[V], rs[V], cf[V], dbv[V], dgv[V], accb[V];
+  const float invM = 1.f / (float)M;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int col = n0 + ch * V + k;
+    mu[k] = mean[col];
+    rs[k] = rstd[col];
+    cf[k] = col < N ? gamma[col] * rs[k] * invM : 0.f;
+    dbv[k] = s_db[ch * V + k];
+    dgv[k] = s_dg[ch * V + k];
+    accb[k] = 0.f;
+  }
+  for (int rl = rg; rl < SLAB_ROWS; rl += RG) {
+    const int row = r0 + rl;
+    const size_t off = (size_t)row * Np + n0 + ch * V;
+    uint4v rd = *(const uint4v*)(dy + off);
+    uint4v ra = *(const uint4v*)(a + off);
+    const T* pd = (const T*)&rd;
+    const T* pa = (const T*)&ra;
+    uint4v ro;
+    T* po = (T*)&ro;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float av = to_f32<T>(pa[k]);
+      const float xh = (av - mu[k]) * rs[k];
+      float da = cf[k] * ((float)M * to_f32<T>(pd[k]) - dbv[k] - xh * dgv[k]);
+      float d = da * act_grad_from_out(av, act, slope);
+      d = row < M ? d : 0.f;
+      const T dt = from_f32<T>(d);
+      po[k] = dt;
+      accb[k] += to_f32<T>(dt);
+    }
+    *(uint4v*)(dz + off) = ro;
+  }
+#pragma unroll
+  for (int k = 0; k < V; ++k) s_red[rg][ch * V + k] = accb[k];
+  __syncthreads();
+  if (tid < SLAB_COLS) {
+    float t = 0.f;
+    for (int g = 0; g < RG; ++g) t += s_red[g][tid];
+    dbpart[(size_t)blockIdx.y * Np + n0 + tid] = t;
+  }
+}
+
+// column sums of a packed matrix -> partials [Mp/128][Np]
+template <typename T>
+__global__ __launch_bounds__(256) void matrix_colsum_k(int M, int Np, const T* __restrict__ x,
+                                                       float* __restrict__ part) {
+  constexpr int V = Vec<T>::N;
+  constexpr int CPR = SLAB_COLS / V;
+  constexpr int RG = 256 / CPR;
+  __shared__ float s_red[RG][SLAB_COLS];
+  const int n0 = blockIdx.x * SLAB_COLS, r0 = blockIdx.y * SLAB_ROWS, tid = threadIdx.x;
+  const int ch = tid % CPR, rg = tid / CPR;
+  float acc[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) acc[k] = 0.f;
+  for (int rl = rg; rl < SLAB_ROWS; rl += RG) {
+    const int row = r0 + rl;
+    if (row >= M) break;
+    uint4v r = *(const uint4v*)(x + (size_t)row * Np + n0 + ch * V);
+    const T* p = (const T*)&r;
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] += to_f32<T>(p[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < V; ++k) s_red[rg][ch * V + k] = acc[k];
+  __syncthreads();
+  if (tid < SLAB_COLS) {
+    float t = 0.f;
+    for (int g = 0; g < RG; ++g) t += s_red[g][tid];
+    part[(size_t)blockIdx.y * Np + n0 + tid] = t;
+  }
+}
+
+__global__ void colsum_k(int n_parts, int N, int Np, const float* __restrict__ part,
+                         int stride, float scale, float* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= Np) return;
+  float t = 0.f;
+  if (j < N)
+    for (int i = 0; i < n_parts; ++i) t += part[(size_t)i * stride + j];
+  out[j] = scale * t;
+}
+
+__global__ __launch_bounds__(1024) void sum2d_k(int rows, int cols, const float* __restrict__ x,
+                                                int64_t ld, float scale, float* out, int accumulate) {
+  __shared__ float red[16];
+  float t = 0.f;
+  const int64_t n = (int64_t)rows * cols;
+  for (int64_t i = threadIdx.x; i < n; i += 1024) {
+    const int64_t r = i / cols, c = i % cols;
+    t += x[r * ld + c];
+  }
+  t = wave_sum(t);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int i = 0; i < 16; ++i) s += red[i];
+    out[0] = (accumulate ? out[0] : 0.f) + scale * s;
+  }
+}
+
+template <typename T>
+__global__ void pack_input_k(int M, int K, int Mp, int Kp, const float* __restrict__ x, int ldx,
+                             T* __restrict__ out) {
+  constexpr int V = Vec<T>::N;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cpr = Kp / V;
+  if (idx >= (int64_t)Mp * cpr) return;
+  const int row = (int)(idx / cpr), c0 = (int)(idx % cpr) * V;
+  uint4v r;
+  T* p = (T*)&r;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int col = c0 + k;
+    p[k] = from_f32<T>((row < M && col < K) ? x[(size_t)row * ldx + col] : 0.f);
+  }
+  *(uint4v*)(out + (size_t)row * Kp + c0) = r;
+}
+
+template <typename T>
+__global__ void unpack_k(int M, int N, int Np, const T* __restrict__ y, float* __restrict__ out,
+                         int ldo) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)M * N) return;
+  const int row = (int)(idx / N), col = (int)(idx % N);
+  out[(size_t)row * ldo + col] = to_f32<T>(y[(size_t)row * Np + col]);
+}
+
+template <typename T>
+__global__ void sse_k(int M, int N, int Np, const T* __restrict__ y, const float* __restrict__ x,
+                      int ldx, float* __restrict__ part) {
+  __shared__ float red[4];
+  float t = 0.f;
+  const int64_t n = (int64_t)M * N;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int row = (int)(i / N), col = (int)(i % N);
+    const float d = to_f32<T>(y[(size_t)row * Np + col]) - x[(size_t)row * ldx + col];
+    t += d * d;
+  }
+  t = wave_sum(t);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// ---------------------------------------------------------------------------
+// Adam (torch.optim.Adam, single-tensor formula) over a flat buffer
+__global__ __launch_bounds__(256) void adam_k(int64_t n, float* __restrict__ p,
+                                              const float* __restrict__ g, float* __restrict__ m,
+                                              float* __restrict__ v, float b1, float b2, float eps,
+                                              float step_size, float bc2_sqrt, bf16* shadow,
+                                              int64_t n_shadow) {
+  const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i4 >= n) return;
+  if (i4 + 4 <= n) {
+    floatx4 pp = *(floatx4*)(p + i4), gg = *(const floatx4*)(g + i4);
+    floatx4 mm = *(floatx4*)(m + i4), vv = *(floatx4*)(v + i4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      mm[k] = b1 * mm[k] + (1.f - b1) * gg[k];
+      vv[k] = b2 * vv[k] + (1.f - b2) * gg[k] * gg[k];
+      const float denom = sqrtf(vv[k]) / bc2_sqrt + eps;
+      pp[k] = pp[k] - step_size * (mm[k] / denom);
+    }
+    *(floatx4*)(p + i4) = pp;
+    *(floatx4*)(m + i4) = mm;
+    *(floatx4*)(v + i4) = vv;
+    if (shadow && i4 < n_shadow) {
+      bf16x4 s;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s[k] = (bf16)pp[k];
+      *(bf16x4*)(shadow + i4) = s;
+    }
+  } else {
+    for (int64_t i = i4; i < n; ++i) {
+      float mm = b1 * m[i] + (1.f - b1) * g[i];
+      float vv = b2 * v[i] + (1.f - b2) * g[i] * g[i];
+      m[i] = mm;
+      v[i] = vv;
+      p[i] = p[i] - step_size * (mm / (sqrtf(vv) / bc2_sqrt + eps));
+      if (shadow && i < n_shadow) shadow[i] = (bf16)p[i];
+    }
+  }
+}
+
+__global__ void to_bf16_k(int64_t n, const float* __restrict__ x, bf16* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = (bf16)x[i];
+}
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 counter-based RNG -> N(0,1) via Box-Muller
+__device__ __forceinline__ void philox_round(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
+  const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+  const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+  const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+  const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+  c[0] = hi1 ^ c[1] ^ k0;
+  c[1] = lo1;
+  c[2] = hi0 ^ c[3] ^ k1;
+  c[3] = lo0;
+}
+__device__ __forceinline__ float philox_normal(uint64_t seed, uint64_t offset, uint64_t idx) {
+  uint32_t c[4] = {(uint32_t)idx, (uint32_t)(idx >> 32), (uint32_t)offset, (uint32_t)(offset >> 32)};
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    philox_round(c, k0, k1);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  const float u1 = ((c[0] >> 8) + 1) * (1.0f / 16777217.0f);  // (0,1]
+  const float u2 = (c[1] >> 8) * (1.0f / 16777216.0f);
+  return sqrtf(-2.f * __logf(u1)) * __cosf(6.2831853071795864f * u2);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void vib_fwd_k(int B, int btl, int k, const T* __restrict__ enc,
+                                                 int ld_enc, const float* __restrict__ eps,
+                                                 float* __restrict__ eps_out, uint64_t seed,
+                                                 uint64_t offset, int det, T* __restrict__ z,
+                                                 int ld_z, int Mpz, float* kl_part) {
+  // one thread per element of the packed z buffer [Mpz][ld_z]; rows < B also
+  // contribute the KL term of their (mu, logvar) pair.
+  __shared__ float red[4];
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)Mpz * ld_z;
+  float kl = 0.f;
+  if (idx < total) {
+    const int row = (int)(idx / ld_z), c = (int)(idx % ld_z);
+    float out = 0.f;
+    if (c < btl && row < k * B) {
+      const int kk = row / B, b = row % B;
+      const float mu = to_f32<T>(enc[(size_t)b * ld_enc + c]);
+      const float lv = to_f32<T>(enc[(size_t)b * ld_enc + btl + c]);
+      if (det) {
+        out = mu;
+      } else {
+        const size_t ei = ((size_t)kk * B + b) * btl + c;
+        const float e = eps ? eps[ei] : philox_normal(seed, offset, ei);
+        if (eps_out) eps_out[ei] = e;
+        out = e * __expf(0.5f * lv) + mu;
+      }
+      if (kk == 0 && kl_part) kl = -0.5f * (1.f + lv - mu * mu - __expf(lv));
+    }
+    z[idx] = from_f32<T>(out);
+  }
+  if (kl_part) {
+    kl = wave_sum(kl);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = kl;
+    __syncthreads();
+    if (threadIdx.x == 0) kl_part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void vib_bwd_k(int B, int btl, int k, const T* __restrict__ enc,
+                                                 int ld_enc, const float* __restrict__ eps,
+                                                 const T* __restrict__ dz, int ld_dz, float beta,
+                                                 T* __restrict__ denc, int ld_denc, int Mpe) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)Mpe * ld_denc) return;
+  const int b = (int)(idx / ld_denc), c = (int)(idx % ld_denc);
+  float out = 0.f;
+  if (b < B && c < 2 * btl) {
+    const int cc = c < btl ? c : c - btl;
+    const float mu = to_f32<T>(enc[(size_t)b * ld_enc + cc]);
+    const float lv = to_f32<T>(enc[(size_t)b * ld_enc + btl + cc]);
+    if (c < btl) {
+      float s = 0.f;
+      for (int kk = 0; kk < k; ++kk) s += to_f32<T>(dz[((size_t)kk * B + b) * ld_dz + cc]);
+      out = s + beta * mu;
+    } else {
+      const float sig = __expf(0.5f * lv);
+      float s = 0.f;
+      for (int kk = 0; kk < k; ++kk)
+        s += to_f32<T>(dz[((size_t)kk * B + b) * ld_dz + cc]) * eps[((size_t)kk * B + b) * btl + cc];
+      out = 0.5f * sig * s + 0.5f * beta * (__expf(lv) - 1.f);
+    }
+  }
+  denc[idx] = from_f32<T>(out);
+}
+
+}  // namespace
+
+// ===========================================================================
+// host launchers
+// ===========================================================================
+static inline int nblk(int64_t n, int b) { return (int)((n + b - 1) / b); }
+
+int mmad_bn_eval_affine(int N, int Np, const float* gamma, const float* beta, const float* rm,
+                        const float* rv, float eps, float* scale, float* shift, void* stream) {
+  MMAD_CHECK_ARG(N >= 0 && Np >= N, "bn_eval_affine: bad sizes");
+  if (Np == 0) return MMAD_OK;
+  bn_eval_affine_k<<<nblk(Np, 256), 256, 0, (hipStream_t)stream>>>(N, Np, gamma, beta, rm, rv, eps,
+                                                                    scale, shift);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_bn_train_apply(int dtype, int M, int N, int Mp, int Np, const void* a, const float* stats,
+                        const float* gamma, const float* beta, float* running_mean,
+                        float* running_var, float momentum, float eps, float* save_mean,
+                        float* save_rstd, void* y, void* stream) {
+  MMAD_CHECK_ARG(Mp % 128 == 0 && Np % 128 == 0 && M >= 1 && M <= Mp && N <= Np,
+                 "bn_train_apply: bad sizes M=%d Mp=%d N=%d Np=%d", M, Mp, N, Np);
+  dim3 grd(Np / SLAB_COLS, Mp / SLAB_ROWS);
+  const int nparts = Mp / MMAD_PART_ROWS;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMAD_BF16)
+    bn_train_apply_k<bf16><<<grd, 256, 0, s>>>(M, N, Np, (const bf16*)a, stats, nparts, gamma, beta,
+                                               running_mean, running_var, momentum, eps, save_mean,
+                                               save_rstd, (bf16*)y);
+  else
+    bn_train_apply_k<float><<<grd, 256, 0, s>>>(M, N, Np, (const float*)a, stats, nparts, gamma,
+                                                beta, running_mean, running_var, momentum, eps,
+                                                save_mean, save_rstd, (float*)y);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+size_t mmad_bn_act_bwd_ws(int Mp, int Np) { return (size_t)(Mp / SLAB_ROWS) * 2 * Np * sizeof(float); }
+
+int mmad_bn_act_bwd(int dtype, int act, float slope, int M, int N, int Mp, int Np, const void* dy,
+                    const void* a, const float* save_mean, const float* save_rstd,
+                    const float* gamma, void* dz, float* dgamma, float* dbeta, float* db_partials,
+                    void* ws, void* stream) {
+  MMAD_CHECK_ARG(Mp % 128 == 0 && Np % 128 == 0 && M >= 1 && M <= Mp && N <= Np,
+                 "bn_act_bwd: bad sizes");
+  dim3 grd(Np / SLAB_COLS, Mp / SLAB_ROWS);
+  hipStream_t s = (hipStream_t)stream;
+  float* part = (float*)ws;
+  const int nparts = Mp / SLAB_ROWS;
+  if (dtype == MMAD_BF16) {
+    bn_bwd_reduce_k<bf16><<<grd, 256, 0, s>>>(M, Np, (const bf16*)dy, (const bf16*)a, save_mean,
+                                              save_rstd, part);
+    bn_bwd_apply_k<bf16><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const bf16*)dy,
+                                             (const bf16*)a, save_mean, save_rstd, gamma, part,
+                                             (bf16*)dz, dgamma, dbeta, db_partials);
+  } else {
+    bn_bwd_reduce_k<float><<<grd, 256, 0, s>>>(M, Np, (const float*)dy, (const float*)a, save_mean,
+                                               save_rstd, part);
+    bn_bwd_apply_k<float><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const float*)dy,
+                                              (const float*)a, save_mean, save_rstd, gamma, part,
+                                              (float*)dz, dgamma, dbeta, db_partials);
+  }
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_matrix_colsum_partials(int dtype, int M, int Mp, int Np, const void* x, float* part,
+                                void* stream) {
+  dim3 grd(Np / SLAB_COLS, Mp / SLAB_ROWS);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMAD_BF16)
+    matrix_colsum_k<bf16><<<grd, 256, 0, s>>>(M, Np, (const bf16*)x, part);
+  else
+    matrix_colsum_k<float><<<grd, 256, 0, s>>>(M, Np, (const float*)x, part);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_colsum(int n_parts, int N, int Np, const float* partials, int part_stride, float scale,
+                float* out, void* stream) {
+  MMAD_CHECK_ARG(n_parts >= 0 && N <= Np, "colsum: bad sizes");
+  if (Np == 0) return MMAD_OK;
+  colsum_k<<<nblk(Np, 256), 256, 0, (hipStream_t)stream>>>(n_parts, N, Np, partials, part_stride,
+                                                            scale, out);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_sum2d(int rows, int cols, const float* x, int64_t ld, float scale, float* out,
+               int accumulate, void* stream) {
+  MMAD_CHECK_ARG(rows >= 0 && cols >= 0, "sum2d: bad sizes");
+  sum2d_k<<<1, 1024, 0, (hipStream_t)stream>>>(rows, cols, x, ld, scale, out, accumulate);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_sum(int64_t n, const float* x, float scale, float* out, int accumulate, void* stream) {
+  MMAD_CHECK_ARG(n >= 0 && n < (1LL << 31), "sum: bad n");
+  return mmad_sum2d(1, (int)n, x, n, scale, out, accumulate, stream);
+}
+
+int mmad_pack_input(int dtype, int M, int K, int Mp, int Kp, const float* x, int ld_x, void* out,
+                    void* stream) {
+  MMAD_CHECK_ARG(M <= Mp && K <= Kp && Kp % 8 == 0 && ld_x >= K, "pack_input: bad sizes");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMAD_BF16) {
+    const int64_t n = (int64_t)Mp * (Kp / 8);
+    pack_input_k<bf16><<<nblk(n, 256), 256, 0, s>>>(M, K, Mp, Kp, x, ld_x, (bf16*)out);
+  } else {
+    const int64_t n = (int64_t)Mp * (Kp / 4);
+    pack_input_k<float><<<nblk(n, 256), 256, 0, s>>>(M, K, Mp, Kp, x, ld_x, (float*)out);
+  }
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_unpack_output(int dtype, int M, int N, int Np, const void* y, float* out, int ld_out,
+                       void* stream) {
+  MMAD_CHECK_ARG(N <= Np && ld_out >= N, "unpack_output: bad sizes");
+  const int64_t n = (int64_t)M * N;
+  if (n == 0) return MMAD_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMAD_BF16)
+    unpack_k<bf16><<<nblk(n, 256), 256, 0, s>>>(M, N, Np, (const bf16*)y, out, ld_out);
+  else
+    unpack_k<float><<<nblk(n, 256), 256, 0, s>>>(M, N, Np, (const float*)y, out, ld_out);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_sse_partials(int dtype, int M, int N, int Np, const void* y, const float* x, int ldx,
+                      float* part, int nparts, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMAD_BF16)
+    sse_k<bf16><<<nparts, 256, 0, s>>>(M, N, Np, (const bf16*)y, x, ldx, part);
+  else
+    sse_k<float><<<nparts, 256, 0, s>>>(M, N, Np, (const float*)y, x, ldx, part);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_adam(int64_t n, float* p, const float* g, float* m, float* v, float beta1, float beta2,
+              float eps, float step_size, float bc2_sqrt, void* shadow, int64_t n_shadow,
+              void* stream) {
+  MMAD_CHECK_ARG(n >= 0 && n_shadow >= 0 && n_shadow <= n, "adam: bad sizes");
+  if (n == 0) return MMAD_OK;
+  MMAD_CHECK_ARG(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
+                 "adam: buffers must be 16-byte aligned");
+  adam_k<<<nblk((n + 3) / 4, 256), 256, 0, (hipStream_t)stream>>>(
+      n, p, g, m, v, beta1, beta2, eps, step_size, bc2_sqrt, (bf16*)shadow, n_shadow);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_to_bf16(int64_t n, const float* x, void* y, void* stream) {
+  if (n == 0) return MMAD_OK;
+  to_bf16_k<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(n, x, (bf16*)y);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_vib_reparam_fwd(int dtype, int B, int btl, int k, const void* enc_out, int ld_enc,
+                         const float* eps, float* eps_out, uint64_t seed, uint64_t offset,
+                         int deterministic, void* z, int ld_z, float* kl_partial, void* stream) {
+  MMAD_CHECK_ARG(B >= 1 && btl >= 1 && k >= 1 && ld_enc >= 2 * btl && ld_z >= btl,
+                 "vib_reparam_fwd: bad sizes");
+  const int Mpz = mmad_roundup(k * B, MMAD_PAD);
+  const int64_t n = (int64_t)Mpz * ld_z;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMAD_BF16)
+    vib_fwd_k<bf16><<<nblk(n, 256), 256, 0, s>>>(B, btl, k, (const bf16*)enc_out, ld_enc, eps,
+                                                 eps_out, seed, offset, deterministic, (bf16*)z,
+                                                 ld_z, Mpz, kl_partial);
+  else
+    vib_fwd_k<float><<<nblk(n, 256), 256, 0, s>>>(B, btl, k, (const float*)enc_out, ld_enc, eps,
+                                                  eps_out, seed, offset, deterministic, (float*)z,
+                                                  ld_z, Mpz, kl_partial);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int64_t mmad_vib_kl_parts(int B, int k, int ld_z) {
+  const int Mpz = mmad_roundup(k * B, MMAD_PAD);
+  return ((int64_t)Mpz * ld_z + 255) / 256;
+}
+
+int mmad_vib_reparam_bwd(int dtype, int B, int btl, int k, const void* enc_out, int ld_enc,
+                         const float* eps, const void* dz, int ld_dz, float beta_kl,
+                         void* d_enc_out, int ld_denc, float* colsum, void* stream) {
+  MMAD_CHECK_ARG(B >= 1 && btl >= 1 && k >= 1 && ld_denc >= 2 * btl, "vib_reparam_bwd: bad sizes");
+  const int Mpe = mmad_roundup(B, MMAD_PAD);
+  const int64_t n = (int64_t)Mpe * ld_denc;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMAD_BF16)
+    vib_bwd_k<bf16><<<nblk(n, 256), 256, 0, s>>>(B, btl, k, (const bf16*)enc_out, ld_enc, eps,
+                                                 (const bf16*)dz, ld_dz, beta_kl,
+                                                 (bf16*)d_enc_out, ld_denc, Mpe);
+  else
+    vib_bwd_k<float><<<nblk(n, 256), 256, 0, s>>>(B, btl, k, (const float*)enc_out, ld_enc, eps,
+                                                  (const float*)dz, ld_dz, beta_kl,
+                                                  (float*)d_enc_out, ld_denc, Mpe);
+  MMAD_LAUNCH_CHECK();
+  if (colsum) return mmad_matrix_colsum_partials(dtype, B, Mpe, ld_denc, d_enc_out, colsum, stream);
+  return MMAD_OK;
+}

@@ -1,0 +1,250 @@
+"""FCLayer / FCModule / Activation / Loss / variational_info_bottleneck.
+
+Mirrors the reference's module surface (names, constructor arguments, error
+behaviour, ``layer_list``, state_dict keys) so callers are drop-in:
+
+* Activation  -- modules/activation.py:20-45
+* Loss        -- modules/loss.py:20-53
+* FCLayer     -- layers/fc_layer.py:23-48 (Linear -> Activation -> BN, dropout)
+* FCModule    -- modules/fc_module.py:23-61 (layer_list + registered ``net``)
+* variational_info_bottleneck -- decorators/variational_info_bottleneck.py:19-42
+
+Parameters are held in ``nn.Linear`` / ``nn.BatchNorm1d`` containers purely so
+the state_dict layout is byte-for-byte the reference's; their torch
+``forward`` is never called.  FCLayer.forward runs the fused HIP kernel
+(``mmad_fc_fwd``: GEMM + bias + activation + BatchNorm) through the C-ABI;
+there is no CPU / eager fallback.
+"""
+import torch
+from torch import nn
+
+from . import _native
+from ._native import call, ptr, stream_ptr, pad
+
+ACT_NAMES = ("sigmoid", "logsigmoid", "softmax", "logsoftmax", "tanh", "relu", "leakyrelu")
+LEAKY_SLOPE = 0.2  # modules/activation.py:37-38
+
+
+class Activation(nn.Module):
+    """modules/activation.py:20-45.  ``name`` selects the nonlinearity; unknown
+    names (incl. None) are the identity.  Element-wise activations are fused
+    into the FC kernel epilogue; softmax/logsoftmax/logsigmoid exist for
+    surface parity and run through torch when used standalone."""
+
+    def __init__(self, act):
+        super().__init__()
+        self.name = act if act in ACT_NAMES else None
+        if act == "sigmoid":
+            self.act = nn.Sigmoid()
+        elif act == "logsigmoid":
+            self.act = nn.LogSigmoid()
+        elif act == "softmax":
+            self.act = nn.Softmax(dim=-1)
+        elif act == "logsoftmax":
+            self.act = nn.LogSoftmax(dim=-1)
+        elif act == "tanh":
+            self.act = nn.Tanh()
+        elif act == "relu":
+            self.act = nn.ReLU()
+        elif act == "leakyrelu":
+            self.act = nn.LeakyReLU(LEAKY_SLOPE)
+        else:
+            self.act = None
+
+    @property
+    def fusable(self):
+        return self.name in (None, "leakyrelu", "relu", "sigmoid", "tanh")
+
+    def forward(self, x):
+        if self.act is not None:
+            return self.act(x)
+        return x
+
+
+class Loss(nn.Module):
+    """modules/loss.py:20-53 (same names/reductions).  The AE's
+    ``Loss('mse', reduction='sum')`` is fused into the last decoder GEMM by the
+    native train step; called directly it evaluates with torch ops."""
+
+    def __init__(self, loss, weight=None, reduction="sum"):
+        self.reduction = reduction
+        super().__init__()
+        self.name = loss
+        if loss == "bce":
+            self.loss = nn.BCELoss(weight=weight, reduction=reduction)
+        elif loss == "bce_with_logit":
+            self.loss = nn.BCEWithLogitsLoss(weight=weight, reduction=reduction)
+        elif loss == "mse":
+            self.loss = nn.MSELoss(reduction=reduction)
+        elif loss == "l1":
+            self.loss = nn.L1Loss(reduction=reduction)
+        elif loss == "ce":
+            self.loss = nn.CrossEntropyLoss(weight=weight, reduction=reduction)
+        elif loss == "nll":
+            self.loss = nn.NLLLoss(weight=weight, reduction=reduction)
+        else:
+            self.loss = None
+
+    def is_classification_task(self):
+        return isinstance(self.loss, (nn.NLLLoss, nn.CrossEntropyLoss))
+
+    def forward(self, y_hat, y):
+        if self.loss is not None:
+            if self.is_classification_task():
+                y = y.long()
+            return self.loss(y_hat, y)
+        return y_hat.mean()
+
+
+class FCLayer(nn.Module):
+    """layers/fc_layer.py:23-48: y = BN(act(x W^T + b)) [-> dropout]."""
+
+    def __init__(self, input_size, output_size=1, bias=True, act="relu", bn=False, dropout_p=0):
+        super().__init__()
+        self.layer = nn.Linear(input_size, output_size, bias)
+        self.bn = nn.BatchNorm1d(output_size) if bn else None
+        self.dropout = nn.Dropout(dropout_p) if dropout_p else None
+        self.act = Activation(act) if act else None
+        self.mmad_dtype = "f32"
+
+    @property
+    def act_name(self):
+        return self.act.name if self.act is not None else None
+
+    def forward(self, x):
+        if self.dropout is not None or (self.act is not None and not self.act.fusable) \
+                or self.layer.bias is None:
+            raise NotImplementedError("FCLayer HIP path supports bias=True, element-wise "
+                                      "activations and no dropout (the AE configuration)")
+        shape = x.shape
+        y = fc_layer_forward(self, x.reshape(-1, shape[-1]), self.training)
+        return y.reshape(*shape[:-1], y.shape[-1])
+
+
+def fc_layer_forward(layer, x2, training):
+    """Run one FCLayer through ``mmad_fc_fwd`` (+ ``mmad_bn_train_apply`` in
+    train mode, which also updates the running statistics in place).  Packs
+    operands into the 128-padded layouts the kernels require."""
+    _native.require_gpu(x2)
+    lin, bn = layer.layer, layer.bn
+    dev = x2.device
+    dt = _native.BF16 if layer.mmad_dtype == "bf16" else _native.F32
+    tdt = torch.bfloat16 if dt == _native.BF16 else torch.float32
+    M, K = x2.shape
+    N = lin.out_features
+    Mp, Kp, Np = pad(M), pad(K), pad(N)
+    x2 = x2.float().contiguous()
+    s = stream_ptr()
+    xin = torch.empty((Mp, Kp), device=dev, dtype=tdt)
+    call("mmad_pack_input", dt, M, K, Mp, Kp, ptr(x2), K, ptr(xin), s)
+    w = torch.zeros((Np, Kp), device=dev, dtype=tdt)
+    w[:N, :K] = lin.weight.detach()
+    b = torch.zeros(Np, device=dev)
+    b[:N] = lin.bias.detach()
+    out = torch.empty((Mp, Np), device=dev, dtype=tdt)
+    act = _native.ACT[layer.act_name]
+    if bn is None:
+        call("mmad_fc_fwd", dt, M, N, K, Mp, Np, Kp, ptr(xin), ptr(w), ptr(b), act,
+             LEAKY_SLOPE, None, None, ptr(out), None, s)
+    else:
+        g = torch.zeros(Np, device=dev)
+        be = torch.zeros(Np, device=dev)
+        g[:N] = bn.weight.detach()
+        be[:N] = bn.bias.detach()
+        rm = torch.zeros(Np, device=dev)
+        rv = torch.ones(Np, device=dev)
+        rm[:N] = bn.running_mean
+        rv[:N] = bn.running_var
+        if training:
+            stats = torch.empty((Mp // 32, 2, Np), device=dev)
+            a = torch.empty((Mp, Np), device=dev, dtype=tdt)
+            call("mmad_fc_fwd", dt, M, N, K, Mp, Np, Kp, ptr(xin), ptr(w), ptr(b), act,
+                 LEAKY_SLOPE, None, None, ptr(a), ptr(stats), s)
+            sm = torch.empty(Np, device=dev)
+            sr = torch.empty(Np, device=dev)
+            call("mmad_bn_train_apply", dt, M, N, Mp, Np, ptr(a), ptr(stats), ptr(g), ptr(be),
+                 ptr(rm), ptr(rv), float(bn.momentum), float(bn.eps), ptr(sm), ptr(sr), ptr(out), s)
+            with torch.no_grad():
+                bn.running_mean.copy_(rm[:N])
+                bn.running_var.copy_(rv[:N])
+                bn.num_batches_tracked.add_(1)
+        else:
+            sc = torch.empty(Np, device=dev)
+            sh = torch.empty(Np, device=dev)
+            call("mmad_bn_eval_affine", N, Np, ptr(g), ptr(be), ptr(rm), ptr(rv), float(bn.eps),
+                 ptr(sc), ptr(sh), s)
+            call("mmad_fc_fwd", dt, M, N, K, Mp, Np, Kp, ptr(xin), ptr(w), ptr(b), act,
+                 LEAKY_SLOPE, ptr(sc), ptr(sh), ptr(out), None, s)
+    y = torch.empty((M, N), device=dev)
+    call("mmad_unpack_output", dt, M, N, Np, ptr(out), ptr(y), N, s)
+    return y
+
+
+def reparameterize(mu, logvar, k, stochastic_inference, eps=None, seed=None):
+    """decorators/variational_info_bottleneck.py:22-26,37 on the GPU through
+    ``mmad_vib_reparam_fwd``: z[k,B,btl] = eps*exp(0.5*logvar) + mu, or
+    mu expanded when grad is disabled and stochastic_inference is False."""
+    _native.require_gpu(mu)
+    B, btl = mu.shape
+    det = not (torch.is_grad_enabled() or stochastic_inference)
+    enc = torch.cat([mu, logvar], dim=-1).float().contiguous()
+    Mpz, Kpz = pad(k * B), pad(btl)
+    z = torch.empty((Mpz, Kpz), device=mu.device)
+    if eps is not None:
+        eps = eps.float().contiguous()
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+    call("mmad_vib_reparam_fwd", _native.F32, B, btl, k, ptr(enc), 2 * btl, ptr(eps), None,
+         int(seed), 0, int(det), ptr(z), Kpz, None, stream_ptr())
+    return z[:k * B, :btl].reshape(k, B, btl)
+
+
+def variational_info_bottleneck(forward_fn):
+    """decorators/variational_info_bottleneck.py:19-42: distribution=None ->
+    pass-through; 'normal' -> split mu|logvar, reparameterise k samples."""
+    def decorated_forward(self, x, distribution=None, k=1, stochastic_inference=True, eps=None):
+        output = forward_fn(self, x)
+        if distribution is None:
+            return output
+        elif distribution == "normal":
+            mu, logvar = output.split(output.size(-1) // 2, dim=-1)
+            if k < 1:
+                raise ValueError("k should be >= 1")
+            z = reparameterize(mu, logvar, k, stochastic_inference, eps=eps)
+            return {"z": z, "mu": mu, "logvar": logvar}
+        else:
+            raise NotImplementedError(
+                "Wrong distribution for information bottleneck: {}".format(distribution))
+    return decorated_forward
+
+
+vib = variational_info_bottleneck
+
+
+class FCModule(nn.Module):
+    """modules/fc_module.py:23-61."""
+
+    def __init__(self, input_size, output_size, hidden_sizes=None, use_batch_norm=True,
+                 dropout_p=0, act="leakyrelu", last_act=None):
+        super().__init__()
+        self.layer_list = []
+        if use_batch_norm and dropout_p > 0:
+            raise Exception("Either batch_norm or dropout is allowed, not both")
+        hidden_sizes = list(hidden_sizes or [])
+        layer_sizes = [input_size] + hidden_sizes + [output_size]
+        for idx, (in_size, out_size) in enumerate(zip(layer_sizes[:-1], layer_sizes[1:])):
+            if idx < len(hidden_sizes):
+                layer = FCLayer(input_size=in_size, output_size=out_size, act=act,
+                                bn=use_batch_norm, dropout_p=dropout_p)
+            else:
+                layer = FCLayer(input_size=in_size, output_size=out_size, act=last_act)
+            self.layer_list.append(layer)
+        self.net = nn.Sequential(*self.layer_list)
+
+    @property
+    def widths(self):
+        return [self.layer_list[0].layer.in_features] + [l.layer.out_features for l in self.layer_list]
+
+    @vib
+    def forward(self, x):
+        return self.net(x)

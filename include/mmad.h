@@ -1,0 +1,223 @@
+/*
+ * mmad.h -- C-ABI of the MI355X-native autoencoder train-and-score hot path.
+ *
+ * The reference (Yoo-Youngjae/ICRA2021_multimodal_ad) has no FFI: its hot path
+ * is stock torch modules behind a Python plugin surface.  Each entry point
+ * below names the reference interface it replaces (file:line, relative to the
+ * reference repo root).  The Python mirror of that surface
+ * (icra2021_multimodal_ad_amd/) binds these with ctypes.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Device pointers unless stated.  All
+ *    tensors are caller-owned; nothing here allocates device memory.
+ *  - Packed layouts: every feature and batch dimension is padded to a
+ *    multiple of mmad_pad_granule() (128) with zeros; a [rows][cols] matrix
+ *    has leading dimension = padded cols.  "M/N/K" are the valid sizes,
+ *    "Mp/Np/Kp" the padded ones.
+ *  - dtype selects the activation/weight storage type of the GEMM operands
+ *    (MMAD_F32: exact-fp32 parity path on f32 MFMA; MMAD_BF16: bf16 storage,
+ *    fp32 accumulation).  Gradients, optimizer state, BN statistics and all
+ *    reductions are fp32.
+ *  - Every call returns 0 (MMAD_OK) or a negative status; the message is in
+ *    mmad_last_error_string() (thread-local).  No exceptions cross the ABI.
+ *  - stream is a hipStream_t passed as void* (0 = legacy default stream).
+ */
+#ifndef MMAD_H_
+#define MMAD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMAD_ABI_VERSION 1
+
+enum { MMAD_OK = 0, MMAD_EINVAL = -1, MMAD_EUNSUPPORTED = -2, MMAD_EHIP = -3 };
+enum { MMAD_F32 = 0, MMAD_BF16 = 1 };
+/* modules/activation.py:20-45 (names 'leakyrelu', 'relu', 'sigmoid', 'tanh', None) */
+enum { MMAD_ACT_NONE = 0, MMAD_ACT_LEAKYRELU = 1, MMAD_ACT_RELU = 2, MMAD_ACT_SIGMOID = 3,
+       MMAD_ACT_TANH = 4 };
+
+const char* mmad_last_error_string(void);
+int mmad_abi_version(void);
+int mmad_pad_granule(void);
+
+/* ------------------------------------------------------------------------
+ * Layer operators
+ * ---------------------------------------------------------------------- */
+
+/* FCLayer.forward, layers/fc_layer.py:37-48 (nn.Linear -> Activation -> BN).
+ * y[Mp][Np] = bn_affine(act(x[Mp][Kp] . w[Np][Kp]^T + bias[Np])).
+ * bn_scale/bn_shift (nullable): eval-mode BatchNorm1d as a per-column affine
+ * (see mmad_bn_eval_affine).  stats (nullable, fp32 [Mp/32][2][Np]): per
+ * 32-row chunk Welford (mean, M2) of the post-activation values, consumed by
+ * mmad_bn_train_apply for train-mode BN.  Rows >= M and cols >= N are written 0. */
+int mmad_fc_fwd(int dtype, int M, int N, int K, int Mp, int Np, int Kp, const void* x,
+                const void* w, const float* bias, int act, float slope, const float* bn_scale,
+                const float* bn_shift, void* y, float* stats, void* stream);
+
+/* Last decoder layer fused with Loss('mse', reduction='sum') forward+backward
+ * (modules/loss.py:31-32,47-52; model_builder.py:42):
+ * d = x.w^T + bias - target; dz = grad_scale*d (dtype, [Mp][Np]);
+ * partials fp32 [Mp/32][2][Np] = (sum_rows dz, sum_rows d^2). */
+int mmad_fc_fwd_mse(int dtype, int M, int N, int K, int Mp, int Np, int Kp, const void* x,
+                    const void* w, const float* bias, const float* target, int ld_target,
+                    float grad_scale, void* dz, float* partials, void* stream);
+
+/* Eval-mode FCLayer.forward fused with the per-window squared-diff reduction
+ * of reconstruction_aggregation.py:22-28: y as mmad_fc_fwd (eval affine), and
+ * rowsq[Np/128][Mp] = per-128-column partial sums of (y - ref)^2; diff
+ * (nullable, fp32, ld_diff) receives y - ref for the valid region. */
+int mmad_fc_fwd_score(int dtype, int M, int N, int K, int Mp, int Np, int Kp, const void* x,
+                      const void* w, const float* bias, int act, float slope,
+                      const float* bn_scale, const float* bn_shift, void* y, const void* ref,
+                      float* rowsq, float* diff, int ld_diff, void* stream);
+
+/* BatchNorm1d eval affine (layers/fc_layer.py:33): scale = gamma/sqrt(rv+eps),
+ * shift = beta - rm*scale, for N columns (padded columns -> 0). */
+int mmad_bn_eval_affine(int N, int Np, const float* gamma, const float* beta, const float* rm,
+                        const float* rv, float eps, float* scale, float* shift, void* stream);
+
+/* BatchNorm1d train-mode forward (layers/fc_layer.py:39-45; torch
+ * native_batch_norm): merges the Welford partials of mmad_fc_fwd, normalises
+ * a -> y with batch statistics (biased var), updates running stats
+ * (momentum, unbiased var), saves mean / rstd for backward. */
+int mmad_bn_train_apply(int dtype, int M, int N, int Mp, int Np, const void* a,
+                        const float* stats, const float* gamma, const float* beta,
+                        float* running_mean, float* running_var, float momentum, float eps,
+                        float* save_mean, float* save_rstd, void* y, void* stream);
+
+/* Backward of Linear (autograd of layers/fc_layer.py:38):
+ * dx[Mp][Kp] = dz[Mp][Np] . w[Np][Kp]; colsum (nullable, [Mp/32][2][Kp]
+ * slot 0) = per-chunk column sums of dx (bias grad of a no-BN producer). */
+int mmad_fc_bwd_data(int dtype, int M, int N, int K, int Mp, int Np, int Kp, const void* dz,
+                     const void* w, void* dx, float* colsum, void* stream);
+
+/* dW[Np][Kp] (fp32) = dz[Mp][Np]^T . x[Mp][Kp] (K = batch). */
+int mmad_fc_bwd_weight(int dtype, int Mp, int Np, int Kp, const void* dz, const void* x,
+                       float* dw, void* stream);
+
+/* Backward of BN(train) o Activation (layers/fc_layer.py:38-45):
+ * dbeta = sum dy, dgamma = sum dy*xhat, da = gamma*rstd/M*(M dy - dbeta - xhat dgamma),
+ * dz = da * act'(a).  Writes dz (dtype), dgamma/dbeta (fp32 [Np]) and db
+ * partials ([Mp/128][Np], consumed by mmad_colsum).  ws: >= mmad_bn_act_bwd_ws(Mp,Np) bytes. */
+size_t mmad_bn_act_bwd_ws(int Mp, int Np);
+int mmad_bn_act_bwd(int dtype, int act, float slope, int M, int N, int Mp, int Np, const void* dy,
+                    const void* a, const float* save_mean, const float* save_rstd,
+                    const float* gamma, void* dz, float* dgamma, float* dbeta, float* db_partials,
+                    void* ws, void* stream);
+
+/* out[j] = scale * sum_{i<n_parts} partials[i*part_stride + j], j < N (Np padded -> 0). */
+int mmad_colsum(int n_parts, int N, int Np, const float* partials, int part_stride, float scale,
+                float* out, void* stream);
+
+/* out[0] = scale * sum of n floats (single block, deterministic). */
+int mmad_sum(int64_t n, const float* x, float scale, float* out, int accumulate, void* stream);
+
+/* f32 [M][ld_x] -> packed dtype [Mp][Kp] (zero padding). */
+int mmad_pack_input(int dtype, int M, int K, int Mp, int Kp, const float* x, int ld_x, void* out,
+                    void* stream);
+
+/* packed dtype [Mp][Np] -> f32 [M][ld_out] (valid region). */
+int mmad_unpack_output(int dtype, int M, int N, int Np, const void* y, float* out, int ld_out,
+                       void* stream);
+
+/* torch.optim.Adam step (novelty_detection.py:90; amsgrad=False,
+ * weight_decay=0) over a flat fp32 buffer of n params:
+ * m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
+ * p -= step_size * m / (sqrt(v)/bc2_sqrt + eps); step_size = lr/(1-b1^t).
+ * shadow (nullable, bf16) receives bf16(p) for the first n_shadow elements. */
+int mmad_adam(int64_t n, float* p, const float* g, float* m, float* v, float beta1, float beta2,
+              float eps, float step_size, float bc2_sqrt, void* shadow, int64_t n_shadow,
+              void* stream);
+
+/* variational_info_bottleneck reparameterisation
+ * (decorators/variational_info_bottleneck.py:22-24,34,37): enc_out [Mp][ld_enc]
+ * (dtype) holds mu | logvar in cols [0,btl) | [btl,2btl) of the first B rows;
+ * z[row = kk*B + b][c] = eps*exp(0.5*logvar) + mu written packed into
+ * z (dtype, [Mpz][ld_z]) for kk < k.  eps: injected fp32 [k][B][btl]
+ * (nullable -> Philox N(0,1) from seed/offset; the draw is stored to eps_out,
+ * nullable).  deterministic != 0 -> z = mu (no_grad and not stochastic).
+ * kl_partial (nullable): fp32 [Mp/128] partial sums of
+ * -0.5*(1 + lv - mu^2 - exp(lv)) (build-defined KL, SURVEY §8 a10'). */
+int mmad_vib_reparam_fwd(int dtype, int B, int btl, int k, const void* enc_out, int ld_enc,
+                         const float* eps, float* eps_out, uint64_t seed, uint64_t offset,
+                         int deterministic, void* z, int ld_z, float* kl_partial, void* stream);
+
+/* Backward of the reparameterisation + beta*KL: dz [k*B rows][ld_dz] (dtype)
+ * -> d_enc_out (dtype [Mp][ld_denc], mu|logvar columns); colsum (nullable)
+ * receives column-sum partials [Mp/128][ld_denc] for the encoder's last bias. */
+int mmad_vib_reparam_bwd(int dtype, int B, int btl, int k, const void* enc_out, int ld_enc,
+                         const float* eps, const void* dz, int ld_dz, float beta_kl,
+                         void* d_enc_out, int ld_denc, float* colsum, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Whole-autoencoder executor (AutoEncoder.step / validate / forward and
+ * get_diffs, models/auto_encoder.py:36-91, reconstruction_aggregation.py:6-37):
+ * sequences the layer operators above on one stream with no host sync.
+ * ---------------------------------------------------------------------- */
+typedef struct mmad_ae mmad_ae;
+
+/* widths: encoder widths [n_enc+1] then decoder widths [n_dec+1]; hidden
+ * layers (all but the last of each module) are Linear->LeakyReLU(slope)->BN,
+ * last layers Linear only (model_builder.py:21-37).  vib != 0: encoder output
+ * is 2*btl (mu|logvar) and dec_widths[0] = btl. */
+int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, int n_dec,
+                   const int* dec_widths, int vib, float slope, float bn_eps, float bn_momentum);
+void mmad_ae_destroy(mmad_ae* h);
+
+/* Flat fp32 parameter layout (padded): all weights first ([Np][Kp] per layer,
+ * encoder then decoder), then per layer bias[Np], gamma[Np], beta[Np].
+ * info (int64[7] per layer): w_off, b_off, gamma_off (-1), beta_off (-1),
+ * Kp, Np, bn_off (offset into the [2][n_bn] running-stat buffer, -1).
+ * totals (int64[4]): n_params, n_weight (= bf16 shadow length), n_bn, n_layers. */
+int mmad_ae_layout(const mmad_ae* h, int64_t* info, int64_t* totals);
+
+/* Device workspace bytes for a batch of B windows and k VIB samples. */
+int64_t mmad_ae_workspace_bytes(const mmad_ae* h, int B, int k);
+
+/* Bind caller-owned device buffers (all fp32 flat, layout above).
+ * shadow: bf16 weights (MMAD_BF16) or NULL (MMAD_F32 reads params). */
+int mmad_ae_bind(mmad_ae* h, float* params, float* grads, float* adam_m, float* adam_v,
+                 void* shadow, float* running /* [2][n_bn]: mean then var */);
+
+/* Refresh the bf16 weight shadow from the fp32 params (after a host-side
+ * load_state_dict or any external parameter write).  No-op for MMAD_F32. */
+int mmad_ae_sync_shadow(mmad_ae* h, void* stream);
+
+/* AutoEncoder.step forward+backward (models/auto_encoder.py:57-73): x fp32
+ * [B][ld_x]; writes grads and loss_out[0] (device fp32; sum-MSE, or
+ * recon/k + beta*KL for VIB).  eps (VIB, nullable) as mmad_vib_reparam_fwd. */
+int mmad_ae_train_fwd_bwd(mmad_ae* h, const float* x, int ld_x, int B, int k, const float* eps,
+                          uint64_t seed, uint64_t offset, float beta_kl, float* loss_out,
+                          void* ws, int64_t ws_bytes, void* stream);
+
+/* loss.backward() after mmad_ae_forward(train_bn=1) on the same workspace
+ * (autograd path of AutoEncoder.forward): dxhat fp32 [B][ld] = dL/dx_hat;
+ * writes all parameter gradients.  Not for the VIB model. */
+int mmad_ae_backward(mmad_ae* h, const float* dxhat, int ld, int B, void* ws, int64_t ws_bytes,
+                     void* stream);
+
+/* optimizer.step() (models/auto_encoder.py:75) on the bound buffers. */
+int mmad_ae_adam(mmad_ae* h, float lr, float beta1, float beta2, float eps, int step,
+                 void* stream);
+
+/* AutoEncoder.forward (models/auto_encoder.py:46-50): x_hat fp32 [B][ld_out].
+ * train_bn != 0: batch-stat BN + running-stat update (module.train()).
+ * loss_out (nullable): sum-MSE of x_hat vs x (AutoEncoder.validate). */
+int mmad_ae_forward(mmad_ae* h, const float* x, int ld_x, int B, int train_bn, float* x_hat,
+                    int ld_out, float* loss_out, void* ws, int64_t ws_bytes, void* stream);
+
+/* get_diffs + per-window squared-diff sums (reconstruction_aggregation.py:6-37,
+ * utils/metric.py:133,171): layer_sq fp32 [n_enc+1][B] with layer_sq[l][b] =
+ * sum_c d_l[b][c]^2.  diffs (nullable): fp32 [B][sum widths] concatenated
+ * d_0 | d_1 | ... (SAP/NAP layout). */
+int mmad_ae_score(mmad_ae* h, const float* x, int ld_x, int B, float* layer_sq, float* diffs,
+                  void* ws, int64_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMAD_H_ */
