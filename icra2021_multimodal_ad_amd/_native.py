@@ -79,6 +79,9 @@ def load():
         raise NativeUnavailable(
             f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             " (or `make -C icra2021_multimodal_ad_amd/csrc`)")
+    # torch must own the process's HIP runtime: import it before libmmad.so so
+    # the dynamic loader resolves libamdhip64.so.7 to torch's copy (one runtime)
+    import torch  # noqa: F401
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -22,6 +22,21 @@ import math
 import numpy as np
 
 F32 = np.float32
+
+
+class _Precision:
+    """Storage precision of the oracle (fp32 = reference numerics; fp64 is
+    used by the tests as 'truth' to size fp32 summation-order tolerances)."""
+    ft = np.float32
+
+
+_P = _Precision()
+
+
+def set_precision(dtype):
+    _P.ft = np.dtype(dtype).type
+
+
 LEAKY_SLOPE = 0.2      # modules/activation.py:37-38 (nn.LeakyReLU(.2))
 BN_EPS = 1e-5          # nn.BatchNorm1d default, layers/fc_layer.py:33
 BN_MOMENTUM = 0.1      # nn.BatchNorm1d default
@@ -54,7 +69,7 @@ def ae_layer_sizes(input_size, btl_size, n_layers, enc_out=None):
 # --------------------------------------------------------------------------
 def leaky(z, slope=LEAKY_SLOPE):
     """modules/activation.py:37-45 (LeakyReLU forward)."""
-    return np.where(z > 0, z, z * F32(slope)).astype(F32)
+    return np.where(z > 0, z, z * _P.ft(slope)).astype(_P.ft)
 
 
 def apply_act(z, act):
@@ -65,11 +80,11 @@ def apply_act(z, act):
     if act == "leakyrelu":
         return leaky(z)
     if act == "relu":
-        return np.maximum(z, 0).astype(F32)
+        return np.maximum(z, 0).astype(_P.ft)
     if act == "sigmoid":
-        return (1.0 / (1.0 + np.exp(-z.astype(np.float64)))).astype(F32)
+        return (1.0 / (1.0 + np.exp(-z.astype(np.float64)))).astype(_P.ft)
     if act == "tanh":
-        return np.tanh(z).astype(F32)
+        return np.tanh(z).astype(_P.ft)
     raise NotImplementedError(act)
 
 
@@ -79,8 +94,8 @@ def fc_forward(x, layer, train):
     Train-mode BN (torch native_batch_norm): biased batch variance for
     normalisation, unbiased for the running update, momentum 0.1, eps 1e-5.
     Returns (y, cache); running stats are updated in place in train mode."""
-    x = x.astype(F32, copy=False)
-    z = (x @ layer["W"].T + layer["b"]).astype(F32)
+    x = x.astype(_P.ft, copy=False)
+    z = (x @ layer["W"].T + layer["b"]).astype(_P.ft)
     a = apply_act(z, layer["act"])
     cache = {"x": x, "z": z, "a": a}
     bn = layer.get("bn")
@@ -91,16 +106,16 @@ def fc_forward(x, layer, train):
         mu = a.mean(axis=0, dtype=np.float64)
         var = ((a - mu) ** 2).mean(axis=0, dtype=np.float64)
         rstd = 1.0 / np.sqrt(var + BN_EPS)
-        xhat = ((a - mu) * rstd).astype(F32)
-        y = (xhat * bn["gamma"] + bn["beta"]).astype(F32)
+        xhat = ((a - mu) * rstd).astype(_P.ft)
+        y = (xhat * bn["gamma"] + bn["beta"]).astype(_P.ft)
         unbiased = var * n / max(n - 1, 1)
-        bn["rm"] = ((1 - BN_MOMENTUM) * bn["rm"] + BN_MOMENTUM * mu).astype(F32)
-        bn["rv"] = ((1 - BN_MOMENTUM) * bn["rv"] + BN_MOMENTUM * unbiased).astype(F32)
+        bn["rm"] = ((1 - BN_MOMENTUM) * bn["rm"] + BN_MOMENTUM * mu).astype(_P.ft)
+        bn["rv"] = ((1 - BN_MOMENTUM) * bn["rv"] + BN_MOMENTUM * unbiased).astype(_P.ft)
         bn["nbt"] = int(bn.get("nbt", 0)) + 1
-        cache.update(xhat=xhat, rstd=rstd.astype(F32), mu=mu.astype(F32))
+        cache.update(xhat=xhat, rstd=rstd.astype(_P.ft), mu=mu.astype(_P.ft))
     else:
         rstd = 1.0 / np.sqrt(bn["rv"].astype(np.float64) + BN_EPS)
-        y = ((a - bn["rm"]) * rstd * bn["gamma"] + bn["beta"]).astype(F32)
+        y = ((a - bn["rm"]) * rstd * bn["gamma"] + bn["beta"]).astype(_P.ft)
     return y, cache
 
 
@@ -142,26 +157,26 @@ def fc_backward(dy, layer, cache):
         dbeta = dy.sum(axis=0, dtype=np.float64)
         dgamma = (dy * xhat).sum(axis=0, dtype=np.float64)
         da = (bn["gamma"] * rstd / n) * (n * dy - dbeta - xhat * dgamma)
-        da = da.astype(F32)
-        g["gamma"] = dgamma.astype(F32)
-        g["beta"] = dbeta.astype(F32)
+        da = da.astype(_P.ft)
+        g["gamma"] = dgamma.astype(_P.ft)
+        g["beta"] = dbeta.astype(_P.ft)
     else:
         da = dy
     if layer["act"] == "leakyrelu":
-        dz = np.where(cache["z"] > 0, da, da * F32(LEAKY_SLOPE)).astype(F32)
+        dz = np.where(cache["z"] > 0, da, da * _P.ft(LEAKY_SLOPE)).astype(_P.ft)
     elif layer["act"] is None:
         dz = da
     else:
         raise NotImplementedError(layer["act"])
-    g["W"] = (dz.T @ cache["x"]).astype(F32)
-    g["b"] = dz.sum(axis=0, dtype=np.float64).astype(F32)
-    dx = (dz @ layer["W"]).astype(F32)
+    g["W"] = (dz.T @ cache["x"]).astype(_P.ft)
+    g["b"] = dz.sum(axis=0, dtype=np.float64).astype(_P.ft)
+    dx = (dz @ layer["W"]).astype(_P.ft)
     return dx, g
 
 
 def module_backward(dout, layers, caches):
     shape = dout.shape
-    d = dout.reshape(-1, shape[-1]).astype(F32)
+    d = dout.reshape(-1, shape[-1]).astype(_P.ft)
     grads = [None] * len(layers)
     for i in range(len(layers) - 1, -1, -1):
         d, grads[i] = fc_backward(d, layers[i], caches[i])
@@ -173,7 +188,7 @@ def ae_train_grads(x, model):
     without the optimiser: returns (loss, x_hat, grads{"enc","dec"})."""
     xh, cache = ae_forward(x, model, train=True)
     loss = mse_sum(xh, x)
-    dxh = (F32(2.0) * (xh - x)).astype(F32)
+    dxh = (_P.ft(2.0) * (xh - x)).astype(_P.ft)
     dz, gd = module_backward(dxh, model["dec"], cache["dec"])
     _, ge = module_backward(dz, model["enc"], cache["enc"])
     return loss, xh, {"enc": ge, "dec": gd}
@@ -206,16 +221,16 @@ def adam_step(model, grads, state, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
     bc2 = 1 - b2 ** t
     for key, layer, where in iter_params(model):
         side, li, name = key
-        g = grads[side][li][name].astype(F32)
+        g = grads[side][li][name].astype(_P.ft)
         holder = layer["bn"] if where == "bn" else layer
         pname = name
         p = holder[pname]
         m = state.setdefault(("m",) + key, np.zeros_like(p))
         v = state.setdefault(("v",) + key, np.zeros_like(p))
-        m[...] = (b1 * m + (1 - b1) * g).astype(F32)
-        v[...] = (b2 * v + (1 - b2) * g * g).astype(F32)
-        denom = (np.sqrt(v) / F32(math.sqrt(bc2)) + F32(eps)).astype(F32)
-        holder[pname] = (p - F32(lr / bc1) * m / denom).astype(F32)
+        m[...] = (b1 * m + (1 - b1) * g).astype(_P.ft)
+        v[...] = (b2 * v + (1 - b2) * g * g).astype(_P.ft)
+        denom = (np.sqrt(v) / _P.ft(math.sqrt(bc2)) + _P.ft(eps)).astype(_P.ft)
+        holder[pname] = (p - _P.ft(lr / bc1) * m / denom).astype(_P.ft)
     return state
 
 
@@ -239,8 +254,8 @@ def vib_reparam(mu, logvar, eps_noise):
     """decorators/variational_info_bottleneck.py:22-24,37:
     sigma = exp(0.5*logvar); z[k] = eps[k]*sigma + mu.  ``eps_noise`` is
     [k, B, btl] (injected noise; the reference draws randn_like)."""
-    sigma = np.exp(F32(0.5) * logvar).astype(F32)
-    return (eps_noise * sigma[None] + mu[None]).astype(F32)
+    sigma = np.exp(_P.ft(0.5) * logvar).astype(_P.ft)
+    return (eps_noise * sigma[None] + mu[None]).astype(_P.ft)
 
 
 def kl_normal(mu, logvar):
@@ -262,13 +277,13 @@ def vib_ae_train_grads(x, model, eps_noise, beta_kl):
     recon = float((d * d).sum()) / k
     kl = kl_normal(mu, logvar)
     loss = recon + beta_kl * kl
-    dxh = (F32(2.0 / k) * (xh - x[None])).astype(F32)
+    dxh = (_P.ft(2.0 / k) * (xh - x[None])).astype(_P.ft)
     dz, gd = module_backward(dxh, model["dec"], cd)
     dz = dz.reshape(z.shape)
-    sigma = np.exp(F32(0.5) * logvar).astype(F32)
-    dmu = dz.sum(axis=0) + F32(beta_kl) * mu
-    dlv = (dz * eps_noise).sum(axis=0) * sigma * F32(0.5) + F32(0.5 * beta_kl) * (np.exp(logvar) - 1)
-    dout = np.concatenate([dmu, dlv], axis=-1).astype(F32)
+    sigma = np.exp(_P.ft(0.5) * logvar).astype(_P.ft)
+    dmu = dz.sum(axis=0) + _P.ft(beta_kl) * mu
+    dlv = (dz * eps_noise).sum(axis=0) * sigma * _P.ft(0.5) + _P.ft(0.5 * beta_kl) * (np.exp(logvar) - 1)
+    dout = np.concatenate([dmu, dlv], axis=-1).astype(_P.ft)
     _, ge = module_backward(dout, model["enc"], ce)
     return loss, {"enc": ge, "dec": gd}, {"mu": mu, "logvar": logvar, "z": z, "x_hat": xh,
                                           "recon": recon, "kl": kl}
@@ -282,7 +297,7 @@ def get_diffs(x, model, batch_size=698):
     each encoder layer l, d_l = enc_l(x_hat_{l-1}) - enc_l(x_{l-1})."""
     out = None
     for s in range(0, x.shape[0], batch_size):
-        xb = x[s:s + batch_size].astype(F32)
+        xb = x[s:s + batch_size].astype(_P.ft)
         xh, _ = ae_forward(xb, model, train=False)
         diffs = [xh - xb]
         h, ht = xb, xh
@@ -295,7 +310,7 @@ def get_diffs(x, model, batch_size=698):
         else:
             for o, d in zip(out, diffs):
                 o.append(d)
-    return [np.concatenate(o, axis=0).astype(F32) for o in out]
+    return [np.concatenate(o, axis=0).astype(_P.ft) for o in out]
 
 
 def layer_sq_sums(diffs):
@@ -331,21 +346,21 @@ def nap_fit(train_cat):
     """utils/normalize.py:52-70 (Rotater.fit: mu, V from SVD of centred train
     diffs) + :20-34 (Standardizer.fit on the rotated train diffs; var is the
     ddof=1 np.cov diagonal)."""
-    x = train_cat.astype(F32)
-    mu_r = x.mean(axis=0, dtype=np.float64).astype(F32)
+    x = train_cat.astype(_P.ft)
+    mu_r = x.mean(axis=0, dtype=np.float64).astype(_P.ft)
     _, _, vt = np.linalg.svd((x - mu_r).astype(np.float64), full_matrices=False)
-    v = vt.T.astype(F32)
-    rot = ((x - mu_r) @ v).astype(F32)
-    mu_s = rot.mean(axis=0, dtype=np.float64).astype(F32)
+    v = vt.T.astype(_P.ft)
+    rot = ((x - mu_r) @ v).astype(_P.ft)
+    mu_s = rot.mean(axis=0, dtype=np.float64).astype(_P.ft)
     c = rot - mu_s
-    var = ((c.astype(np.float64) ** 2).sum(axis=0) / max(c.shape[0] - 1, 1)).astype(F32)
+    var = ((c.astype(np.float64) ** 2).sum(axis=0) / max(c.shape[0] - 1, 1)).astype(_P.ft)
     return {"mu_r": mu_r, "v": v, "mu_s": mu_s, "var": var}
 
 
 def nap_score(cat, fit):
     """utils/metric.py:219-222 + utils/normalize.py:36-45,72-103:
     mean_j(((x-mu_r) V - mu_s)_j^2 / var_j)."""
-    rot = ((cat.astype(F32) - fit["mu_r"]) @ fit["v"]).astype(np.float64)
+    rot = ((cat.astype(_P.ft) - fit["mu_r"]) @ fit["v"]).astype(np.float64)
     st = (rot - fit["mu_s"]) / np.sqrt(fit["var"].astype(np.float64))
     return (st ** 2).mean(axis=1)
 

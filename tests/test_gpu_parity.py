@@ -37,6 +37,37 @@ def _model(d, btl, nl, sd, dtype="f32", models="ae", k=1, beta_kl=1.0):
     return m, cfg
 
 
+_TRUTH = {}
+
+
+def _truth_grads(g, name):
+    """float64 oracle gradients ('truth') for a golden case."""
+    if name not in _TRUTH:
+        sd = _sd(g, "init/")
+        O.set_precision(np.float64)
+        try:
+            m = model_from_state_dict({k: (np.asarray(v, np.float64) if np.asarray(v).dtype == np.float32
+                                           else v) for k, v in sd.items()})
+            _, _, gr = O.ae_train_grads(g["x/0"].astype(np.float64), m)
+        finally:
+            O.set_precision(np.float32)
+        _TRUTH[name] = grads_to_flat(gr)
+    return _TRUTH[name]
+
+
+def assert_grads_close(got, g, name):
+    """fp32 bar: within 1e-4 of max|g| of the fp64 truth, or within 2x the
+    reference's own fp32 deviation from that truth (near-cancelling BN-layer
+    bias gradients are summation-order noise in the reference too)."""
+    truth = _truth_grads(g, name)
+    for k, t in truth.items():
+        ref = g["step1/grad/" + k]
+        scale = np.abs(t).max() + 1e-30
+        ref_err = np.abs(ref - t).max() / scale
+        err = np.abs(np.asarray(got[k], np.float64) - t).max() / scale
+        assert err < max(1e-4, 2.0 * ref_err), (k, err, ref_err)
+
+
 def _grads_flat(model):
     nat = model._native
     out = {}
@@ -62,8 +93,7 @@ def test_train_step_fp32_matches_reference(golden, name):
     x = torch.from_numpy(g["x/0"]).cuda()
     loss = float(m._native.train_step(x))
     assert abs(loss - g["step1/loss"]) <= 1e-4 * g["step1/loss"]
-    for k, v in _grads_flat(m).items():
-        assert _rel(v, g["step1/grad/" + k]) < 1e-4, k
+    assert_grads_close(_grads_flat(m), g, name)
     sd = m.state_dict()
     for k in sd:
         if "running" in k:
@@ -179,8 +209,7 @@ def test_autograd_forward_backward_matches(golden):
     assert abs(loss.item() - g["step1/loss"]) <= 1e-4 * g["step1/loss"]
     m.zero_grad()
     loss.backward()
-    for name, p in m.named_parameters():
-        assert _rel(p.grad.cpu().numpy(), g["step1/grad/" + name]) < 1e-4, name
+    assert_grads_close({n: p.grad.cpu().numpy() for n, p in m.named_parameters()}, g, "mm192")
 
 
 def test_d1728_reference_width_fp32(golden):
