@@ -52,6 +52,8 @@ SIGNATURES = {
     "mmad_ae_bind": (_I, [_P, _P, _P, _P, _P, _P, _P]),
     "mmad_ae_sync_shadow": (_I, [_P, _P]),
     "mmad_ae_train_fwd_bwd": (_I, [_P, _P, _I, _I, _I, _P, _U64, _U64, _F, _P, _P, _I64, _P]),
+    "mmad_ae_train_step": (_I, [_P, _P, _I, _I, _I, _P, _U64, _U64, _F, _F, _F, _F, _F, _I, _P,
+                                _P, _I64, _P]),
     "mmad_ae_backward": (_I, [_P, _P, _I, _I, _P, _I64, _P]),
     "mmad_ae_adam": (_I, [_P, _F, _F, _F, _F, _I, _P]),
     "mmad_ae_forward": (_I, [_P, _P, _I, _I, _I, _P, _I, _P, _P, _I64, _P]),

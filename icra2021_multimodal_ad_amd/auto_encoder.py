@@ -209,15 +209,36 @@ class AutoEncoder(AbstractModel):
         self.train()
         nat = self._native
         seed = 0x9E3779B97F4A7C15 & ((1 << 63) - 1)
+        if self.dist is None:
+            lr, betas, aeps = self._adam_hyper(optimizer)
+            loss = nat.train_step_fused(x, lr=lr, betas=betas, adam_eps=aeps, k=self.k, eps=eps,
+                                        seed=seed, offset=self._rng_offset, beta_kl=self.beta_kl)
+            self._rng_offset += 1
+            self._count_bn_step()
+            if optimizer is not None:
+                self._mirror_optimizer_state(optimizer)
+            return loss
         loss = nat.train_step(x, k=self.k, eps=eps, seed=seed, offset=self._rng_offset,
                               beta_kl=self.beta_kl)
         self._rng_offset += 1
         self._count_bn_step()
-        if self.dist is not None:
-            self.dist.all_reduce_grads(nat.grads)
-            self.dist.all_reduce_loss(loss)
+        self.dist.all_reduce_grads(nat.grads)
+        self.dist.all_reduce_loss(loss)
         self._optimizer_step(optimizer)
         return loss
+
+    @staticmethod
+    def _adam_hyper(optimizer):
+        lr, betas, eps = 1e-3, (0.9, 0.999), 1e-8
+        if optimizer is not None:
+            if not isinstance(optimizer, torch.optim.Adam):
+                raise NotImplementedError("native step supports torch.optim.Adam "
+                                          "(novelty_detection.py:90)")
+            grp = optimizer.param_groups[0]
+            if grp.get("weight_decay", 0) or grp.get("amsgrad", False) or grp.get("maximize", False):
+                raise NotImplementedError("native Adam: weight_decay/amsgrad/maximize unsupported")
+            lr, betas, eps = float(grp["lr"]), tuple(grp["betas"]), float(grp["eps"])
+        return lr, betas, eps
 
     def _optimizer_step(self, optimizer):
         nat = self._native

@@ -1,0 +1,639 @@
+// Whole-autoencoder executor (mmad_ae_* in include/mmad.h).
+//
+// Replaces the reference's per-op Python dispatch of AutoEncoder.step /
+// validate / forward (models/auto_encoder.py:36-91) and get_diffs
+// (reconstruction_aggregation.py:6-37): one host call enqueues the whole
+// forward + backward (+ Adam) or scoring sequence, no host syncs, no device
+// allocation (caller workspace).
+//
+// Train-mode dataflow per hidden layer l (Linear -> LeakyReLU -> BN):
+//   fwd GEMM (A normalised on load with layer l-1's BN affine) -> a_l + Welford
+//   partials -> bn_finalize (mean, rstd, affine, running stats); y_l is never
+//   written to HBM.  Backward: the bwd-data GEMM epilogue emits the BN-backward
+//   column partials of dy_l; bn_act_bwd_apply produces dz_l; the dW GEMM
+//   (B operand = y_{l-1} normalised on load) runs on a side stream, followed
+//   (single-GPU fused step) by that layer's Adam update, overlapping the
+//   remaining backward chain on the main stream.
+#include <cmath>
+#include <vector>
+
+#include "mmad_common.h"
+#include "mmad_gemm.h"
+#include "mmad_ops.h"
+
+#define RET_IF(x)                    \
+  do {                               \
+    int r_ = (x);                    \
+    if (r_ != MMAD_OK) return r_;    \
+  } while (0)
+
+struct AeLayer {
+  int K, N, Kp, Np;
+  int act, bn, enc;
+  int64_t w_off, b_off, g_off, be_off, bn_off;
+};
+
+struct mmad_ae {
+  int dtype, n_enc, n_dec, vib, btl;
+  float slope, bn_eps, bn_mom;
+  std::vector<AeLayer> L;
+  int64_t n_params, n_weight, n_bn;
+  float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr, *running = nullptr;
+  void* shadow = nullptr;
+  // side stream + events for the dW / Adam overlap (created at bind time)
+  hipStream_t side = nullptr;
+  std::vector<hipEvent_t> ev_fork, ev_data;
+  hipEvent_t ev_join = nullptr;
+  ~mmad_ae() {
+    for (auto e : ev_fork) (void)hipEventDestroy(e);
+    for (auto e : ev_data) (void)hipEventDestroy(e);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (side) (void)hipStreamDestroy(side);
+  }
+};
+
+struct LayerWS {
+  void *out, *y, *dy, *dz;
+  float *stats, *mean, *rstd, *scale, *shift, *bnpart, *dbpart, *rowsq;
+};
+struct AeWS {
+  int B, k, Mpe, Mpd;
+  void *xin, *zbuf, *dzin;
+  float *eps, *klpart, *misc;
+  int64_t kl_parts;
+  std::vector<LayerWS> l;
+  int64_t bytes;
+};
+
+static size_t esz(int dtype) { return dtype == MMAD_BF16 ? 2 : 4; }
+
+static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
+  int64_t off = 0;
+  auto take = [&](int64_t bytes) -> char* {
+    off = (off + 255) / 256 * 256;
+    char* p = base ? base + off : nullptr;
+    off += bytes;
+    return p;
+  };
+  const size_t es = esz(h->dtype);
+  w.B = B;
+  w.k = k;
+  w.Mpe = mmad_roundup(B, MMAD_PAD);
+  w.Mpd = mmad_roundup(B * k, MMAD_PAD);
+  const int nL = (int)h->L.size();
+  w.xin = take((int64_t)w.Mpe * h->L[0].Kp * es);
+  w.zbuf = w.dzin = nullptr;
+  w.eps = w.klpart = nullptr;
+  w.kl_parts = 0;
+  if (h->vib) {
+    const AeLayer& d0 = h->L[h->n_enc];
+    w.zbuf = take((int64_t)w.Mpd * d0.Kp * es);
+    w.dzin = take((int64_t)w.Mpd * d0.Kp * es);
+    w.eps = (float*)take((int64_t)k * B * h->btl * 4);
+    w.kl_parts = mmad_vib_kl_parts(B, k, d0.Kp);
+    w.klpart = (float*)take(w.kl_parts * 4);
+  }
+  w.misc = (float*)take(1024 * 4);
+  w.l.resize(nL);
+  for (int i = 0; i < nL; ++i) {
+    const AeLayer& a = h->L[i];
+    const int Mp = a.enc ? w.Mpe : w.Mpd;
+    const int64_t mat = (int64_t)Mp * a.Np * es;
+    LayerWS& s = w.l[i];
+    s.out = take(mat);
+    s.y = a.bn ? take(mat) : nullptr;
+    s.dy = take(mat);
+    s.dz = a.bn ? take(mat) : nullptr;
+    s.stats = (float*)take((int64_t)(Mp / MMAD_PART_ROWS) * 2 * a.Np * 4);
+    s.mean = (float*)take(a.Np * 4);
+    s.rstd = (float*)take(a.Np * 4);
+    s.scale = (float*)take(a.Np * 4);
+    s.shift = (float*)take(a.Np * 4);
+    s.bnpart = (float*)take((int64_t)(Mp / 64) * 2 * a.Np * 4);
+    s.dbpart = (float*)take((int64_t)(Mp / 128) * a.Np * 4);
+    s.rowsq = (float*)take((int64_t)(a.Np / 128) * Mp * 4);
+  }
+  w.bytes = (off + 255) / 256 * 256;
+}
+
+// ---------------------------------------------------------------------------
+int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, int n_dec,
+                   const int* dec_widths, int vib, float slope, float bn_eps, float bn_momentum) {
+  MMAD_CHECK_ARG(out != nullptr, "ae_create: null out");
+  *out = nullptr;
+  MMAD_CHECK_ARG(dtype == MMAD_F32 || dtype == MMAD_BF16, "ae_create: bad dtype %d", dtype);
+  MMAD_CHECK_ARG(n_enc >= 1 && n_dec >= 1 && enc_widths && dec_widths, "ae_create: bad layers");
+  for (int i = 0; i <= n_enc; ++i) MMAD_CHECK_ARG(enc_widths[i] >= 1, "ae_create: bad enc width");
+  for (int i = 0; i <= n_dec; ++i) MMAD_CHECK_ARG(dec_widths[i] >= 1, "ae_create: bad dec width");
+  MMAD_CHECK_ARG(dec_widths[n_dec] == enc_widths[0], "ae_create: decoder must reconstruct input");
+  if (vib)
+    MMAD_CHECK_ARG(enc_widths[n_enc] == 2 * dec_widths[0],
+                   "ae_create: VIB encoder output must be 2*btl");
+  else
+    MMAD_CHECK_ARG(enc_widths[n_enc] == dec_widths[0], "ae_create: bottleneck mismatch");
+  mmad_ae* h = new mmad_ae();
+  h->dtype = dtype;
+  h->n_enc = n_enc;
+  h->n_dec = n_dec;
+  h->vib = vib;
+  h->btl = dec_widths[0];
+  h->slope = slope;
+  h->bn_eps = bn_eps;
+  h->bn_mom = bn_momentum;
+  for (int side = 0; side < 2; ++side) {
+    const int n = side == 0 ? n_enc : n_dec;
+    const int* wd = side == 0 ? enc_widths : dec_widths;
+    for (int i = 0; i < n; ++i) {
+      AeLayer a{};
+      a.K = wd[i];
+      a.N = wd[i + 1];
+      a.Kp = mmad_roundup(a.K, MMAD_PAD);
+      a.Np = mmad_roundup(a.N, MMAD_PAD);
+      a.bn = i < n - 1;
+      a.act = a.bn ? MMAD_ACT_LEAKYRELU : MMAD_ACT_NONE;
+      a.enc = side == 0;
+      h->L.push_back(a);
+    }
+  }
+  int64_t off = 0;
+  for (auto& a : h->L) { a.w_off = off; off += (int64_t)a.Np * a.Kp; }
+  h->n_weight = off;
+  int64_t bn = 0;
+  for (auto& a : h->L) {
+    a.b_off = off; off += a.Np;
+    a.g_off = a.be_off = a.bn_off = -1;
+    if (a.bn) {
+      a.g_off = off; off += a.Np;
+      a.be_off = off; off += a.Np;
+      a.bn_off = bn; bn += a.Np;
+    }
+  }
+  h->n_params = off;
+  h->n_bn = bn;
+  *out = h;
+  return MMAD_OK;
+}
+
+void mmad_ae_destroy(mmad_ae* h) { delete h; }
+
+int mmad_ae_layout(const mmad_ae* h, int64_t* info, int64_t* totals) {
+  MMAD_CHECK_ARG(h && info && totals, "ae_layout: null arg");
+  for (size_t i = 0; i < h->L.size(); ++i) {
+    const AeLayer& a = h->L[i];
+    int64_t* r = info + 7 * i;
+    r[0] = a.w_off; r[1] = a.b_off; r[2] = a.g_off; r[3] = a.be_off;
+    r[4] = a.Kp; r[5] = a.Np; r[6] = a.bn_off;
+  }
+  totals[0] = h->n_params;
+  totals[1] = h->n_weight;
+  totals[2] = h->n_bn;
+  totals[3] = (int64_t)h->L.size();
+  return MMAD_OK;
+}
+
+int64_t mmad_ae_workspace_bytes(const mmad_ae* h, int B, int k) {
+  if (!h || B < 1 || k < 1) return -1;
+  AeWS w;
+  carve(h, B, k, nullptr, w);
+  return w.bytes;
+}
+
+int mmad_ae_bind(mmad_ae* h, float* params, float* grads, float* adam_m, float* adam_v,
+                 void* shadow, float* running) {
+  MMAD_CHECK_ARG(h && params, "ae_bind: null params");
+  MMAD_CHECK_ARG(h->dtype != MMAD_BF16 || shadow, "ae_bind: bf16 needs a shadow buffer");
+  h->params = params;
+  h->grads = grads;
+  h->m = adam_m;
+  h->v = adam_v;
+  h->shadow = shadow;
+  h->running = running;
+  if (!h->side) {
+    MMAD_HIP_CHECK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+    const size_t n = h->L.size();
+    h->ev_fork.resize(n);
+    h->ev_data.resize(n);
+    for (size_t i = 0; i < n; ++i) {
+      MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_fork[i], hipEventDisableTiming));
+      MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_data[i], hipEventDisableTiming));
+    }
+    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+  }
+  return MMAD_OK;
+}
+
+int mmad_ae_sync_shadow(mmad_ae* h, void* stream) {
+  MMAD_CHECK_ARG(h && h->params, "ae_sync_shadow: unbound");
+  if (h->dtype != MMAD_BF16) return MMAD_OK;
+  return mmad_to_bf16(h->n_weight, h->params, h->shadow, stream);
+}
+
+// ---------------------------------------------------------------------------
+static const void* weights(const mmad_ae* h, const AeLayer& a) {
+  if (h->dtype == MMAD_BF16) return (const char*)h->shadow + a.w_off * 2;
+  return h->params + a.w_off;
+}
+
+// input of layer l; in train mode a BN producer's output stays pre-BN (a) and
+// the consumer normalises it on load with (scale, shift)
+static const void* input_of(const mmad_ae* h, const AeWS& w, int l, bool train,
+                            const float** scale, const float** shift) {
+  *scale = *shift = nullptr;
+  if (l == 0) return w.xin;
+  if (h->vib && l == h->n_enc) return w.zbuf;
+  const AeLayer& p = h->L[l - 1];
+  const LayerWS& ps = w.l[l - 1];
+  if (!p.bn) return ps.out;
+  if (!train) return ps.y;
+  *scale = ps.scale;
+  *shift = ps.shift;
+  return ps.out;
+}
+
+static int prepare_ws(const mmad_ae* h, int B, int k, void* ws, int64_t ws_bytes, AeWS& w) {
+  MMAD_CHECK_ARG(B >= 1 && k >= 1, "bad batch B=%d k=%d", B, k);
+  MMAD_CHECK_ARG(h->vib || k == 1, "k>1 needs the VIB head");
+  carve(h, B, k, (char*)ws, w);
+  MMAD_CHECK_ARG(ws && ws_bytes >= w.bytes, "workspace too small (%lld < %lld bytes)",
+                 (long long)ws_bytes, (long long)w.bytes);
+  MMAD_CHECK_ARG(((uintptr_t)ws) % 256 == 0, "workspace must be 256-byte aligned");
+  return MMAD_OK;
+}
+
+static inline int rows_of(const AeWS& w, const AeLayer& a) { return a.enc ? w.B : w.B * w.k; }
+static inline int prows_of(const AeWS& w, const AeLayer& a) { return a.enc ? w.Mpe : w.Mpd; }
+static float* running_mean(const mmad_ae* h, const AeLayer& a) { return h->running + a.bn_off; }
+static float* running_var(const mmad_ae* h, const AeLayer& a) {
+  return h->running + h->n_bn + a.bn_off;
+}
+
+static GemmEpi fwd_epi(const mmad_ae* h, const AeLayer& a, int M, void* out, const float* a_scale,
+                       const float* a_shift) {
+  GemmEpi ep{};
+  ep.M = M;
+  ep.N = a.N;
+  ep.out = out;
+  ep.ldo = a.Np;
+  ep.bias = h->params + a.b_off;
+  ep.act = a.act;
+  ep.slope = h->slope;
+  ep.ldpart = a.Np;
+  ep.a_scale = a_scale;
+  ep.a_shift = a_shift;
+  return ep;
+}
+
+// mode 0 = train (MSE-fused last layer), 1 = eval, 2 = train BN, plain last layer
+static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, const float* eps,
+                       uint64_t seed, uint64_t offset, hipStream_t st) {
+  const int dt = h->dtype;
+  const int nL = (int)h->L.size();
+  const int B = w.B, k = w.k;
+  const bool train = mode != 1;
+  RET_IF(mmad_pack_input(dt, B, h->L[0].K, w.Mpe, h->L[0].Kp, x, ld_x, w.xin, st));
+  for (int l = 0; l < nL; ++l) {
+    const AeLayer& a = h->L[l];
+    LayerWS& s = w.l[l];
+    const int M = rows_of(w, a), Mp = prows_of(w, a);
+    const float *isc, *ish;
+    const void* in = input_of(h, w, l, train, &isc, &ish);
+    const void* wt = weights(h, a);
+    if (mode == 0 && l == nL - 1) {
+      GemmEpi ep = fwd_epi(h, a, M, s.out, isc, ish);
+      ep.act = MMAD_ACT_NONE;
+      ep.part = s.stats;
+      ep.target = x;
+      ep.ldt = ld_x;
+      ep.tmod = B;
+      ep.gscale = 2.0f / (float)k;
+      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_MSE, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
+    } else if (a.bn && train) {
+      GemmEpi ep = fwd_epi(h, a, M, s.out, isc, ish);
+      ep.part = s.stats;
+      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
+      RET_IF(mmad_bn_finalize(M, a.N, Mp, a.Np, s.stats, h->params + a.g_off,
+                              h->params + a.be_off, running_mean(h, a), running_var(h, a),
+                              h->bn_mom, h->bn_eps, s.mean, s.rstd, s.scale, s.shift, st));
+    } else if (a.bn) {
+      RET_IF(mmad_bn_eval_affine(a.N, a.Np, h->params + a.g_off, h->params + a.be_off,
+                                 running_mean(h, a), running_var(h, a), h->bn_eps, s.scale,
+                                 s.shift, st));
+      GemmEpi ep = fwd_epi(h, a, M, s.y, isc, ish);
+      ep.bn_scale = s.scale;
+      ep.bn_shift = s.shift;
+      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
+    } else {
+      GemmEpi ep = fwd_epi(h, a, M, s.out, isc, ish);
+      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
+    }
+    if (h->vib && l == h->n_enc - 1) {
+      const AeLayer& d0 = h->L[h->n_enc];
+      RET_IF(mmad_vib_reparam_fwd(dt, B, h->btl, k, s.out, a.Np, eps, w.eps, seed, offset,
+                                  mode == 1 ? 1 : 0, w.zbuf, d0.Kp,
+                                  mode == 0 ? w.klpart : nullptr, st));
+    }
+  }
+  return MMAD_OK;
+}
+
+// where the bias gradient partials of layer l live after the backward of l+1
+struct BiasSrc { const float* src; int nparts, stride; };
+static BiasSrc bias_src(const mmad_ae* h, const AeWS& w, int l, bool from_mse) {
+  const AeLayer& a = h->L[l];
+  const LayerWS& s = w.l[l];
+  const int Mp = prows_of(w, a);
+  const int nL = (int)h->L.size();
+  if (l == nL - 1 && from_mse) return {s.stats, Mp / MMAD_PART_ROWS, 2 * a.Np};
+  if (l == nL - 1 || a.bn || (h->vib && l == h->n_enc - 1)) return {s.dbpart, Mp / 128, a.Np};
+  return {s.stats, Mp / MMAD_PART_ROWS, 2 * a.Np};  // bwd-data epilogue column sums
+}
+
+struct AdamHyper { float b1, b2, eps, step_size, bc2_sqrt; };
+
+// backward through every layer.  from_mse: the last layer's dz and bias
+// partials come from the MSE-fused forward epilogue; otherwise the caller has
+// packed dL/dx_hat into the last layer's dy buffer.  adam != null: each
+// layer's Adam update runs on the side stream right after its dW GEMM.
+static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const AdamHyper* adam,
+                        hipStream_t st) {
+  const int dt = h->dtype;
+  const int nL = (int)h->L.size();
+  hipStream_t side = h->side;
+  for (int l = nL - 1; l >= 0; --l) {
+    const AeLayer& a = h->L[l];
+    LayerWS& s = w.l[l];
+    const int Mp = prows_of(w, a);
+    const void* dz = (l == nL - 1) ? (from_mse ? s.out : s.dy) : (a.bn ? s.dz : s.dy);
+    const float *isc, *ish;
+    const void* in = input_of(h, w, l, true, &isc, &ish);
+    // fork: dz_l (and every small grad of layer l) is complete on the main stream
+    MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
+    MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
+    {
+      GemmEpi ep{};
+      ep.M = a.Np;
+      ep.N = a.Kp;
+      ep.out = h->grads + a.w_off;
+      ep.ldo = a.Kp;
+      ep.b_scale = isc;
+      ep.b_shift = ish;
+      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, ep,
+                                side));
+    }
+    if (l > 0) {
+      const AeLayer& p = h->L[l - 1];
+      LayerWS& ps = w.l[l - 1];
+      const int M = rows_of(w, a);
+      const int Mpp = prows_of(w, p);
+      GemmEpi ep{};
+      ep.M = M;
+      ep.N = a.K;
+      ep.ldo = a.Kp;
+      ep.ldpart = a.Kp;
+      if (h->vib && l == h->n_enc) {
+        ep.out = w.dzin;
+        RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
+                                  a.Np, ep, st));
+        RET_IF(mmad_vib_reparam_bwd(dt, w.B, h->btl, w.k, ps.out, p.Np, w.eps, w.dzin, a.Kp,
+                                    beta_kl, ps.dy, p.Np, ps.dbpart, st));
+      } else if (p.bn) {
+        ep.out = ps.dy;
+        ep.bn_a = ps.out;
+        ep.bn_mean = ps.mean;
+        ep.bn_rstd = ps.rstd;
+        ep.bn_part = ps.bnpart;
+        RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
+                                  a.Np, ep, st));
+        RET_IF(mmad_bn_act_bwd_apply(dt, p.act, h->slope, rows_of(w, p), p.N, Mpp, p.Np, ps.dy,
+                                     ps.out, ps.mean, ps.rstd, h->params + p.g_off, ps.bnpart,
+                                     Mpp / 64, ps.dz, h->grads + p.g_off, h->grads + p.be_off,
+                                     ps.dbpart, st));
+      } else {
+        ep.out = ps.dy;
+        ep.part = ps.stats;
+        RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
+                                  a.Np, ep, st));
+      }
+    }
+    if (adam) {
+      // W_l is free once the main stream has finished reading it (bwd-data of l)
+      MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
+      MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_data[l], 0));
+      const BiasSrc bs = bias_src(h, w, l, from_mse);
+      MmadAdamSeg s0{h->params + a.w_off, h->grads + a.w_off, h->m + a.w_off, h->v + a.w_off,
+                     h->dtype == MMAD_BF16 ? (void*)((char*)h->shadow + a.w_off * 2) : nullptr,
+                     (int64_t)a.Np * a.Kp, nullptr, 0, 0, 0, 0};
+      const int64_t nsmall = a.bn ? 3 * (int64_t)a.Np : a.Np;
+      MmadAdamSeg s1{h->params + a.b_off, h->grads + a.b_off, h->m + a.b_off, h->v + a.b_off,
+                     nullptr, nsmall, bs.src, bs.nparts, bs.stride, a.N, a.Np};
+      RET_IF(mmad_adam2(s0, s1, adam->b1, adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt,
+                        side));
+    }
+  }
+  // join the side stream back into the main stream
+  MMAD_HIP_CHECK(hipEventRecord(h->ev_join, side));
+  MMAD_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
+  return MMAD_OK;
+}
+
+// bias grads of every layer (when Adam did not finalise them) + the loss
+static int finish_reductions(mmad_ae* h, AeWS& w, bool biases, bool from_mse, float beta_kl,
+                             float* loss_out, hipStream_t st) {
+  MmadReduceJobs jobs{};
+  int n = 0, max_np = 1;
+  const int nL = (int)h->L.size();
+  if (biases) {
+    for (int l = 0; l < nL; ++l) {
+      const AeLayer& a = h->L[l];
+      const BiasSrc bs = bias_src(h, w, l, from_mse);
+      MmadReduceJob& j = jobs.j[n++];
+      j.src = bs.src;
+      j.dst = h->grads + a.b_off;
+      j.nparts = bs.nparts;
+      j.stride = bs.stride;
+      j.N = a.N;
+      j.Np = a.Np;
+      j.scale = 1.f;
+      max_np = a.Np > max_np ? a.Np : max_np;
+    }
+  }
+  if (loss_out) {
+    const AeLayer& last = h->L[nL - 1];
+    MmadReduceJob& j = jobs.j[n++];
+    j.scalar = 1;
+    j.src = w.l[nL - 1].stats + last.Np;   // slot 1: sum of d^2 per column
+    j.dst = loss_out;
+    j.nparts = w.Mpd / MMAD_PART_ROWS;
+    j.stride = 2 * last.Np;
+    j.N = last.N;
+    j.Np = last.Np;
+    j.scale = 1.f / (float)w.k;
+    if (h->vib) {
+      j.src2 = w.klpart;
+      j.n2 = (int)w.kl_parts;
+      j.scale2 = beta_kl;
+    }
+  }
+  if (n == 0) return MMAD_OK;
+  return mmad_reduce_jobs(jobs, n, max_np, st);
+}
+
+int mmad_ae_train_fwd_bwd(mmad_ae* h, const float* x, int ld_x, int B, int k, const float* eps,
+                          uint64_t seed, uint64_t offset, float beta_kl, float* loss_out,
+                          void* ws, int64_t ws_bytes, void* stream) {
+  MMAD_CHECK_ARG(h && h->params && h->grads && h->running, "ae_train: unbound handle");
+  MMAD_CHECK_ARG(x && ld_x >= h->L[0].K && loss_out, "ae_train: bad input");
+  AeWS w;
+  RET_IF(prepare_ws(h, B, k, ws, ws_bytes, w));
+  hipStream_t st = (hipStream_t)stream;
+  RET_IF(run_forward(h, w, x, ld_x, 0, eps, seed, offset, st));
+  RET_IF(run_backward(h, w, true, beta_kl, nullptr, st));
+  return finish_reductions(h, w, true, true, beta_kl, loss_out, st);
+}
+
+static AdamHyper adam_hyper(float lr, float b1, float b2, float eps, int step) {
+  const double bc1 = 1.0 - pow((double)b1, step);
+  const double bc2 = 1.0 - pow((double)b2, step);
+  return AdamHyper{b1, b2, eps, (float)(lr / bc1), (float)sqrt(bc2)};
+}
+
+int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const float* eps,
+                       uint64_t seed, uint64_t offset, float beta_kl, float lr, float beta1,
+                       float beta2, float adam_eps, int step, float* loss_out, void* ws,
+                       int64_t ws_bytes, void* stream) {
+  MMAD_CHECK_ARG(h && h->params && h->grads && h->running && h->m && h->v,
+                 "ae_train_step: unbound handle");
+  MMAD_CHECK_ARG(x && ld_x >= h->L[0].K && loss_out, "ae_train_step: bad input");
+  MMAD_CHECK_ARG(step >= 1, "ae_train_step: step must be >= 1");
+  AeWS w;
+  RET_IF(prepare_ws(h, B, k, ws, ws_bytes, w));
+  hipStream_t st = (hipStream_t)stream;
+  const AdamHyper ah = adam_hyper(lr, beta1, beta2, adam_eps, step);
+  RET_IF(run_forward(h, w, x, ld_x, 0, eps, seed, offset, st));
+  RET_IF(run_backward(h, w, true, beta_kl, &ah, st));
+  return finish_reductions(h, w, false, true, beta_kl, loss_out, st);
+}
+
+int mmad_ae_backward(mmad_ae* h, const float* dxhat, int ld, int B, void* ws, int64_t ws_bytes,
+                     void* stream) {
+  MMAD_CHECK_ARG(h && h->params && h->grads, "ae_backward: unbound handle");
+  MMAD_CHECK_ARG(!h->vib, "ae_backward: the VIB model trains through mmad_ae_train_fwd_bwd");
+  AeWS w;
+  RET_IF(prepare_ws(h, B, 1, ws, ws_bytes, w));
+  hipStream_t st = (hipStream_t)stream;
+  const int nL = (int)h->L.size();
+  const AeLayer& last = h->L[nL - 1];
+  LayerWS& s = w.l[nL - 1];
+  MMAD_CHECK_ARG(dxhat && ld >= last.N, "ae_backward: bad dxhat");
+  RET_IF(mmad_pack_input(h->dtype, B, last.N, w.Mpd, last.Np, dxhat, ld, s.dy, st));
+  RET_IF(mmad_matrix_colsum_partials(h->dtype, B, w.Mpd, last.Np, s.dy, s.dbpart, st));
+  RET_IF(run_backward(h, w, false, 0.f, nullptr, st));
+  return finish_reductions(h, w, true, false, 0.f, nullptr, st);
+}
+
+int mmad_ae_adam(mmad_ae* h, float lr, float beta1, float beta2, float eps, int step,
+                 void* stream) {
+  MMAD_CHECK_ARG(h && h->params && h->grads && h->m && h->v, "ae_adam: unbound handle");
+  MMAD_CHECK_ARG(step >= 1, "ae_adam: step must be >= 1");
+  const AdamHyper ah = adam_hyper(lr, beta1, beta2, eps, step);
+  return mmad_adam(h->n_params, h->params, h->grads, h->m, h->v, beta1, beta2, eps, ah.step_size,
+                   ah.bc2_sqrt, h->dtype == MMAD_BF16 ? h->shadow : nullptr,
+                   h->dtype == MMAD_BF16 ? h->n_weight : 0, stream);
+}
+
+int mmad_ae_forward(mmad_ae* h, const float* x, int ld_x, int B, int train_bn, float* x_hat,
+                    int ld_out, float* loss_out, void* ws, int64_t ws_bytes, void* stream) {
+  MMAD_CHECK_ARG(h && h->params && h->running, "ae_forward: unbound handle");
+  MMAD_CHECK_ARG(x && ld_x >= h->L[0].K, "ae_forward: bad input");
+  AeWS w;
+  RET_IF(prepare_ws(h, B, 1, ws, ws_bytes, w));
+  hipStream_t st = (hipStream_t)stream;
+  RET_IF(run_forward(h, w, x, ld_x, train_bn ? 2 : 1, nullptr, 0x5eed, 0, st));
+  const AeLayer& last = h->L.back();
+  const void* xh = w.l.back().out;
+  if (x_hat) RET_IF(mmad_unpack_output(h->dtype, B, last.N, last.Np, xh, x_hat, ld_out, st));
+  if (loss_out) {
+    RET_IF(mmad_sse_partials(h->dtype, B, last.N, last.Np, xh, x, ld_x, w.misc, 256, st));
+    RET_IF(mmad_sum(256, w.misc, 1.f, loss_out, 0, st));
+  }
+  return MMAD_OK;
+}
+
+int mmad_ae_score(mmad_ae* h, const float* x, int ld_x, int B, float* layer_sq, float* diffs,
+                  void* ws, int64_t ws_bytes, void* stream) {
+  MMAD_CHECK_ARG(h && h->params && h->running, "ae_score: unbound handle");
+  MMAD_CHECK_ARG(x && ld_x >= h->L[0].K && layer_sq, "ae_score: bad args");
+  AeWS w;
+  RET_IF(prepare_ws(h, B, 1, ws, ws_bytes, w));
+  hipStream_t st = (hipStream_t)stream;
+  const int dt = h->dtype;
+  const int nL = (int)h->L.size();
+  RET_IF(mmad_pack_input(dt, B, h->L[0].K, w.Mpe, h->L[0].Kp, x, ld_x, w.xin, st));
+  int ld_diff = h->L[0].K;
+  for (int e = 0; e < h->n_enc; ++e) ld_diff += h->L[e].N;
+  // pass 1: eval forward; the decoder's last layer scores d0 = x_hat - x
+  for (int l = 0; l < nL; ++l) {
+    const AeLayer& a = h->L[l];
+    LayerWS& s = w.l[l];
+    const int M = rows_of(w, a), Mp = prows_of(w, a);
+    const float *isc, *ish;
+    const void* in = input_of(h, w, l, false, &isc, &ish);
+    GemmEpi ep = fwd_epi(h, a, M, a.bn ? s.y : s.out, nullptr, nullptr);
+    if (a.bn) {
+      RET_IF(mmad_bn_eval_affine(a.N, a.Np, h->params + a.g_off, h->params + a.be_off,
+                                 running_mean(h, a), running_var(h, a), h->bn_eps, s.scale,
+                                 s.shift, st));
+      ep.bn_scale = s.scale;
+      ep.bn_shift = s.shift;
+    }
+    if (l == nL - 1) {
+      ep.ref = w.xin;
+      ep.ldref = a.Np;
+      ep.rowsq = s.rowsq;
+      ep.ldrow = Mp;
+      ep.diff = diffs;
+      ep.lddiff = ld_diff;
+      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_SCORE, in, a.Kp, weights(h, a), a.Kp, Mp, a.Np, a.Kp,
+                                ep, st));
+    } else {
+      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_FWD, in, a.Kp, weights(h, a), a.Kp, Mp, a.Np, a.Kp,
+                                ep, st));
+    }
+    if (h->vib && l == h->n_enc - 1) {
+      RET_IF(mmad_vib_reparam_fwd(dt, B, h->btl, 1, s.out, a.Np, nullptr, nullptr, 0, 0, 1, w.zbuf,
+                                  h->L[h->n_enc].Kp, nullptr, st));
+    }
+  }
+  // pass 2: x_hat through the encoder, diff against pass-1 activations
+  const void* cur = w.l[nL - 1].out;
+  int coff = h->L[0].K;
+  for (int e = 0; e < h->n_enc; ++e) {
+    const AeLayer& a = h->L[e];
+    LayerWS& s = w.l[e];
+    GemmEpi ep = fwd_epi(h, a, B, s.dy, nullptr, nullptr);
+    if (a.bn) {
+      ep.bn_scale = s.scale;
+      ep.bn_shift = s.shift;
+    }
+    ep.ref = a.bn ? s.y : s.out;
+    ep.ldref = a.Np;
+    ep.rowsq = s.rowsq;
+    ep.ldrow = w.Mpe;
+    ep.diff = diffs ? diffs + coff : nullptr;
+    ep.lddiff = ld_diff;
+    RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_SCORE, cur, a.Kp, weights(h, a), a.Kp, w.Mpe, a.Np,
+                              a.Kp, ep, st));
+    coff += a.N;
+    cur = s.dy;
+  }
+  // per-window sums: layer_sq[0] from the decoder's last layer, [1+e] from pass 2
+  MmadReduceJobs jobs{};
+  const AeLayer& last = h->L[nL - 1];
+  jobs.j[0] = MmadReduceJob{w.l[nL - 1].rowsq, layer_sq, last.Np / 128, w.Mpd, B, B, 1.f, 0,
+                            nullptr, 0, 0.f};
+  for (int e = 0; e < h->n_enc; ++e)
+    jobs.j[e + 1] = MmadReduceJob{w.l[e].rowsq, layer_sq + (size_t)(e + 1) * B, h->L[e].Np / 128,
+                                  w.Mpe, B, B, 1.f, 0, nullptr, 0, 0.f};
+  MMAD_CHECK_ARG(h->n_enc + 1 <= MMAD_MAX_REDUCE_JOBS, "too many encoder layers");
+  return mmad_reduce_jobs(jobs, h->n_enc + 1, B, st);
+}

@@ -31,6 +31,16 @@ struct GemmEpi {
   int ldrow;
   float* diff;           // SCORE optional fp32 diff output
   int lddiff;
+  // BatchNorm normalise-on-load (train mode: y = a*scale + shift per feature)
+  const float* a_scale;  // A operand (K-major), indexed by k (nullable)
+  const float* a_shift;
+  const float* b_scale;  // B operand (MN-major), indexed by n (nullable)
+  const float* b_shift;
+  // BWD_DATA: BatchNorm-backward column partials of the produced dy
+  const void* bn_a;      // pre-BN activation, same shape/ld as out (nullable)
+  const float* bn_mean;
+  const float* bn_rstd;
+  float* bn_part;        // [Mp/64][2][ldo]: (sum dy, sum dy*xhat)
 };
 
 int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,

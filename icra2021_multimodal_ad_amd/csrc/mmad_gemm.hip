@@ -129,6 +129,22 @@ __device__ __forceinline__ floatx4 frag_f32(const char* img, int rbase, int kc, 
   }
 }
 
+// y = x*scale + shift on one 16-byte chunk (BatchNorm normalise-on-load)
+template <typename T>
+__device__ __forceinline__ void chunk_affine(uint4v& r, const float* sc, const float* sh) {
+  if constexpr (sizeof(T) == 2) {
+    bf16x8 v = __builtin_bit_cast(bf16x8, r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] * sc[e] + sh[e]);
+    r = __builtin_bit_cast(uint4v, v);
+  } else {
+    floatx4 v = __builtin_bit_cast(floatx4, r);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = v[e] * sc[e] + sh[e];
+    r = __builtin_bit_cast(uint4v, v);
+  }
+}
+
 }  // namespace
 
 // -------------------------------------------------------------------------
@@ -141,8 +157,9 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
   using IB = Img<T, BK_, BN>;
   constexpr int STAGE = IA::BYTES + IB::BYTES;
   constexpr int OSTRIDE = BN * (int)sizeof(TO) + 16;
-  constexpr int OBYTES = BM * OSTRIDE;
+  constexpr int OBYTES = BM * OSTRIDE + (EPI == GEMM_EPI_BWD_DATA ? 2 * 256 * 4 : 0);
   constexpr int LDS_BYTES = (2 * STAGE > OBYTES) ? 2 * STAGE : OBYTES;
+  constexpr int EPC = 16 / (int)sizeof(T);
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -156,9 +173,39 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  // BatchNorm normalise-on-load: every A chunk of a thread spans the same 8
+  // (bf16) / 4 (f32) k of a stage; every B chunk the same n of the block.
+  const bool atr = AK && ep.a_scale != nullptr;
+  const bool btr = !BK_ && ep.b_scale != nullptr;
+  float sa[EPC], ta[EPC], sb[EPC], tb[EPC];
+  auto load_a_affine = [&](int k0) {
+    if (atr) {
+      const int kb = k0 + (tid & 7) * EPC;
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) { sa[e] = ep.a_scale[kb + e]; ta[e] = ep.a_shift[kb + e]; }
+    }
+  };
+  if (btr) {
+    const int nb = n0 + (tid % IB::CPR) * EPC;
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) { sb[e] = ep.b_scale[nb + e]; tb[e] = ep.b_shift[nb + e]; }
+  }
   uint4v ra[IA::CHUNKS], rb[IB::CHUNKS];
+  auto transform = [&]() {
+    if (atr) {
+#pragma unroll
+      for (int i = 0; i < IA::CHUNKS; ++i) chunk_affine<T>(ra[i], sa, ta);
+    }
+    if (btr) {
+#pragma unroll
+      for (int i = 0; i < IB::CHUNKS; ++i) chunk_affine<T>(rb[i], sb, tb);
+    }
+  };
+
   stage_load<T, AK, BM>(ra, A, lda, m0, 0, tid);
   stage_load<T, BK_, BN>(rb, B, ldb, n0, 0, tid);
+  load_a_affine(0);
+  transform();
   stage_store<T, AK, BM>(smem, ra, tid);
   stage_store<T, BK_, BN>(smem + IA::BYTES, rb, tid);
   __syncthreads();
@@ -169,6 +216,7 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
     if (t + 1 < nt) {
       stage_load<T, AK, BM>(ra, A, lda, m0, (t + 1) * IA::BK, tid);
       stage_load<T, BK_, BN>(rb, B, ldb, n0, (t + 1) * IA::BK, tid);
+      load_a_affine((t + 1) * IA::BK);
     }
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
@@ -202,6 +250,7 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
       }
     }
     if (t + 1 < nt) {
+      transform();
       char* na = smem + ((t + 1) & 1) * STAGE;
       stage_store<T, AK, BM>(na, ra, tid);
       stage_store<T, BK_, BN>(na + IA::BYTES, rb, tid);
@@ -301,7 +350,7 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
       }
   __syncthreads();
   constexpr int CPR = BN * (int)sizeof(TO) / 16;  // 16-byte chunks per output row
-  constexpr int EPC = 16 / (int)sizeof(TO);
+  constexpr int OEPC = 16 / (int)sizeof(TO);
   constexpr int ITERS = BM * CPR / 256;
   TO* out = (TO*)ep.out;
 #pragma unroll
@@ -310,7 +359,7 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
     const int rl = idx / CPR, ch = idx % CPR;
     const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
     const int row = m0 + rl;
-    const int col = n0 + ch * EPC;
+    const int col = n0 + ch * OEPC;
     *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
     if (EPI == GEMM_EPI_SCORE) {
       const TO* ref = (const TO*)ep.ref + (size_t)row * ep.ldref + col;
@@ -318,21 +367,60 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
       const TO* pv = (const TO*)&v;
       const TO* pr = (const TO*)&rv;
       float sq = 0.f;
-      float dd[EPC];
+      float dd[OEPC];
 #pragma unroll
-      for (int e = 0; e < EPC; ++e) {
+      for (int e = 0; e < OEPC; ++e) {
         dd[e] = to_f32<TO>(pv[e]) - to_f32<TO>(pr[e]);
         sq += dd[e] * dd[e];
       }
       if (ep.diff && row < ep.M) {
         float* dp = ep.diff + (size_t)row * ep.lddiff + col;
 #pragma unroll
-        for (int e = 0; e < EPC; ++e)
+        for (int e = 0; e < OEPC; ++e)
           if (col + e < ep.N) dp[e] = dd[e];
       }
 #pragma unroll
       for (int o = 1; o < CPR; o <<= 1) sq += __shfl_xor(sq, o);
       if (ch == 0) ep.rowsq[(size_t)blockIdx.x * ep.ldrow + row] = sq;
+    }
+  }
+  if constexpr (EPI == GEMM_EPI_BWD_DATA) {
+    if (ep.bn_part) {
+      // sum over rows of dy and dy*xhat, xhat = (a - mean)*rstd, per 64-row chunk
+      constexpr int NG = 256 / BN;   // thread groups per column
+      constexpr int RPG = BM / NG;   // rows per group
+      constexpr int GPP = RPG >= 64 ? 1 : 64 / RPG;
+      const int cc = tid % BN, grp = tid / BN;
+      const int col = n0 + cc;
+      const float mu = ep.bn_mean[col], rs = ep.bn_rstd[col];
+      const TO* an = (const TO*)ep.bn_a;
+      float s1 = 0.f, s2 = 0.f;
+      for (int r = 0; r < RPG; ++r) {
+        const int rl = grp * RPG + r;
+        const float dy = to_f32<TO>(*(const TO*)(smem + rl * OSTRIDE + cc * (int)sizeof(TO)));
+        const float av = to_f32<TO>(an[(size_t)(m0 + rl) * ep.ldo + col]);
+        s1 += dy;
+        s2 += dy * (av - mu) * rs;
+      }
+      float* scr = (float*)(smem + BM * OSTRIDE);
+      if constexpr (GPP == 1) {
+        float* pp = ep.bn_part + (size_t)((m0 + grp * RPG) / 64) * 2 * ep.ldo;
+        pp[col] = s1;
+        pp[ep.ldo + col] = s2;
+      } else {
+        scr[grp * BN + cc] = s1;
+        scr[256 + grp * BN + cc] = s2;
+        __syncthreads();
+        if (grp % GPP == 0) {
+          for (int q = 1; q < GPP; ++q) {
+            s1 += scr[(grp + q) * BN + cc];
+            s2 += scr[256 + (grp + q) * BN + cc];
+          }
+          float* pp = ep.bn_part + (size_t)((m0 + grp * RPG) / 64) * 2 * ep.ldo;
+          pp[col] = s1;
+          pp[ep.ldo + col] = s2;
+        }
+      }
     }
   }
 }

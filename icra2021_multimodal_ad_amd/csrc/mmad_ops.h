@@ -10,3 +10,37 @@ int mmad_sse_partials(int dtype, int M, int N, int Np, const void* y, const floa
                       float* part, int nparts, void* stream);
 int mmad_to_bf16(int64_t n, const float* x, void* y, void* stream);
 int64_t mmad_vib_kl_parts(int B, int k, int ld_z);
+
+#define MMAD_MAX_REDUCE_JOBS 24
+struct MmadReduceJob {
+  const float* src;   // partials, row i at src + i*stride
+  float* dst;         // [Np] (column job) or [1] (scalar job)
+  int nparts, stride, N, Np;
+  float scale;
+  int scalar;         // 1: dst[0] = scale*sum(all) + scale2*sum(src2[0:n2])
+  const float* src2;
+  int n2;
+  float scale2;
+};
+struct MmadReduceJobs { MmadReduceJob j[MMAD_MAX_REDUCE_JOBS]; };
+int mmad_reduce_jobs(const MmadReduceJobs& jobs, int n_jobs, int max_np, void* stream);
+
+// One Adam segment.  If bsrc != null the first bNp elements take their
+// gradient from bias partials: g[e] = sum_i bsrc[i*bstride + e] (e < bN,
+// else 0), written back to g (the bias grad is finalised inside the update).
+struct MmadAdamSeg {
+  float* p; float* g; float* m; float* v; void* shadow; int64_t n;
+  const float* bsrc; int bparts, bstride, bN, bNp;
+};
+int mmad_adam2(const MmadAdamSeg& s0, const MmadAdamSeg& s1, float beta1, float beta2, float eps,
+               float step_size, float bc2_sqrt, void* stream);
+
+int mmad_bn_finalize(int M, int N, int Mp, int Np, const float* stats, const float* gamma,
+                     const float* beta, float* running_mean, float* running_var, float momentum,
+                     float eps, float* save_mean, float* save_rstd, float* scale, float* shift,
+                     void* stream);
+int mmad_bn_act_bwd_apply(int dtype, int act, float slope, int M, int N, int Mp, int Np,
+                          const void* dy, const void* a, const float* save_mean,
+                          const float* save_rstd, const float* gamma, const float* part,
+                          int nparts, void* dz, float* dgamma, float* dbeta, float* db_partials,
+                          void* stream);

@@ -119,6 +119,37 @@ __global__ __launch_bounds__(256) void bn_train_apply_k(int M, int N, int Np, co
   }
 }
 
+// Train-mode BN finalize only: batch mean/rstd, per-column affine for the
+// consumers' normalise-on-load, running-stat update.  One block per 64 cols.
+__global__ __launch_bounds__(256) void bn_finalize_k(int M, int N, int Np, const float* __restrict__ stats,
+                                                     int nparts, const float* gamma, const float* beta,
+                                                     float* rmean, float* rvar, float momentum,
+                                                     float eps, float* save_mean, float* save_rstd,
+                                                     float* scale, float* shift) {
+  __shared__ float s_mean[SLAB_COLS], s_var[SLAB_COLS];
+  const int n0 = blockIdx.x * SLAB_COLS, tid = threadIdx.x;
+  merge_welford(M, nparts, stats, Np, n0, s_mean, s_var);
+  if (tid < SLAB_COLS) {
+    const int col = n0 + tid;
+    if (col < N) {
+      const float rstd = rsqrtf(s_var[tid] + eps);
+      const float sc = gamma[col] * rstd;
+      save_mean[col] = s_mean[tid];
+      save_rstd[col] = rstd;
+      scale[col] = sc;
+      shift[col] = beta[col] - s_mean[tid] * sc;
+      const float unb = M > 1 ? s_var[tid] * (float)M / (float)(M - 1) : s_var[tid];
+      rmean[col] = (1.f - momentum) * rmean[col] + momentum * s_mean[tid];
+      rvar[col] = (1.f - momentum) * rvar[col] + momentum * unb;
+    } else {
+      save_mean[col] = 0.f;
+      save_rstd[col] = 0.f;
+      scale[col] = 0.f;
+      shift[col] = 0.f;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // BN(train) + activation backward.  Pass 1: per-slab partial sums of dy and
 // dy*xhat.  Pass 2: finalise dgamma/dbeta, dz, and db partials.
@@ -395,6 +426,79 @@ __global__ void to_bf16_k(int64_t n, const float* __restrict__ x, bf16* __restri
 }
 
 // ---------------------------------------------------------------------------
+// One launch for all end-of-backward reductions (bias grads, loss): job j,
+// block x covers 256 output columns; scalar jobs run in block x == 0 only.
+__global__ __launch_bounds__(256) void reduce_jobs_k(MmadReduceJobs jobs) {
+  const MmadReduceJob& jb = jobs.j[blockIdx.y];
+  const int tid = threadIdx.x;
+  if (jb.scalar) {
+    if (blockIdx.x != 0) return;
+    __shared__ float red[4];
+    float t = 0.f;
+    for (int i = 0; i < jb.nparts; ++i)
+      for (int c = tid; c < jb.N; c += 256) t += jb.src[(size_t)i * jb.stride + c];
+    t *= jb.scale;
+    float t2 = 0.f;
+    for (int c = tid; c < jb.n2; c += 256) t2 += jb.src2[c];
+    t += jb.scale2 * t2;
+    t = wave_sum(t);
+    if ((tid & 63) == 0) red[tid >> 6] = t;
+    __syncthreads();
+    if (tid == 0) jb.dst[0] = red[0] + red[1] + red[2] + red[3];
+    return;
+  }
+  const int j = blockIdx.x * 256 + tid;
+  if (j >= jb.Np) return;
+  float t = 0.f;
+  if (j < jb.N)
+    for (int i = 0; i < jb.nparts; ++i) t += jb.src[(size_t)i * jb.stride + j];
+  jb.dst[j] = jb.scale * t;
+}
+
+// Adam over two flat segments (a layer's weights and its bias/gamma/beta)
+__global__ __launch_bounds__(256) void adam2_k(MmadAdamSeg s0, MmadAdamSeg s1, float b1, float b2,
+                                               float eps, float step_size, float bc2_sqrt) {
+  int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  const MmadAdamSeg* sg = &s0;
+  if (i4 >= s0.n) { i4 -= s0.n; sg = &s1; }
+  if (i4 >= sg->n) return;
+  float* p = sg->p + i4;
+  float* g = sg->g + i4;
+  float* m = sg->m + i4;
+  float* v = sg->v + i4;
+  floatx4 gg;
+  if (sg->bsrc && i4 < sg->bNp) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = (int)i4 + k;
+      float t = 0.f;
+      if (e < sg->bN)
+        for (int i = 0; i < sg->bparts; ++i) t += sg->bsrc[(size_t)i * sg->bstride + e];
+      gg[k] = t;
+    }
+    *(floatx4*)g = gg;
+  } else {
+    gg = *(const floatx4*)g;
+  }
+  floatx4 pp = *(floatx4*)p, mm = *(floatx4*)m, vv = *(floatx4*)v;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    mm[k] = b1 * mm[k] + (1.f - b1) * gg[k];
+    vv[k] = b2 * vv[k] + (1.f - b2) * gg[k] * gg[k];
+    pp[k] = pp[k] - step_size * (mm[k] / (sqrtf(vv[k]) / bc2_sqrt + eps));
+  }
+  *(floatx4*)p = pp;
+  *(floatx4*)m = mm;
+  *(floatx4*)v = vv;
+  if (sg->shadow) {
+    bf16x4 sh;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sh[k] = (bf16)pp[k];
+    *(bf16x4*)((bf16*)sg->shadow + i4) = sh;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Philox4x32-10 counter-based RNG -> N(0,1) via Box-Muller
 __device__ __forceinline__ void philox_round(uint32_t (&c)[4], uint32_t k0, uint32_t k1) {
   const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
@@ -521,6 +625,57 @@ int mmad_bn_train_apply(int dtype, int M, int N, int Mp, int Np, const void* a, 
     bn_train_apply_k<float><<<grd, 256, 0, s>>>(M, N, Np, (const float*)a, stats, nparts, gamma,
                                                 beta, running_mean, running_var, momentum, eps,
                                                 save_mean, save_rstd, (float*)y);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_bn_finalize(int M, int N, int Mp, int Np, const float* stats, const float* gamma,
+                     const float* beta, float* running_mean, float* running_var, float momentum,
+                     float eps, float* save_mean, float* save_rstd, float* scale, float* shift,
+                     void* stream) {
+  MMAD_CHECK_ARG(Mp % 128 == 0 && Np % 128 == 0 && M >= 1 && M <= Mp && N <= Np,
+                 "bn_finalize: bad sizes");
+  bn_finalize_k<<<Np / SLAB_COLS, 256, 0, (hipStream_t)stream>>>(
+      M, N, Np, stats, Mp / MMAD_PART_ROWS, gamma, beta, running_mean, running_var, momentum, eps,
+      save_mean, save_rstd, scale, shift);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_reduce_jobs(const MmadReduceJobs& jobs, int n_jobs, int max_np, void* stream) {
+  MMAD_CHECK_ARG(n_jobs >= 1 && n_jobs <= MMAD_MAX_REDUCE_JOBS, "reduce_jobs: bad job count");
+  dim3 grd((max_np + 255) / 256, n_jobs);
+  reduce_jobs_k<<<grd, 256, 0, (hipStream_t)stream>>>(jobs);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_adam2(const MmadAdamSeg& s0, const MmadAdamSeg& s1, float beta1, float beta2, float eps,
+               float step_size, float bc2_sqrt, void* stream) {
+  MMAD_CHECK_ARG(s0.n % 4 == 0 && s1.n % 4 == 0, "adam2: segment lengths must be multiples of 4");
+  const int64_t n4 = (s0.n + s1.n) / 4;
+  if (n4 == 0) return MMAD_OK;
+  adam2_k<<<nblk(n4, 256), 256, 0, (hipStream_t)stream>>>(s0, s1, beta1, beta2, eps, step_size,
+                                                          bc2_sqrt);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_bn_act_bwd_apply(int dtype, int act, float slope, int M, int N, int Mp, int Np,
+                          const void* dy, const void* a, const float* save_mean,
+                          const float* save_rstd, const float* gamma, const float* part,
+                          int nparts, void* dz, float* dgamma, float* dbeta, float* db_partials,
+                          void* stream) {
+  dim3 grd(Np / SLAB_COLS, Mp / SLAB_ROWS);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMAD_BF16)
+    bn_bwd_apply_k<bf16><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const bf16*)dy,
+                                             (const bf16*)a, save_mean, save_rstd, gamma, part,
+                                             (bf16*)dz, dgamma, dbeta, db_partials);
+  else
+    bn_bwd_apply_k<float><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const float*)dy,
+                                              (const float*)a, save_mean, save_rstd, gamma, part,
+                                              (float*)dz, dgamma, dbeta, db_partials);
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
 }

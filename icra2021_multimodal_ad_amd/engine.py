@@ -179,6 +179,28 @@ class NativeAE:
              int(seed), int(offset), float(beta_kl), ptr(loss_out), ws, nb, stream_ptr())
         return loss_out
 
+    def train_step_fused(self, x, lr=1e-3, betas=(0.9, 0.999), adam_eps=1e-8, k=1, eps=None,
+                         seed=0, offset=0, beta_kl=0.0, loss_out=None):
+        """Whole step with per-layer Adam overlapped on the side stream
+        (mmad_ae_train_step); returns the device loss tensor [1]."""
+        self._require(x)
+        x = self._as_input(x, self.enc_widths[0])
+        B = x.shape[0]
+        self.sync_shadow()
+        ws, nb = self.workspace(B, k)
+        if loss_out is None:
+            loss_out = torch.empty(1, device=self.device, dtype=torch.float32)
+        if eps is not None:
+            eps = eps.contiguous().float()
+            assert eps.numel() == k * B * self.btl
+        self.adam_step_count += 1
+        call("mmad_ae_train_step", self._h, ptr(x), x.stride(0), B, int(k), ptr(eps), int(seed),
+             int(offset), float(beta_kl), float(lr), float(betas[0]), float(betas[1]),
+             float(adam_eps), int(self.adam_step_count), ptr(loss_out), ws, nb, stream_ptr())
+        if self.shadow is not None:
+            self._synced_version = self.params._version
+        return loss_out
+
     def backward(self, dxh, B):
         """loss.backward() after forward(train_bn=True) on the same workspace."""
         self._require(dxh)

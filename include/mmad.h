@@ -194,6 +194,19 @@ int mmad_ae_train_fwd_bwd(mmad_ae* h, const float* x, int ld_x, int B, int k, co
                           uint64_t seed, uint64_t offset, float beta_kl, float* loss_out,
                           void* ws, int64_t ws_bytes, void* stream);
 
+/* One whole AutoEncoder.step (models/auto_encoder.py:57-77) with
+ * optimizer.step() fused in: forward + sum-MSE + backward as in
+ * mmad_ae_train_fwd_bwd, and each layer's Adam update (hyper-parameters as
+ * mmad_ae_adam, step = t) issued on the executor's side stream right after
+ * that layer's dW GEMM, overlapping the rest of the backward.  Single-process
+ * only (with data parallelism use train_fwd_bwd + all-reduce + mmad_ae_adam).
+ * On return every kernel is enqueued and ordered before later work on
+ * `stream`. */
+int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const float* eps,
+                       uint64_t seed, uint64_t offset, float beta_kl, float lr, float beta1,
+                       float beta2, float adam_eps, int step, float* loss_out, void* ws,
+                       int64_t ws_bytes, void* stream);
+
 /* loss.backward() after mmad_ae_forward(train_bn=1) on the same workspace
  * (autograd path of AutoEncoder.forward): dxhat fp32 [B][ld] = dL/dx_hat;
  * writes all parameter gradients.  Not for the VIB model. */

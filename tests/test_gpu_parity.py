@@ -290,3 +290,21 @@ def test_full_size_properties_bf16():
         gw = nat.grads[L["w_off"]: L["w_off"] + L["Np"] * L["Kp"]].view(L["Np"], L["Kp"])
         assert float(w[L["N"]:].abs().sum() + w[:, L["K"]:].abs().sum()) == 0.0
         assert float(gw[L["N"]:].abs().sum() + gw[:, L["K"]:].abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_fused_step_equals_unfused(dtype):
+    """mmad_ae_train_step (per-layer Adam on the side stream, overlapped with
+    the backward) == train_fwd_bwd followed by one flat Adam."""
+    sd = init_state_dict(192, 16, 5, seed=31)
+    ma, _ = _model(192, 16, 5, sd, dtype=dtype)
+    mb, _ = _model(192, 16, 5, sd, dtype=dtype)
+    for s in range(3):
+        x = torch.from_numpy(synth_windows(200, 192, seed=40 + s)).cuda()
+        la = ma._native.train_step_fused(x)
+        lb = mb._native.train_step(x)
+        mb._native.adam()
+        assert float(la) == float(lb)
+    torch.cuda.synchronize()
+    assert torch.allclose(ma._native.params, mb._native.params, atol=1e-6, rtol=0)
+    assert torch.equal(ma._native.running, mb._native.running)
