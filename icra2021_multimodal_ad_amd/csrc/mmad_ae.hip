@@ -59,7 +59,7 @@ struct LayerWS {
 struct AeWS {
   int B, k, Mpe, Mpd;
   void *xin, *zbuf, *dzin;
-  float *eps, *klpart, *misc;
+  float *eps, *klpart, *misc, *lossp;
   int64_t kl_parts;
   std::vector<LayerWS> l;
   int64_t bytes;
@@ -94,6 +94,10 @@ static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
     w.klpart = (float*)take(w.kl_parts * 4);
   }
   w.misc = (float*)take(1024 * 4);
+  {
+    const AeLayer& last = h->L[nL - 1];
+    w.lossp = (float*)take((int64_t)(w.Mpd / 64) * (last.Np / 64) * 4);
+  }
   w.l.resize(nL);
   for (int i = 0; i < nL; ++i) {
     const AeLayer& a = h->L[i];
@@ -209,7 +213,10 @@ int mmad_ae_bind(mmad_ae* h, float* params, float* grads, float* adam_m, float* 
   h->shadow = shadow;
   h->running = running;
   if (!h->side) {
-    MMAD_HIP_CHECK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+    // lowest priority: the side stream fills CUs the critical chain leaves idle
+    int least = 0, greatest = 0;
+    MMAD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    MMAD_HIP_CHECK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, least));
     const size_t n = h->L.size();
     h->ev_fork.resize(n);
     h->ev_data.resize(n);
@@ -306,6 +313,7 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
       ep.ldt = ld_x;
       ep.tmod = B;
       ep.gscale = 2.0f / (float)k;
+      ep.lossp = w.lossp;
       RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_MSE, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
     } else if (a.bn && train) {
       GemmEpi ep = fwd_epi(h, a, M, s.out, isc, ish);
@@ -366,18 +374,18 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     const void* dz = (l == nL - 1) ? (from_mse ? s.out : s.dy) : (a.bn ? s.dz : s.dy);
     const float *isc, *ish;
     const void* in = input_of(h, w, l, true, &isc, &ish);
-    // fork: dz_l (and every small grad of layer l) is complete on the main stream
-    MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
-    MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
-    {
-      GemmEpi ep{};
-      ep.M = a.Np;
-      ep.N = a.Kp;
-      ep.out = h->grads + a.w_off;
-      ep.ldo = a.Kp;
-      ep.b_scale = isc;
-      ep.b_shift = ish;
-      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, ep,
+    GemmEpi dwe{};
+    dwe.M = a.Np;
+    dwe.N = a.Kp;
+    dwe.out = h->grads + a.w_off;
+    dwe.ldo = a.Kp;
+    dwe.b_scale = isc;
+    dwe.b_shift = ish;
+    if (!adam) {
+      // fork: dz_l is complete on the main stream; dW_l overlaps the chain below
+      MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
+      MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
+      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe,
                                 side));
     }
     if (l > 0) {
@@ -404,6 +412,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
         ep.bn_part = ps.bnpart;
         RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
                                   a.Np, ep, st));
+        if (adam) MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
         RET_IF(mmad_bn_act_bwd_apply(dt, p.act, h->slope, rows_of(w, p), p.N, Mpp, p.Np, ps.dy,
                                      ps.out, ps.mean, ps.rstd, h->params + p.g_off, ps.bnpart,
                                      Mpp / 64, ps.dz, h->grads + p.g_off, h->grads + p.be_off,
@@ -416,18 +425,34 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       }
     }
     if (adam) {
-      // W_l is free once the main stream has finished reading it (bwd-data of l)
-      MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
+      // dW_l with this layer's Adam update fused into its epilogue.  It rewrites
+      // W_l, so it starts only once the main stream has finished reading W_l
+      // (bwd-data of l); the rest of the chain keeps overlapping it.
+      if (l == 0 || !(h->L[l - 1].bn) || (h->vib && l == h->n_enc))
+        MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
       MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_data[l], 0));
       const BiasSrc bs = bias_src(h, w, l, from_mse);
-      MmadAdamSeg s0{h->params + a.w_off, h->grads + a.w_off, h->m + a.w_off, h->v + a.w_off,
-                     h->dtype == MMAD_BF16 ? (void*)((char*)h->shadow + a.w_off * 2) : nullptr,
-                     (int64_t)a.Np * a.Kp, nullptr, 0, 0, 0, 0};
-      const int64_t nsmall = a.bn ? 3 * (int64_t)a.Np : a.Np;
-      MmadAdamSeg s1{h->params + a.b_off, h->grads + a.b_off, h->m + a.b_off, h->v + a.b_off,
-                     nullptr, nsmall, bs.src, bs.nparts, bs.stride, a.N, a.Np};
-      RET_IF(mmad_adam2(s0, s1, adam->b1, adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt,
-                        side));
+      dwe.ad_p = h->params + a.w_off;
+      dwe.ad_m = h->m + a.w_off;
+      dwe.ad_v = h->v + a.w_off;
+      dwe.ad_shadow = h->dtype == MMAD_BF16 ? (void*)((char*)h->shadow + a.w_off * 2) : nullptr;
+      dwe.ad_b1 = adam->b1;
+      dwe.ad_b2 = adam->b2;
+      dwe.ad_eps = adam->eps;
+      dwe.ad_step = adam->step_size;
+      dwe.ad_bc2 = adam->bc2_sqrt;
+      dwe.sm_p = h->params + a.b_off;
+      dwe.sm_g = h->grads + a.b_off;
+      dwe.sm_m = h->m + a.b_off;
+      dwe.sm_v = h->v + a.b_off;
+      dwe.sm_n = a.bn ? 3 * a.Np : a.Np;
+      dwe.sm_bsrc = bs.src;
+      dwe.sm_bparts = bs.nparts;
+      dwe.sm_bstride = bs.stride;
+      dwe.sm_bN = a.N;
+      dwe.sm_bNp = a.Np;
+      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe,
+                                side));
     }
   }
   // join the side stream back into the main stream
@@ -461,12 +486,12 @@ static int finish_reductions(mmad_ae* h, AeWS& w, bool biases, bool from_mse, fl
     const AeLayer& last = h->L[nL - 1];
     MmadReduceJob& j = jobs.j[n++];
     j.scalar = 1;
-    j.src = w.l[nL - 1].stats + last.Np;   // slot 1: sum of d^2 per column
+    j.src = w.lossp;                        // one sum of d^2 per MSE-GEMM block
     j.dst = loss_out;
-    j.nparts = w.Mpd / MMAD_PART_ROWS;
-    j.stride = 2 * last.Np;
-    j.N = last.N;
-    j.Np = last.Np;
+    j.nparts = 1;
+    j.stride = 0;
+    j.N = mmad_gemm_grid_blocks(w.Mpd, last.Np, GEMM_EPI_MSE);
+    j.Np = j.N;
     j.scale = 1.f / (float)w.k;
     if (h->vib) {
       j.src2 = w.klpart;

@@ -41,7 +41,28 @@ struct GemmEpi {
   const float* bn_mean;
   const float* bn_rstd;
   float* bn_part;        // [Mp/64][2][ldo]: (sum dy, sum dy*xhat)
+  // MSE: one loss partial (sum d^2) per block, index blockIdx.y*gridDim.x+blockIdx.x
+  float* lossp;
+  // BWD_WEIGHT: torch.optim.Adam step fused into the epilogue (nullable p).
+  // Weight tile: p/m/v share the dW layout (ld = ldo); shadow gets bf16(p).
+  float* ad_p;
+  float* ad_m;
+  float* ad_v;
+  void* ad_shadow;
+  float ad_b1, ad_b2, ad_eps, ad_step, ad_bc2;
+  // ... and the layer's small segment [bias | gamma | beta], spread over all
+  // blocks; the first bNp elements take g = sum of bias partials.
+  float* sm_p;
+  float* sm_g;
+  float* sm_m;
+  float* sm_v;
+  int sm_n;
+  const float* sm_bsrc;
+  int sm_bparts, sm_bstride, sm_bN, sm_bNp;
 };
+
+// blocks of the grid mmad_gemm_dispatch launches for this problem
+int mmad_gemm_grid_blocks(int Mp, int Np, int epi);
 
 int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,
                        int Np, int K, const GemmEpi& ep, hipStream_t s);

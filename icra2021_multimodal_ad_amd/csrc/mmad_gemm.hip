@@ -338,6 +338,24 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
 
   // ===================== epilogue, LDS-staged coalesced store ===============
   __syncthreads();  // main-loop LDS no longer read
+  if constexpr (EPI == GEMM_EPI_MSE) {
+    if (ep.lossp) {
+      // one loss partial per block: sum of d^2 = sum (dz/gscale)^2 over the tile
+      float lt = 0.f;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) lt += acc[i][j][r] * acc[i][j][r];
+      lt = wave_sum(lt) / (ep.gscale * ep.gscale);
+      float* red = (float*)smem;
+      if (lane == 0) red[w] = lt;
+      __syncthreads();
+      if (tid == 0) ep.lossp[blockIdx.y * gridDim.x + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+      __syncthreads();
+    }
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -361,6 +379,30 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
     const int row = m0 + rl;
     const int col = n0 + ch * OEPC;
     *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
+    if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
+      if (ep.ad_p) {
+        // torch.optim.Adam on this dW chunk (4 fp32), same formula as adam_k
+        const size_t off = (size_t)row * ep.ldo + col;
+        floatx4 gg = __builtin_bit_cast(floatx4, v);
+        floatx4 pp = *(floatx4*)(ep.ad_p + off), mm = *(floatx4*)(ep.ad_m + off);
+        floatx4 vv = *(floatx4*)(ep.ad_v + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          mm[e] = ep.ad_b1 * mm[e] + (1.f - ep.ad_b1) * gg[e];
+          vv[e] = ep.ad_b2 * vv[e] + (1.f - ep.ad_b2) * gg[e] * gg[e];
+          pp[e] = pp[e] - ep.ad_step * (mm[e] / (sqrtf(vv[e]) / ep.ad_bc2 + ep.ad_eps));
+        }
+        *(floatx4*)(ep.ad_p + off) = pp;
+        *(floatx4*)(ep.ad_m + off) = mm;
+        *(floatx4*)(ep.ad_v + off) = vv;
+        if (ep.ad_shadow) {
+          bf16x4 sh;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sh[e] = (bf16)pp[e];
+          *(bf16x4*)((bf16*)ep.ad_shadow + off) = sh;
+        }
+      }
+    }
     if (EPI == GEMM_EPI_SCORE) {
       const TO* ref = (const TO*)ep.ref + (size_t)row * ep.ldref + col;
       const uint4v rv = *(const uint4v*)ref;
@@ -382,6 +424,40 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
 #pragma unroll
       for (int o = 1; o < CPR; o <<= 1) sq += __shfl_xor(sq, o);
       if (ch == 0) ep.rowsq[(size_t)blockIdx.x * ep.ldrow + row] = sq;
+    }
+  }
+  if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
+    if (ep.ad_p && ep.sm_p) {
+      // the layer's bias/gamma/beta Adam, 4 elements per thread, spread over the grid
+      const int nb = gridDim.x * gridDim.y;
+      const int b = blockIdx.y * gridDim.x + blockIdx.x;
+      for (int q = b * 256 + tid; q * 4 < ep.sm_n; q += nb * 256) {
+        const int i4 = q * 4;
+        floatx4 gg;
+        if (ep.sm_bsrc && i4 < ep.sm_bNp) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float t = 0.f;
+            if (i4 + e < ep.sm_bN)
+              for (int i = 0; i < ep.sm_bparts; ++i) t += ep.sm_bsrc[(size_t)i * ep.sm_bstride + i4 + e];
+            gg[e] = t;
+          }
+          *(floatx4*)(ep.sm_g + i4) = gg;
+        } else {
+          gg = *(const floatx4*)(ep.sm_g + i4);
+        }
+        floatx4 pp = *(floatx4*)(ep.sm_p + i4), mm = *(floatx4*)(ep.sm_m + i4);
+        floatx4 vv = *(floatx4*)(ep.sm_v + i4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          mm[e] = ep.ad_b1 * mm[e] + (1.f - ep.ad_b1) * gg[e];
+          vv[e] = ep.ad_b2 * vv[e] + (1.f - ep.ad_b2) * gg[e] * gg[e];
+          pp[e] = pp[e] - ep.ad_step * (mm[e] / (sqrtf(vv[e]) / ep.ad_bc2 + ep.ad_eps));
+        }
+        *(floatx4*)(ep.sm_p + i4) = pp;
+        *(floatx4*)(ep.sm_m + i4) = mm;
+        *(floatx4*)(ep.sm_v + i4) = vv;
+      }
     }
   }
   if constexpr (EPI == GEMM_EPI_BWD_DATA) {
@@ -451,6 +527,14 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
   }
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
+}
+
+int mmad_gemm_grid_blocks(int Mp, int Np, int epi) {
+  switch (mmad_pick_tile(Mp, Np, epi)) {
+    case 0: return (Mp / 128) * (Np / 128);
+    case 1: return (Mp / 64) * (Np / 128);
+    default: return (Mp / 64) * (Np / 64);
+  }
 }
 
 int mmad_pick_tile(int Mp, int Np, int epi) {

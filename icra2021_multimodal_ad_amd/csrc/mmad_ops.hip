@@ -121,25 +121,62 @@ __global__ __launch_bounds__(256) void bn_train_apply_k(int M, int N, int Np, co
 
 // Train-mode BN finalize only: batch mean/rstd, per-column affine for the
 // consumers' normalise-on-load, running-stat update.  One block per 64 cols.
-__global__ __launch_bounds__(256) void bn_finalize_k(int M, int N, int Np, const float* __restrict__ stats,
-                                                     int nparts, const float* gamma, const float* beta,
-                                                     float* rmean, float* rvar, float momentum,
-                                                     float eps, float* save_mean, float* save_rstd,
-                                                     float* scale, float* shift) {
-  __shared__ float s_mean[SLAB_COLS], s_var[SLAB_COLS];
-  const int n0 = blockIdx.x * SLAB_COLS, tid = threadIdx.x;
-  merge_welford(M, nparts, stats, Np, n0, s_mean, s_var);
+// 1024 threads = 16 chunk groups x 64 columns; each group merges its chunks
+// (loads issued back to back), then 64 threads merge the 16 group results.
+__global__ __launch_bounds__(1024) void bn_finalize_k(int M, int N, int Np, const float* __restrict__ stats,
+                                                      int nparts, const float* gamma, const float* beta,
+                                                      float* rmean, float* rvar, float momentum,
+                                                      float eps, float* save_mean, float* save_rstd,
+                                                      float* scale, float* shift) {
+  constexpr int G = 16;
+  __shared__ float pm[G][SLAB_COLS], pq[G][SLAB_COLS], pn[G][SLAB_COLS];
+  const int n0 = blockIdx.x * SLAB_COLS, tid = threadIdx.x, c = tid & 63, grp = tid >> 6;
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  for (int i0 = grp; i0 < nparts; i0 += 4 * G) {
+    float mb[4], qb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * G;
+      mb[u] = i < nparts ? stats[(size_t)i * 2 * Np + n0 + c] : 0.f;
+      qb[u] = i < nparts ? stats[((size_t)i * 2 + 1) * Np + n0 + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * G;
+      int cnt = M - i * MMAD_PART_ROWS;
+      cnt = cnt < 0 ? 0 : (cnt > MMAD_PART_ROWS ? MMAD_PART_ROWS : cnt);
+      if (i >= nparts || cnt == 0) continue;
+      const float nb = (float)cnt, nn = n + nb, d = mb[u] - mean;
+      mean += d * (nb / nn);
+      m2 += qb[u] + d * d * (n * nb / nn);
+      n = nn;
+    }
+  }
+  pm[grp][c] = mean;
+  pq[grp][c] = m2;
+  pn[grp][c] = n;
+  __syncthreads();
   if (tid < SLAB_COLS) {
+    float n1 = 0.f, mu = 0.f, q = 0.f;
+    for (int g = 0; g < G; ++g) {
+      const float nb = pn[g][tid];
+      if (nb == 0.f) continue;
+      const float nn = n1 + nb, d = pm[g][tid] - mu;
+      mu += d * (nb / nn);
+      q += pq[g][tid] + d * d * (n1 * nb / nn);
+      n1 = nn;
+    }
+    const float var = n1 > 0.f ? q / n1 : 0.f;
     const int col = n0 + tid;
     if (col < N) {
-      const float rstd = rsqrtf(s_var[tid] + eps);
+      const float rstd = rsqrtf(var + eps);
       const float sc = gamma[col] * rstd;
-      save_mean[col] = s_mean[tid];
+      save_mean[col] = mu;
       save_rstd[col] = rstd;
       scale[col] = sc;
-      shift[col] = beta[col] - s_mean[tid] * sc;
-      const float unb = M > 1 ? s_var[tid] * (float)M / (float)(M - 1) : s_var[tid];
-      rmean[col] = (1.f - momentum) * rmean[col] + momentum * s_mean[tid];
+      shift[col] = beta[col] - mu * sc;
+      const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+      rmean[col] = (1.f - momentum) * rmean[col] + momentum * mu;
       rvar[col] = (1.f - momentum) * rvar[col] + momentum * unb;
     } else {
       save_mean[col] = 0.f;
@@ -635,7 +672,7 @@ int mmad_bn_finalize(int M, int N, int Mp, int Np, const float* stats, const flo
                      void* stream) {
   MMAD_CHECK_ARG(Mp % 128 == 0 && Np % 128 == 0 && M >= 1 && M <= Mp && N <= Np,
                  "bn_finalize: bad sizes");
-  bn_finalize_k<<<Np / SLAB_COLS, 256, 0, (hipStream_t)stream>>>(
+  bn_finalize_k<<<Np / SLAB_COLS, 1024, 0, (hipStream_t)stream>>>(
       M, N, Np, stats, Mp / MMAD_PART_ROWS, gamma, beta, running_mean, running_var, momentum, eps,
       save_mean, save_rstd, scale, shift);
   MMAD_LAUNCH_CHECK();
