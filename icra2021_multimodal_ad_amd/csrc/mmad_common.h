@@ -70,6 +70,30 @@ __device__ __forceinline__ float act_grad_from_out(float a, int act, float slope
   }
 }
 
+// torch.optim.Adam element update (single-tensor formula, amsgrad=False):
+// m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= step * m / (sqrt(v)/bc2 + eps).
+// Contractions pinned with fmaf so every kernel that fuses an Adam update
+// (flat Adam, dW-epilogue Adam) produces bit-identical results.
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float b1,
+                                          float b2, float eps, float step, float bc2) {
+  m = fmaf(b1, m, (1.f - b1) * g);
+  v = fmaf(b2, v, ((1.f - b2) * g) * g);
+  const float denom = __fsqrt_rn(v) / bc2 + eps;
+  p = fmaf(-step, __fdiv_rn(m, denom), p);
+}
+
+__device__ __forceinline__ void adam4(floatx4& p, floatx4& m, floatx4& v, floatx4 g, float b1,
+                                      float b2, float eps, float step, float bc2) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float pe = p[e], me = m[e], ve = v[e];
+    adam_elem(pe, me, ve, g[e], b1, b2, eps, step, bc2);
+    p[e] = pe;
+    m[e] = me;
+    v[e] = ve;
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

@@ -30,18 +30,29 @@
 
 namespace {
 
-template <typename T> struct Esz { static constexpr int v = sizeof(T); };
+// bytes of K per LDS row per stage (BK = MMAD_KB / sizeof(T))
+#ifndef MMAD_KB
+#define MMAD_KB 256
+#endif
 
 template <typename T, bool KMAJ, int ROWS>
 struct Img {
   static constexpr int ES = sizeof(T);
-  static constexpr int BK = 128 / ES;                       // K per stage
+  static constexpr int KB = MMAD_KB;
+  static constexpr int BK = KB / ES;                            // K per stage
   static constexpr int PADB = (ES == 2) ? 32 : 16;
-  static constexpr int STRIDE = KMAJ ? 128 : ROWS * ES + PADB;  // bytes per LDS row
-  static constexpr int BYTES = KMAJ ? ROWS * 128 : BK * (ROWS * ES + PADB);
-  static constexpr int CHUNKS = ROWS * 8 / 256;              // 16 B chunks per thread
-  static constexpr int CPR = ROWS * ES / 16;                 // MN-major: chunks per k-row
+  static constexpr int STRIDE = KMAJ ? KB : ROWS * ES + PADB;   // bytes per LDS row
+  static constexpr int BYTES = KMAJ ? ROWS * KB : BK * (ROWS * ES + PADB);
+  static constexpr int CHUNKS = ROWS * KB / 16 / 256;           // 16 B chunks per thread
+  static constexpr int CPR = ROWS * ES / 16;                    // MN-major: chunks per k-row
+  static constexpr int CPRK = KB / 16;                          // K-major: chunks per row
 };
+
+// K-major image swizzle (16-byte chunk units): conflict-free fragment reads
+// for 128-byte rows (rows pair up in the 64 banks) and >= 256-byte rows.
+__device__ __forceinline__ constexpr int kswz(int row) {
+  return MMAD_KB == 128 ? ((row >> 1) & 7) : (row & 15);
+}
 
 // global -> registers for one stage of one operand
 template <typename T, bool KMAJ, int ROWS>
@@ -54,7 +65,7 @@ __device__ __forceinline__ void stage_load(uint4v* r,
     int c = tid + 256 * i;
     const T* p;
     if (KMAJ) {
-      int row = c >> 3, j = c & 7;
+      int row = c / I::CPRK, j = c % I::CPRK;
       p = G + (size_t)(r0 + row) * ld + k0 + j * EPC;
     } else {
       int kr = c / I::CPR, j = c % I::CPR;
@@ -73,8 +84,8 @@ __device__ __forceinline__ void stage_store(char* img, const uint4v* r,
     int c = tid + 256 * i;
     int off;
     if (KMAJ) {
-      int row = c >> 3, j = c & 7;
-      off = row * 128 + ((j ^ ((row >> 1) & 7)) << 4);
+      int row = c / I::CPRK, j = c % I::CPRK;
+      off = row * I::KB + ((j ^ kswz(row)) << 4);
     } else {
       int kr = c / I::CPR, j = c % I::CPR;
       off = kr * I::STRIDE + (j << 4);
@@ -90,11 +101,11 @@ __device__ __forceinline__ bf16x8 frag_bf16(const char* img, int rbase, int kk, 
   const int g = lane >> 4;
   if (KMAJ) {
     const int m = rbase + (lane & 15);
-    const int f = ((m >> 1) & 7) << 1;        // swizzle in 8-byte units
+    const int f = kswz(m) << 1;        // swizzle in 8-byte units
     const int c1 = (kk * 8 + g) ^ f;
     const int c2 = (kk * 8 + 4 + g) ^ f;
-    bf16x4 lo = *(const bf16x4*)(img + m * 128 + c1 * 8);
-    bf16x4 hi = *(const bf16x4*)(img + m * 128 + c2 * 8);
+    bf16x4 lo = *(const bf16x4*)(img + m * I::KB + c1 * 8);
+    bf16x4 hi = *(const bf16x4*)(img + m * I::KB + c2 * 8);
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   } else {
     const int q = (lane >> 2) & 3, p = lane & 3;
@@ -118,8 +129,8 @@ __device__ __forceinline__ floatx4 frag_f32(const char* img, int rbase, int kc, 
   const int g = lane >> 4;
   if (KMAJ) {
     const int m = rbase + (lane & 15);
-    const int j = (kc * 4 + g) ^ ((m >> 1) & 7);
-    return *(const floatx4*)(img + m * 128 + j * 16);
+    const int j = (kc * 4 + g) ^ kswz(m);
+    return *(const floatx4*)(img + m * I::KB + j * 16);
   } else {
     const int col = rbase + (lane & 15);
     floatx4 r;
@@ -180,7 +191,7 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
   float sa[EPC], ta[EPC], sb[EPC], tb[EPC];
   auto load_a_affine = [&](int k0) {
     if (atr) {
-      const int kb = k0 + (tid & 7) * EPC;
+      const int kb = k0 + (tid % IA::CPRK) * EPC;
 #pragma unroll
       for (int e = 0; e < EPC; ++e) { sa[e] = ep.a_scale[kb + e]; ta[e] = ep.a_shift[kb + e]; }
     }
@@ -220,7 +231,7 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
     }
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
+      for (int kk = 0; kk < IA::BK / 32; ++kk) {
         bf16x8 fa[MI], fb[NI];
 #pragma unroll
         for (int i = 0; i < MI; ++i) fa[i] = frag_bf16<AK, BM>(sa, wm * 16 * MI + i * 16, kk, lane);
@@ -234,7 +245,7 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
       }
     } else {
 #pragma unroll
-      for (int kc = 0; kc < 2; ++kc) {
+      for (int kc = 0; kc < IA::BK / 16; ++kc) {
         floatx4 fa[MI], fb[NI];
 #pragma unroll
         for (int i = 0; i < MI; ++i) fa[i] = frag_f32<AK, BM>(sa, wm * 16 * MI + i * 16, kc, lane);
@@ -386,12 +397,7 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
         floatx4 gg = __builtin_bit_cast(floatx4, v);
         floatx4 pp = *(floatx4*)(ep.ad_p + off), mm = *(floatx4*)(ep.ad_m + off);
         floatx4 vv = *(floatx4*)(ep.ad_v + off);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          mm[e] = ep.ad_b1 * mm[e] + (1.f - ep.ad_b1) * gg[e];
-          vv[e] = ep.ad_b2 * vv[e] + (1.f - ep.ad_b2) * gg[e] * gg[e];
-          pp[e] = pp[e] - ep.ad_step * (mm[e] / (sqrtf(vv[e]) / ep.ad_bc2 + ep.ad_eps));
-        }
+        adam4(pp, mm, vv, gg, ep.ad_b1, ep.ad_b2, ep.ad_eps, ep.ad_step, ep.ad_bc2);
         *(floatx4*)(ep.ad_p + off) = pp;
         *(floatx4*)(ep.ad_m + off) = mm;
         *(floatx4*)(ep.ad_v + off) = vv;
@@ -448,12 +454,7 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
         }
         floatx4 pp = *(floatx4*)(ep.sm_p + i4), mm = *(floatx4*)(ep.sm_m + i4);
         floatx4 vv = *(floatx4*)(ep.sm_v + i4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          mm[e] = ep.ad_b1 * mm[e] + (1.f - ep.ad_b1) * gg[e];
-          vv[e] = ep.ad_b2 * vv[e] + (1.f - ep.ad_b2) * gg[e] * gg[e];
-          pp[e] = pp[e] - ep.ad_step * (mm[e] / (sqrtf(vv[e]) / ep.ad_bc2 + ep.ad_eps));
-        }
+        adam4(pp, mm, vv, gg, ep.ad_b1, ep.ad_b2, ep.ad_eps, ep.ad_step, ep.ad_bc2);
         *(floatx4*)(ep.sm_p + i4) = pp;
         *(floatx4*)(ep.sm_m + i4) = mm;
         *(floatx4*)(ep.sm_v + i4) = vv;

@@ -254,13 +254,24 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
   constexpr int RG = 256 / CPR;
   __shared__ float s_db[SLAB_COLS], s_dg[SLAB_COLS];
   __shared__ float s_red[RG][SLAB_COLS];
+  __shared__ float s_p1[4][SLAB_COLS], s_p2[4][SLAB_COLS];
   const int n0 = blockIdx.x * SLAB_COLS, r0 = blockIdx.y * SLAB_ROWS, tid = threadIdx.x;
-  if (tid < SLAB_COLS) {
+  {
+    // 4 groups of 64 threads split the partial rows (independent loads)
+    const int c = tid & 63, grp = tid >> 6;
     float t1 = 0.f, t2 = 0.f;
-    for (int i = 0; i < nparts; ++i) {
-      t1 += part[((size_t)i * 2) * Np + n0 + tid];
-      t2 += part[((size_t)i * 2 + 1) * Np + n0 + tid];
+#pragma unroll 4
+    for (int i = grp; i < nparts; i += 4) {
+      t1 += part[((size_t)i * 2) * Np + n0 + c];
+      t2 += part[((size_t)i * 2 + 1) * Np + n0 + c];
     }
+    s_p1[grp][c] = t1;
+    s_p2[grp][c] = t2;
+  }
+  __syncthreads();
+  if (tid < SLAB_COLS) {
+    float t1 = s_p1[0][tid] + s_p1[1][tid] + s_p1[2][tid] + s_p1[3][tid];
+    float t2 = s_p2[0][tid] + s_p2[1][tid] + s_p2[2][tid] + s_p2[3][tid];
     const int col = n0 + tid;
     if (col >= N) { t1 = 0.f; t2 = 0.f; }
     s_db[tid] = t1;
@@ -429,13 +440,7 @@ __global__ __launch_bounds__(256) void adam_k(int64_t n, float* __restrict__ p,
   if (i4 + 4 <= n) {
     floatx4 pp = *(floatx4*)(p + i4), gg = *(const floatx4*)(g + i4);
     floatx4 mm = *(floatx4*)(m + i4), vv = *(floatx4*)(v + i4);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      mm[k] = b1 * mm[k] + (1.f - b1) * gg[k];
-      vv[k] = b2 * vv[k] + (1.f - b2) * gg[k] * gg[k];
-      const float denom = sqrtf(vv[k]) / bc2_sqrt + eps;
-      pp[k] = pp[k] - step_size * (mm[k] / denom);
-    }
+    adam4(pp, mm, vv, gg, b1, b2, eps, step_size, bc2_sqrt);
     *(floatx4*)(p + i4) = pp;
     *(floatx4*)(m + i4) = mm;
     *(floatx4*)(v + i4) = vv;
@@ -447,12 +452,12 @@ __global__ __launch_bounds__(256) void adam_k(int64_t n, float* __restrict__ p,
     }
   } else {
     for (int64_t i = i4; i < n; ++i) {
-      float mm = b1 * m[i] + (1.f - b1) * g[i];
-      float vv = b2 * v[i] + (1.f - b2) * g[i] * g[i];
+      float pp = p[i], mm = m[i], vv = v[i];
+      adam_elem(pp, mm, vv, g[i], b1, b2, eps, step_size, bc2_sqrt);
+      p[i] = pp;
       m[i] = mm;
       v[i] = vv;
-      p[i] = p[i] - step_size * (mm / (sqrtf(vv) / bc2_sqrt + eps));
-      if (shadow && i < n_shadow) shadow[i] = (bf16)p[i];
+      if (shadow && i < n_shadow) shadow[i] = (bf16)pp;
     }
   }
 }
@@ -518,12 +523,7 @@ __global__ __launch_bounds__(256) void adam2_k(MmadAdamSeg s0, MmadAdamSeg s1, f
     gg = *(const floatx4*)g;
   }
   floatx4 pp = *(floatx4*)p, mm = *(floatx4*)m, vv = *(floatx4*)v;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    mm[k] = b1 * mm[k] + (1.f - b1) * gg[k];
-    vv[k] = b2 * vv[k] + (1.f - b2) * gg[k] * gg[k];
-    pp[k] = pp[k] - step_size * (mm[k] / (sqrtf(vv[k]) / bc2_sqrt + eps));
-  }
+  adam4(pp, mm, vv, gg, b1, b2, eps, step_size, bc2_sqrt);
   *(floatx4*)p = pp;
   *(floatx4*)m = mm;
   *(floatx4*)v = vv;
