@@ -25,6 +25,7 @@ SIGNATURES = {
     "mmad_last_error_string": (ctypes.c_char_p, []),
     "mmad_abi_version": (_I, []),
     "mmad_pad_granule": (_I, []),
+    "mmad_tune_set": (_I, [_I, _I]),
     "mmad_fc_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P, _P, _P, _P, _P]),
     "mmad_fc_fwd_mse": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _F, _P, _P, _P]),
     "mmad_fc_fwd_score": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P, _P, _P, _P,

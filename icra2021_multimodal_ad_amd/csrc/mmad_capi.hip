@@ -29,12 +29,24 @@ const char* mmad_last_error_string(void) { return g_err; }
 int mmad_abi_version(void) { return MMAD_ABI_VERSION; }
 int mmad_pad_granule(void) { return MMAD_PAD; }
 
-int mmad_tile_override() {
-  static int v = [] {
-    const char* e = getenv("MMAD_GEMM_TILE");
-    return e ? atoi(e) : -1;
-  }();
-  return v;
+// tuning knobs (env defaults, overridable at run time through mmad_tune_set)
+static int g_tile = [] {
+  const char* e = getenv("MMAD_GEMM_TILE");
+  return e ? atoi(e) : -1;
+}();
+static int g_group = [] {
+  const char* e = getenv("MMAD_GEMM_GROUP_M");
+  return e ? atoi(e) : -1;
+}();
+int mmad_tile_override() { return g_tile; }
+int mmad_group_override() { return g_group; }
+
+int mmad_tune_set(int knob, int value) {
+  switch (knob) {
+    case 0: g_tile = value; return MMAD_OK;
+    case 1: g_group = value; return MMAD_OK;
+    default: mmad_set_error("tune_set: unknown knob %d", knob); return MMAD_EINVAL;
+  }
 }
 
 #define RET_IF(x)              \

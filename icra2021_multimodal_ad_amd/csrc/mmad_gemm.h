@@ -59,7 +59,11 @@ struct GemmEpi {
   int sm_n;
   const float* sm_bsrc;
   int sm_bparts, sm_bstride, sm_bN, sm_bNp;
+  // set by the launcher: XCD-aware grouped tile order
+  int tiles_n, group_m;
 };
+
+int mmad_group_override();
 
 // blocks of the grid mmad_gemm_dispatch launches for this problem
 int mmad_gemm_grid_blocks(int Mp, int Np, int epi);

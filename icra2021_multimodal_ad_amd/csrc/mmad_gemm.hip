@@ -175,7 +175,24 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  // XCD-aware tile order (1-D grid).  Under round-robin dispatch, blocks with
+  // equal bid % 8 share an XCD (speed only, never correctness); each such set
+  // gets a contiguous range of logical tiles, and logical tiles are grouped
+  // group_m M-tiles at a time, so every XCD works on a compact rectangle whose
+  // A/B panels stay in its 4 MB L2.
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  int tm, tn;
+  {
+    const int q = nblk >> 3, r = nblk & 7, xcd = bid & 7;
+    const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int tiles_m = nblk / ep.tiles_n;
+    const int per_group = ep.group_m * ep.tiles_n;
+    const int first_m = (wg / per_group) * ep.group_m;
+    const int gsz = min(tiles_m - first_m, ep.group_m);
+    tm = first_m + (wg % per_group) % gsz;
+    tn = (wg % per_group) / gsz;
+  }
+  const int m0 = tm * BM, n0 = tn * BN;
   const int nt = K / IA::BK;
 
   floatx4 acc[MI][NI];
@@ -363,7 +380,7 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
       float* red = (float*)smem;
       if (lane == 0) red[w] = lt;
       __syncthreads();
-      if (tid == 0) ep.lossp[blockIdx.y * gridDim.x + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+      if (tid == 0) ep.lossp[bid] = red[0] + red[1] + red[2] + red[3];
       __syncthreads();
     }
   }
@@ -429,14 +446,14 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
       }
 #pragma unroll
       for (int o = 1; o < CPR; o <<= 1) sq += __shfl_xor(sq, o);
-      if (ch == 0) ep.rowsq[(size_t)blockIdx.x * ep.ldrow + row] = sq;
+      if (ch == 0) ep.rowsq[(size_t)tn * ep.ldrow + row] = sq;
     }
   }
   if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
     if (ep.ad_p && ep.sm_p) {
       // the layer's bias/gamma/beta Adam, 4 elements per thread, spread over the grid
-      const int nb = gridDim.x * gridDim.y;
-      const int b = blockIdx.y * gridDim.x + blockIdx.x;
+      const int nb = nblk;
+      const int b = bid;
       for (int q = b * 256 + tid; q * 4 < ep.sm_n; q += nb * 256) {
         const int i4 = q * 4;
         floatx4 gg;
@@ -507,24 +524,30 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
 // -------------------------------------------------------------------------
 template <typename T, typename TO, bool AK, bool BK_, int EPI>
 static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np, int K,
-                        const GemmEpi& ep, int tile, hipStream_t s) {
+                        const GemmEpi& ep_in, int tile, hipStream_t s) {
   dim3 blk(256);
+  const int BM = tile == 0 ? 128 : 64, BN = tile == 2 ? 64 : 128;
+  const int tiles_m = Mp / BM, tiles_n = Np / BN, nblk = tiles_m * tiles_n;
+  GemmEpi ep = ep_in;
+  ep.tiles_n = tiles_n;
+  // group height balancing the per-XCD A-panel (gm*BM rows) and B-panel
+  // ((nblk/8/gm)*BN cols) footprints
+  const double per_xcd = nblk / 8.0;
+  int gm = (int)(sqrt(per_xcd * BN / BM) + 0.5);
+  const int env_gm = mmad_group_override();
+  if (env_gm > 0) gm = env_gm;
+  ep.group_m = gm < 1 ? 1 : (gm > tiles_m ? tiles_m : gm);
+  dim3 grd(nblk);
   switch (tile) {
-    case 0: {  // 128 x 128
-      dim3 grd(Np / 128, Mp / 128);
+    case 0:  // 128 x 128
       mmad_gemm_kernel<T, TO, AK, BK_, 4, 4, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep);
       break;
-    }
-    case 1: {  // 64 x 128
-      dim3 grd(Np / 128, Mp / 64);
+    case 1:  // 64 x 128
       mmad_gemm_kernel<T, TO, AK, BK_, 2, 4, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep);
       break;
-    }
-    default: {  // 64 x 64
-      dim3 grd(Np / 64, Mp / 64);
+    default:  // 64 x 64
       mmad_gemm_kernel<T, TO, AK, BK_, 2, 2, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep);
       break;
-    }
   }
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;

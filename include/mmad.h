@@ -43,6 +43,10 @@ enum { MMAD_ACT_NONE = 0, MMAD_ACT_LEAKYRELU = 1, MMAD_ACT_RELU = 2, MMAD_ACT_SI
 const char* mmad_last_error_string(void);
 int mmad_abi_version(void);
 int mmad_pad_granule(void);
+/* Tuning knobs (no reference counterpart): knob 0 = GEMM tile override
+ * (-1 auto, 0 = 128x128, 1 = 64x128, 2 = 64x64), knob 1 = XCD tile-group
+ * height override (-1 auto).  Defaults from MMAD_GEMM_TILE / MMAD_GEMM_GROUP_M. */
+int mmad_tune_set(int knob, int value);
 
 /* ------------------------------------------------------------------------
  * Layer operators
