@@ -1,0 +1,150 @@
+"""CPU-side checks of the C-ABI library and the host logic (no GPU compute)."""
+import ctypes
+import os
+import re
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "mmad.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    return re.findall(r"^\s*(?:const char\*|int64_t|size_t|void|int)\s+(mmad_\w+)\s*\(", src, re.M)
+
+
+def header_arg_counts():
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"(?:const char\*|int64_t|size_t|void|int)\s+(mmad_\w+)\s*\(([^;]*?)\);", src,
+                         re.S):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from icra2021_multimodal_ad_amd import _native
+    return _native.load()
+
+
+def test_library_exports_every_header_symbol(lib):
+    names = header_functions()
+    assert len(names) >= 30
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+def test_ctypes_signatures_match_header():
+    from icra2021_multimodal_ad_amd._native import SIGNATURES
+    counts = header_arg_counts()
+    assert set(SIGNATURES) == set(counts), set(SIGNATURES) ^ set(counts)
+    for n, (_, args) in SIGNATURES.items():
+        assert len(args) == counts[n], (n, len(args), counts[n])
+
+
+def test_abi_constants_and_errors(lib):
+    assert lib.mmad_abi_version() == 1
+    assert lib.mmad_pad_granule() == 128
+    # argument validation runs on the host and reports through the error string
+    rc = lib.mmad_fc_fwd(0, 10, 10, 10, 100, 128, 128, None, None, None, 0, 0.2, None, None, None,
+                         None, None)
+    assert rc == -1
+    assert b"multiples of 128" in lib.mmad_last_error_string()
+    assert lib.mmad_tune_set(7, 0) == -1
+
+
+def test_executor_layout_matches_reference_shapes(lib):
+    from icra2021_multimodal_ad_amd.engine import NativeAE
+    from icra2021_multimodal_ad_amd.common_utils import ae_widths
+    enc, dec = ae_widths(1728, 100, 5)
+    nat = NativeAE(enc, dec, dtype="bf16", device="cpu")
+    assert [L["N"] for L in nat.layers] == enc[1:] + dec[1:]
+    assert all(L["Kp"] % 128 == 0 and L["Np"] % 128 == 0 for L in nat.layers)
+    n_ref = sum(a * b + b for a, b in zip(enc[:-1], enc[1:])) + \
+        sum(a * b + b for a, b in zip(dec[:-1], dec[1:])) + 2 * (sum(enc[1:-1]) + sum(dec[1:-1]))
+    assert n_ref == 10225670                       # SURVEY §8 a2 probe
+    real = sum(v.numel() for l in range(10) for v in nat.param_views(nat.params, l) if v is not None)
+    assert real == n_ref
+    assert nat.workspace is not None
+    assert lib.mmad_ae_workspace_bytes(nat._h, 1024, 1) > 0
+    assert lib.mmad_ae_workspace_bytes(nat._h, 0, 1) == -1
+
+
+def test_model_surface_state_dict_roundtrip():
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    from icra2021_multimodal_ad_amd.common_utils import init_state_dict, state_dict_keys
+    cfg = types.SimpleNamespace(input_size=1728, btl_size=100, n_layers=5, gpu_id=-1)
+    m = get_model(cfg)
+    sd = m.state_dict()
+    assert len(sd) == 60                           # SURVEY §5 probe: 60 keys
+    assert list(sd.keys()) == state_dict_keys(5, "encoder") + state_dict_keys(5, "decoder")
+    ref = init_state_dict(1728, 100, 5, seed=3)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in ref.items()})
+    sd2 = m.state_dict()
+    for k, v in ref.items():
+        assert np.array_equal(sd2[k].numpy(), np.asarray(v)), k
+        assert sd2[k].is_contiguous()
+    # parameters are views of the flat native buffer
+    w = m.encoder.layer_list[0].layer.weight
+    assert w.data_ptr() == m._native.params.data_ptr()
+    assert len(m.encoder.layer_list) == 5 and m.encoder.layer_list[-1].bn is None
+    # the HIP path refuses to run without a GPU (no CPU fallback)
+    from icra2021_multimodal_ad_amd._native import NativeUnavailable
+    if not torch.cuda.is_available():
+        with pytest.raises(NativeUnavailable):
+            m(torch.zeros(4, 1728))
+
+
+def test_reference_error_behaviour():
+    from icra2021_multimodal_ad_amd.fc_module import FCModule, variational_info_bottleneck
+    with pytest.raises(Exception, match="Either batch_norm or dropout"):
+        FCModule(8, 4, [6], use_batch_norm=True, dropout_p=0.5)
+
+    class Dummy:
+        @variational_info_bottleneck
+        def forward(self, x):
+            return x
+    d = Dummy()
+    x = torch.zeros(2, 4)
+    assert d.forward(x) is x
+    with pytest.raises(ValueError):
+        d.forward(x, distribution="normal", k=0)
+    with pytest.raises(NotImplementedError):
+        d.forward(x, distribution="laplace")
+    from icra2021_multimodal_ad_amd.auto_encoder import AbstractModel
+    with pytest.raises(Exception, match="iterable"):
+        AbstractModel(3)
+
+
+def test_engine_loop_running_average():
+    from icra2021_multimodal_ad_amd.engine_loop import Engine, Events, RunningAverage
+    eng = Engine(lambda e, b: (float(b),))
+    RunningAverage(output_transform=lambda x: x[0]).attach(eng, "recon")
+    seen = []
+    eng.add_event_handler(Events.EPOCH_COMPLETED, lambda e: seen.append(e.state.metrics["recon"]))
+    eng.run([1.0, 2.0, 3.0], max_epochs=2)
+    v = 1.0
+    for b in (2.0, 3.0):
+        v = 0.98 * v + 0.02 * b
+    assert seen == pytest.approx([v, v])
+
+
+def test_data_generator_layout():
+    from icra2021_multimodal_ad_amd.data import synth_windows, synth_split, get_input_size
+    x = synth_windows(64, 1728, seed=0)
+    assert x.shape == (64, 1728) and x.dtype == np.float32
+    assert np.all(x[:, 1536:1600] == x[:, 1536:1537])          # F/T broadcast x64
+    assert np.all(x[:, 1600:1608] == x[:, 1600:1601])          # mic value repeated x8
+    assert np.array_equal(x, synth_windows(64, 1728, seed=0))  # seeded
+    sp = synth_split(100, 20, 64, seed=1)
+    assert len(sp["train"]) == 60 and len(sp["valid"]) == 20 and len(sp["test"]) == 40
+    assert sp["test_label"].sum() == 20
+    assert get_input_size(types.SimpleNamespace(sensor="All")) == 1728
+    assert get_input_size(types.SimpleNamespace(sensor="force_torque")) == 64
