@@ -30,92 +30,78 @@
 
 namespace {
 
-// bytes of K per LDS row per stage (BK = MMAD_KB / sizeof(T))
-#ifndef MMAD_KB
-#define MMAD_KB 256
-#endif
+// LDS images are lane-linear (global_load_lds writes wave base + lane*16), so
+// every bank-conflict swizzle is applied to the per-lane SOURCE address and
+// undone on the read side.  KB = bytes of K per LDS row per stage.
+constexpr int MMAD_KB = 128;
 
 template <typename T, bool KMAJ, int ROWS>
 struct Img {
   static constexpr int ES = sizeof(T);
   static constexpr int KB = MMAD_KB;
-  static constexpr int BK = KB / ES;                            // K per stage
-  static constexpr int PADB = (ES == 2) ? 32 : 16;
-  static constexpr int STRIDE = KMAJ ? KB : ROWS * ES + PADB;   // bytes per LDS row
-  static constexpr int BYTES = KMAJ ? ROWS * KB : BK * (ROWS * ES + PADB);
-  static constexpr int CHUNKS = ROWS * KB / 16 / 256;           // 16 B chunks per thread
-  static constexpr int CPR = ROWS * ES / 16;                    // MN-major: chunks per k-row
-  static constexpr int CPRK = KB / 16;                          // K-major: chunks per row
+  static constexpr int BK = KB / ES;                  // K per stage
+  static constexpr int RB = KMAJ ? KB : ROWS * ES;    // bytes per LDS row
+  static constexpr int BYTES = ROWS * KB;             // image bytes (both layouts)
+  static constexpr int CPROW = RB / 16;               // 16 B chunks per LDS row
+  static constexpr int CHUNKS = BYTES / 16 / 256;     // global_load_lds per thread
 };
 
-// K-major image swizzle (16-byte chunk units): conflict-free fragment reads
-// for 128-byte rows (rows pair up in the 64 banks) and >= 256-byte rows.
-__device__ __forceinline__ constexpr int kswz(int row) {
-  return MMAD_KB == 128 ? ((row >> 1) & 7) : (row & 15);
+// 16-byte-chunk XOR swizzle of LDS row `r` (an involution):
+//  * K-major, 128 B rows: (r>>1)&7 -> both ds_read_b64 fragment reads
+//    (bf16) / the ds_read_b128 read (f32) of a wave are conflict-free;
+//  * MN-major bf16, 256 B rows: (r&7)<<1; 128 B rows: ((r>>1)&3)<<1 ->
+//    ds_read_b64_tr_b16 of 8 consecutive k-rows hits all 64 banks once;
+//  * MN-major f32: r&7 (spreads the 4-row-apart ds_read_b32 groups).
+template <typename T, bool KMAJ, int RB>
+__device__ __forceinline__ int swz(int r) {
+  if constexpr (KMAJ) return (r >> 1) & 7;
+  else if constexpr (sizeof(T) == 2) return RB >= 256 ? ((r & 7) << 1) : (((r >> 1) & 3) << 1);
+  else return r & 7;
 }
 
-// global -> registers for one stage of one operand
+// issue one stage of one operand: global -> LDS, 16 B per lane, no registers
 template <typename T, bool KMAJ, int ROWS>
-__device__ __forceinline__ void stage_load(uint4v* r,
-                                           const T* __restrict__ G, int ld, int r0, int k0, int tid) {
+__device__ __forceinline__ void issue_stage(char* img, const T* __restrict__ G, int ld, int r0,
+                                            int k0, int tid, int w) {
   using I = Img<T, KMAJ, ROWS>;
-  constexpr int EPC = 16 / sizeof(T);  // elements per chunk
+  constexpr int EPC = 16 / sizeof(T);
 #pragma unroll
   for (int i = 0; i < I::CHUNKS; ++i) {
-    int c = tid + 256 * i;
-    const T* p;
-    if (KMAJ) {
-      int row = c / I::CPRK, j = c % I::CPRK;
-      p = G + (size_t)(r0 + row) * ld + k0 + j * EPC;
-    } else {
-      int kr = c / I::CPR, j = c % I::CPR;
-      p = G + (size_t)(k0 + kr) * ld + r0 + j * EPC;
-    }
-    r[i] = *(const uint4v*)p;
-  }
-}
-
-template <typename T, bool KMAJ, int ROWS>
-__device__ __forceinline__ void stage_store(char* img, const uint4v* r,
-                                            int tid) {
-  using I = Img<T, KMAJ, ROWS>;
-#pragma unroll
-  for (int i = 0; i < I::CHUNKS; ++i) {
-    int c = tid + 256 * i;
-    int off;
-    if (KMAJ) {
-      int row = c / I::CPRK, j = c % I::CPRK;
-      off = row * I::KB + ((j ^ kswz(row)) << 4);
-    } else {
-      int kr = c / I::CPR, j = c % I::CPR;
-      off = kr * I::STRIDE + (j << 4);
-    }
-    *(uint4v*)(img + off) = r[i];
+    const int p = 256 * i + tid;                       // LDS position (16 B units)
+    const int row = p / I::CPROW;
+    const int j = (p % I::CPROW) ^ swz<T, KMAJ, I::RB>(row);
+    const T* src = KMAJ ? G + (size_t)(r0 + row) * ld + k0 + j * EPC
+                        : G + (size_t)(k0 + row) * ld + r0 + j * EPC;
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (MMAD_LDS void*)(img + (256 * i + 64 * w) * 16), 16, 0, 0);
   }
 }
 
 // ---- bf16 fragment reads (16x16x32 MFMA operand, permuted k slots) ------
+// lane group g (= lane>>4) owns k = {4g..4g+3} U {16+4g..16+4g+3} of each
+// 32-deep step, in both operands, so the contraction is exact.
 template <bool KMAJ, int ROWS>
 __device__ __forceinline__ bf16x8 frag_bf16(const char* img, int rbase, int kk, int lane) {
   using I = Img<bf16, KMAJ, ROWS>;
   const int g = lane >> 4;
-  if (KMAJ) {
+  if constexpr (KMAJ) {
     const int m = rbase + (lane & 15);
-    const int f = kswz(m) << 1;        // swizzle in 8-byte units
+    const int f = swz<bf16, true, I::RB>(m) << 1;     // in 8-byte units
     const int c1 = (kk * 8 + g) ^ f;
     const int c2 = (kk * 8 + 4 + g) ^ f;
-    bf16x4 lo = *(const bf16x4*)(img + m * I::KB + c1 * 8);
-    bf16x4 hi = *(const bf16x4*)(img + m * I::KB + c2 * 8);
+    bf16x4 lo = *(const bf16x4*)(img + m * I::RB + c1 * 8);
+    bf16x4 hi = *(const bf16x4*)(img + m * I::RB + c2 * 8);
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   } else {
     const int q = (lane >> 2) & 3, p = lane & 3;
-    const int k1 = kk * 32 + 4 * g + q;
-    const int col = rbase + 4 * p;
+    const int k1 = kk * 32 + 4 * g + q, k2 = k1 + 16;
+    const int byte = (rbase + 4 * p) * 2;
+    const int j = byte >> 4, within = byte & 15;
     const MMAD_LDS char* base = (const MMAD_LDS char*)img;
     short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (MMAD_LDS short4v*)(base + k1 * I::STRIDE + col * 2));
+        (MMAD_LDS short4v*)(base + k1 * I::RB + ((j ^ swz<bf16, false, I::RB>(k1)) << 4) + within));
     short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (MMAD_LDS short4v*)(base + (k1 + 16) * I::STRIDE + col * 2));
+        (MMAD_LDS short4v*)(base + k2 * I::RB + ((j ^ swz<bf16, false, I::RB>(k2)) << 4) + within));
     bf16x4 l4 = __builtin_bit_cast(bf16x4, lo);
     bf16x4 h4 = __builtin_bit_cast(bf16x4, hi);
     return __builtin_shufflevector(l4, h4, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -127,50 +113,73 @@ template <bool KMAJ, int ROWS>
 __device__ __forceinline__ floatx4 frag_f32(const char* img, int rbase, int kc, int lane) {
   using I = Img<float, KMAJ, ROWS>;
   const int g = lane >> 4;
-  if (KMAJ) {
+  if constexpr (KMAJ) {
     const int m = rbase + (lane & 15);
-    const int j = (kc * 4 + g) ^ kswz(m);
-    return *(const floatx4*)(img + m * I::KB + j * 16);
+    const int j = (kc * 4 + g) ^ swz<float, true, I::RB>(m);
+    return *(const floatx4*)(img + m * I::RB + j * 16);
   } else {
     const int col = rbase + (lane & 15);
+    const int j = col >> 2, within = (col & 3) * 4;
     floatx4 r;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) r[s] = *(const float*)(img + (kc * 16 + 4 * g + s) * I::STRIDE + col * 4);
+    for (int s = 0; s < 4; ++s) {
+      const int k = kc * 16 + 4 * g + s;
+      r[s] = *(const float*)(img + k * I::RB + ((j ^ swz<float, false, I::RB>(k)) << 4) + within);
+    }
     return r;
   }
 }
 
-// y = x*scale + shift on one 16-byte chunk (BatchNorm normalise-on-load)
-template <typename T>
-__device__ __forceinline__ void chunk_affine(uint4v& r, const float* sc, const float* sh) {
-  if constexpr (sizeof(T) == 2) {
-    bf16x8 v = __builtin_bit_cast(bf16x8, r);
+__device__ __forceinline__ bf16x8 affine8(bf16x8 v, floatx4 s0, floatx4 s1, floatx4 t0, floatx4 t1) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] * sc[e] + sh[e]);
-    r = __builtin_bit_cast(uint4v, v);
-  } else {
-    floatx4 v = __builtin_bit_cast(floatx4, r);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = v[e] * sc[e] + sh[e];
-    r = __builtin_bit_cast(uint4v, v);
+  for (int e = 0; e < 4; ++e) {
+    v[e] = (bf16)((float)v[e] * s0[e] + t0[e]);
+    v[4 + e] = (bf16)((float)v[4 + e] * s1[e] + t1[e]);
   }
+  return v;
 }
+
+__device__ __forceinline__ bf16x8 affine8c(bf16x8 v, float s, float t) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] * s + t);
+  return v;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void block_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int MI, int NI> struct Ring { static constexpr int NS = (MI == 2 && NI == 4) ? 5 : 4; };
 
 }  // namespace
 
 // -------------------------------------------------------------------------
-template <typename T, typename TO, bool AK, bool BK_, int MI, int NI, int EPI>
-__global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__ A, int lda,
+// TR: BatchNorm normalise-on-load -- A operand (K-major, indexed by k) for the
+// forward GEMMs, B operand (MN-major, indexed by n) for the dW GEMM; applied
+// to the MFMA fragments right after the LDS read.
+template <typename T, typename TO, bool AK, bool BK_, int MI, int NI, int EPI, bool TR>
+__global__ __launch_bounds__(256, 1) void mmad_gemm_kernel(const T* __restrict__ A, int lda,
                                                             const T* __restrict__ B, int ldb, int K,
                                                             GemmEpi ep) {
   constexpr int BM = 32 * MI, BN = 32 * NI;
   using IA = Img<T, AK, BM>;
   using IB = Img<T, BK_, BN>;
-  constexpr int STAGE = IA::BYTES + IB::BYTES;
+  constexpr bool ATR = TR && AK;
+  constexpr bool BTR = TR && !BK_;
+  constexpr int NS = Ring<MI, NI>::NS;
+  constexpr int SLOT = IA::BYTES + IB::BYTES + (ATR ? 4096 : 0);
+  constexpr int NL = IA::CHUNKS + IB::CHUNKS + (ATR ? 1 : 0);   // vm ops per thread per stage
   constexpr int OSTRIDE = BN * (int)sizeof(TO) + 16;
   constexpr int OBYTES = BM * OSTRIDE + (EPI == GEMM_EPI_BWD_DATA ? 2 * 256 * 4 : 0);
-  constexpr int LDS_BYTES = (2 * STAGE > OBYTES) ? 2 * STAGE : OBYTES;
-  constexpr int EPC = 16 / (int)sizeof(T);
+  constexpr int LDS_BYTES = (NS * SLOT > OBYTES) ? NS * SLOT : OBYTES;
+  static_assert((NS - 2) * NL <= 63, "vmcnt range");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -201,51 +210,47 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // BatchNorm normalise-on-load: every A chunk of a thread spans the same 8
-  // (bf16) / 4 (f32) k of a stage; every B chunk the same n of the block.
-  const bool atr = AK && ep.a_scale != nullptr;
-  const bool btr = !BK_ && ep.b_scale != nullptr;
-  float sa[EPC], ta[EPC], sb[EPC], tb[EPC];
-  auto load_a_affine = [&](int k0) {
-    if (atr) {
-      const int kb = k0 + (tid % IA::CPRK) * EPC;
+  // B-side BatchNorm affine: one (scale, shift) per lane per n-tile, loaded
+  // (and waited for) before any LDS-DMA is in flight
+  float sbn[NI], tbn[NI];
+  if constexpr (BTR) {
 #pragma unroll
-      for (int e = 0; e < EPC; ++e) { sa[e] = ep.a_scale[kb + e]; ta[e] = ep.a_shift[kb + e]; }
+    for (int j = 0; j < NI; ++j) {
+      const int n = n0 + wn * 16 * NI + j * 16 + (lane & 15);
+      sbn[j] = ep.b_scale[n];
+      tbn[j] = ep.b_shift[n];
+      asm volatile("" ::"v"(sbn[j]), "v"(tbn[j]));
     }
-  };
-  if (btr) {
-    const int nb = n0 + (tid % IB::CPR) * EPC;
-#pragma unroll
-    for (int e = 0; e < EPC; ++e) { sb[e] = ep.b_scale[nb + e]; tb[e] = ep.b_shift[nb + e]; }
   }
-  uint4v ra[IA::CHUNKS], rb[IB::CHUNKS];
-  auto transform = [&]() {
-    if (atr) {
-#pragma unroll
-      for (int i = 0; i < IA::CHUNKS; ++i) chunk_affine<T>(ra[i], sa, ta);
-    }
-    if (btr) {
-#pragma unroll
-      for (int i = 0; i < IB::CHUNKS; ++i) chunk_affine<T>(rb[i], sb, tb);
+
+  auto issue = [&](int s) {
+    char* base = smem + (s % NS) * SLOT;
+    const int k0 = s * IA::BK;
+    issue_stage<T, AK, BM>(base, A, lda, m0, k0, tid, w);
+    issue_stage<T, BK_, BN>(base + IA::BYTES, B, ldb, n0, k0, tid, w);
+    if constexpr (ATR) {
+      // per-wave copy of [scale(k0..k0+BK) | shift(k0..k0+BK)] for the A-side affine
+      constexpr int Q = IA::BK / 4;
+      const float* src = lane < Q ? ep.a_scale + k0 + 4 * lane
+                                  : (lane < 2 * Q ? ep.a_shift + k0 + 4 * (lane - Q) : ep.a_scale + k0);
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (MMAD_LDS void*)(base + IA::BYTES + IB::BYTES + w * 1024), 16,
+                                       0, 0);
     }
   };
 
-  stage_load<T, AK, BM>(ra, A, lda, m0, 0, tid);
-  stage_load<T, BK_, BN>(rb, B, ldb, n0, 0, tid);
-  load_a_affine(0);
-  transform();
-  stage_store<T, AK, BM>(smem, ra, tid);
-  stage_store<T, BK_, BN>(smem + IA::BYTES, rb, tid);
-  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nt) issue(s);
 
   for (int t = 0; t < nt; ++t) {
-    char* sa = smem + (t & 1) * STAGE;
-    char* sb = sa + IA::BYTES;
-    if (t + 1 < nt) {
-      stage_load<T, AK, BM>(ra, A, lda, m0, (t + 1) * IA::BK, tid);
-      stage_load<T, BK_, BN>(rb, B, ldb, n0, (t + 1) * IA::BK, tid);
-      load_a_affine((t + 1) * IA::BK);
-    }
+    if (t + NS - 2 < nt) wait_vmcnt<(NS - 2) * NL>();
+    else wait_vmcnt<0>();
+    block_barrier();                       // stage t landed for every wave; slot t-1 free
+    if (t + NS - 1 < nt) issue(t + NS - 1);
+    const char* sa = smem + (t % NS) * SLOT;
+    const char* sb = sa + IA::BYTES;
+    const char* sc = sb + IB::BYTES + w * 1024;   // this wave's affine copy (ATR)
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
       for (int kk = 0; kk < IA::BK / 32; ++kk) {
@@ -254,6 +259,19 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
         for (int i = 0; i < MI; ++i) fa[i] = frag_bf16<AK, BM>(sa, wm * 16 * MI + i * 16, kk, lane);
 #pragma unroll
         for (int j = 0; j < NI; ++j) fb[j] = frag_bf16<BK_, BN>(sb, wn * 16 * NI + j * 16, kk, lane);
+        if constexpr (ATR) {
+          const int g4 = (lane >> 4) * 4;
+          const floatx4 s0 = *(const floatx4*)(sc + (kk * 32 + g4) * 4);
+          const floatx4 s1 = *(const floatx4*)(sc + (kk * 32 + 16 + g4) * 4);
+          const floatx4 t0 = *(const floatx4*)(sc + (IA::BK + kk * 32 + g4) * 4);
+          const floatx4 t1 = *(const floatx4*)(sc + (IA::BK + kk * 32 + 16 + g4) * 4);
+#pragma unroll
+          for (int i = 0; i < MI; ++i) fa[i] = affine8(fa[i], s0, s1, t0, t1);
+        }
+        if constexpr (BTR) {
+#pragma unroll
+          for (int j = 0; j < NI; ++j) fb[j] = affine8c(fb[j], sbn[j], tbn[j]);
+        }
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -268,6 +286,21 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
         for (int i = 0; i < MI; ++i) fa[i] = frag_f32<AK, BM>(sa, wm * 16 * MI + i * 16, kc, lane);
 #pragma unroll
         for (int j = 0; j < NI; ++j) fb[j] = frag_f32<BK_, BN>(sb, wn * 16 * NI + j * 16, kc, lane);
+        if constexpr (ATR) {
+          const int g4 = (lane >> 4) * 4;
+          const floatx4 s0 = *(const floatx4*)(sc + (kc * 16 + g4) * 4);
+          const floatx4 t0 = *(const floatx4*)(sc + (IA::BK + kc * 16 + g4) * 4);
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) fa[i][e] = fa[i][e] * s0[e] + t0[e];
+        }
+        if constexpr (BTR) {
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) fb[j][e] = fb[j][e] * sbn[j] + tbn[j];
+        }
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -277,13 +310,6 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
       }
     }
-    if (t + 1 < nt) {
-      transform();
-      char* na = smem + ((t + 1) & 1) * STAGE;
-      stage_store<T, AK, BM>(na, ra, tid);
-      stage_store<T, BK_, BN>(na + IA::BYTES, rb, tid);
-    }
-    __syncthreads();
   }
 
   // ===================== epilogue, register phase ==========================
@@ -522,7 +548,7 @@ __global__ __launch_bounds__(256, 2) void mmad_gemm_kernel(const T* __restrict__
 // -------------------------------------------------------------------------
 // host-side launch
 // -------------------------------------------------------------------------
-template <typename T, typename TO, bool AK, bool BK_, int EPI>
+template <typename T, typename TO, bool AK, bool BK_, int EPI, bool TR>
 static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np, int K,
                         const GemmEpi& ep_in, int tile, hipStream_t s) {
   dim3 blk(256);
@@ -540,13 +566,13 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
   dim3 grd(nblk);
   switch (tile) {
     case 0:  // 128 x 128
-      mmad_gemm_kernel<T, TO, AK, BK_, 4, 4, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep);
+      mmad_gemm_kernel<T, TO, AK, BK_, 4, 4, EPI, TR><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep);
       break;
     case 1:  // 64 x 128
-      mmad_gemm_kernel<T, TO, AK, BK_, 2, 4, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep);
+      mmad_gemm_kernel<T, TO, AK, BK_, 2, 4, EPI, TR><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep);
       break;
     default:  // 64 x 64
-      mmad_gemm_kernel<T, TO, AK, BK_, 2, 2, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep);
+      mmad_gemm_kernel<T, TO, AK, BK_, 2, 2, EPI, TR><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep);
       break;
   }
   MMAD_LAUNCH_CHECK();
@@ -577,30 +603,33 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   MMAD_CHECK_ARG(Mp > 0 && Np > 0 && K > 0, "gemm: empty problem");
   const int tile = mmad_pick_tile(Mp, Np, epi);
   if (epi == GEMM_EPI_SCORE) MMAD_CHECK_ARG(tile != 2, "score epilogue needs a 128-wide tile");
-#define MMAD_DISPATCH_T(T)                                                                        \
-  switch (epi) {                                                                                  \
-    case GEMM_EPI_FWD:                                                                            \
-      return launch_tiled<T, T, true, true, GEMM_EPI_FWD>((const T*)A, lda, (const T*)B, ldb, Mp,  \
-                                                          Np, K, ep, tile, s);                    \
-    case GEMM_EPI_MSE:                                                                            \
-      return launch_tiled<T, T, true, true, GEMM_EPI_MSE>((const T*)A, lda, (const T*)B, ldb, Mp,  \
-                                                          Np, K, ep, tile, s);                    \
-    case GEMM_EPI_SCORE:                                                                          \
-      return launch_tiled<T, T, true, true, GEMM_EPI_SCORE>((const T*)A, lda, (const T*)B, ldb,    \
-                                                            Mp, Np, K, ep, tile, s);              \
-    case GEMM_EPI_BWD_DATA:                                                                       \
-      return launch_tiled<T, T, true, false, GEMM_EPI_BWD_DATA>((const T*)A, lda, (const T*)B,     \
-                                                                ldb, Mp, Np, K, ep, tile, s);     \
-    case GEMM_EPI_BWD_WEIGHT:                                                                     \
-      return launch_tiled<T, float, false, false, GEMM_EPI_BWD_WEIGHT>(                            \
-          (const T*)A, lda, (const T*)B, ldb, Mp, Np, K, ep, tile, s);                            \
-    default: mmad_set_error("gemm: bad epilogue %d", epi); return MMAD_EINVAL;                   \
+  const bool atr = ep.a_scale != nullptr, btr = ep.b_scale != nullptr;
+#define MMAD_LT(T, TO, AK, BK_, EPI, TR)                                                  \
+  return launch_tiled<T, TO, AK, BK_, EPI, TR>((const T*)A, lda, (const T*)B, ldb, Mp, Np, K, ep, \
+                                               tile, s)
+#define MMAD_DISPATCH_T(T)                                                               \
+  switch (epi) {                                                                         \
+    case GEMM_EPI_FWD:                                                                   \
+      if (atr) MMAD_LT(T, T, true, true, GEMM_EPI_FWD, true);                            \
+      MMAD_LT(T, T, true, true, GEMM_EPI_FWD, false);                                    \
+    case GEMM_EPI_MSE:                                                                   \
+      if (atr) MMAD_LT(T, T, true, true, GEMM_EPI_MSE, true);                            \
+      MMAD_LT(T, T, true, true, GEMM_EPI_MSE, false);                                    \
+    case GEMM_EPI_SCORE:                                                                 \
+      MMAD_LT(T, T, true, true, GEMM_EPI_SCORE, false);                                  \
+    case GEMM_EPI_BWD_DATA:                                                              \
+      MMAD_LT(T, T, true, false, GEMM_EPI_BWD_DATA, false);                              \
+    case GEMM_EPI_BWD_WEIGHT:                                                            \
+      if (btr) MMAD_LT(T, float, false, false, GEMM_EPI_BWD_WEIGHT, true);               \
+      MMAD_LT(T, float, false, false, GEMM_EPI_BWD_WEIGHT, false);                       \
+    default: mmad_set_error("gemm: bad epilogue %d", epi); return MMAD_EINVAL;          \
   }
   if (dtype == MMAD_BF16) {
     MMAD_DISPATCH_T(bf16)
   } else if (dtype == MMAD_F32) {
     MMAD_DISPATCH_T(float)
   }
+#undef MMAD_LT
 #undef MMAD_DISPATCH_T
   mmad_set_error("gemm: bad dtype %d", dtype);
   return MMAD_EINVAL;
