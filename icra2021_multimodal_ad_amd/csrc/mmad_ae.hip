@@ -44,6 +44,7 @@ struct mmad_ae {
   hipStream_t side = nullptr;
   std::vector<hipEvent_t> ev_fork, ev_data;
   hipEvent_t ev_join = nullptr;
+  int mse_tiles = 0;   // loss partials written by the last MSE GEMM
   ~mmad_ae() {
     for (auto e : ev_fork) (void)hipEventDestroy(e);
     for (auto e : ev_data) (void)hipEventDestroy(e);
@@ -314,7 +315,9 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
       ep.tmod = B;
       ep.gscale = 2.0f / (float)k;
       ep.lossp = w.lossp;
-      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_MSE, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
+      int cfg = 0;
+      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_MSE, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st, &cfg));
+      h->mse_tiles = mmad_gemm_ntiles(cfg, Mp, a.Np);
     } else if (a.bn && train) {
       GemmEpi ep = fwd_epi(h, a, M, s.out, isc, ish);
       ep.part = s.stats;
@@ -385,8 +388,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       // fork: dz_l is complete on the main stream; dW_l overlaps the chain below
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
       MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
-      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe,
-                                side));
+      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side));
     }
     if (l > 0) {
       const AeLayer& p = h->L[l - 1];
@@ -451,8 +453,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       dwe.sm_bstride = bs.stride;
       dwe.sm_bN = a.N;
       dwe.sm_bNp = a.Np;
-      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe,
-                                side));
+      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side));
     }
   }
   // join the side stream back into the main stream
@@ -486,11 +487,11 @@ static int finish_reductions(mmad_ae* h, AeWS& w, bool biases, bool from_mse, fl
     const AeLayer& last = h->L[nL - 1];
     MmadReduceJob& j = jobs.j[n++];
     j.scalar = 1;
-    j.src = w.lossp;                        // one sum of d^2 per MSE-GEMM block
+    j.src = w.lossp;                        // one sum of d^2 per MSE-GEMM output tile
     j.dst = loss_out;
     j.nparts = 1;
     j.stride = 0;
-    j.N = mmad_gemm_grid_blocks(w.Mpd, last.Np, GEMM_EPI_MSE);
+    j.N = h->mse_tiles;
     j.Np = j.N;
     j.scale = 1.f / (float)w.k;
     if (h->vib) {

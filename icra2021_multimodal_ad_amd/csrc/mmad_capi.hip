@@ -38,13 +38,22 @@ static int g_group = [] {
   const char* e = getenv("MMAD_GEMM_GROUP_M");
   return e ? atoi(e) : -1;
 }();
+static int g_autotune = [] {
+  const char* e = getenv("MMAD_GEMM_AUTOTUNE");
+  return e ? atoi(e) : 1;
+}();
 int mmad_tile_override() { return g_tile; }
 int mmad_group_override() { return g_group; }
+int mmad_autotune_enabled() { return g_autotune; }
+static int g_dbg = 0;
+int mmad_dbg_override() { return g_dbg; }
 
 int mmad_tune_set(int knob, int value) {
   switch (knob) {
     case 0: g_tile = value; return MMAD_OK;
     case 1: g_group = value; return MMAD_OK;
+    case 2: g_autotune = value; return MMAD_OK;
+    case 3: g_dbg = value; return MMAD_OK;
     default: mmad_set_error("tune_set: unknown knob %d", knob); return MMAD_EINVAL;
   }
 }
@@ -82,7 +91,8 @@ int mmad_fc_fwd(int dtype, int M, int N, int K, int Mp, int Np, int Kp, const vo
   GemmEpi ep{};
   ep.M = M; ep.N = N; ep.out = y; ep.ldo = Np; ep.bias = bias; ep.act = act; ep.slope = slope;
   ep.bn_scale = bn_scale; ep.bn_shift = bn_shift; ep.part = stats; ep.ldpart = Np;
-  return mmad_gemm_dispatch(dtype, GEMM_EPI_FWD, x, Kp, w, Kp, Mp, Np, Kp, ep, (hipStream_t)stream);
+  return mmad_gemm_dispatch(dtype, GEMM_EPI_FWD, x, Kp, w, Kp, Mp, Np, Kp, ep,
+                            (hipStream_t)stream);
 }
 
 static int fc_fwd_mse_impl(int dtype, int M, int N, int K, int Mp, int Np, int Kp, const void* x,
@@ -94,7 +104,8 @@ static int fc_fwd_mse_impl(int dtype, int M, int N, int K, int Mp, int Np, int K
   GemmEpi ep{};
   ep.M = M; ep.N = N; ep.out = dz; ep.ldo = Np; ep.bias = bias; ep.part = partials;
   ep.ldpart = Np; ep.target = target; ep.ldt = ld_target; ep.tmod = tmod; ep.gscale = grad_scale;
-  return mmad_gemm_dispatch(dtype, GEMM_EPI_MSE, x, Kp, w, Kp, Mp, Np, Kp, ep, (hipStream_t)stream);
+  return mmad_gemm_dispatch(dtype, GEMM_EPI_MSE, x, Kp, w, Kp, Mp, Np, Kp, ep,
+                            (hipStream_t)stream);
 }
 
 int mmad_fc_fwd_mse(int dtype, int M, int N, int K, int Mp, int Np, int Kp, const void* x,

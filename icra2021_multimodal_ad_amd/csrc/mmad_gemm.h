@@ -41,7 +41,7 @@ struct GemmEpi {
   const float* bn_mean;
   const float* bn_rstd;
   float* bn_part;        // [Mp/64][2][ldo]: (sum dy, sum dy*xhat)
-  // MSE: one loss partial (sum d^2) per block, index blockIdx.y*gridDim.x+blockIdx.x
+  // MSE: one loss partial (sum d^2) per output tile, [mmad_gemm_ntiles(plan)]
   float* lossp;
   // BWD_WEIGHT: torch.optim.Adam step fused into the epilogue (nullable p).
   // Weight tile: p/m/v share the dW layout (ld = ldo); shadow gets bf16(p).
@@ -61,16 +61,23 @@ struct GemmEpi {
   int sm_bparts, sm_bstride, sm_bN, sm_bNp;
   // set by the launcher: XCD-aware grouped tile order
   int tiles_n, group_m;
+  int dbg;               // diagnostics (tools/gemm_sweep): 1 skip main loop, 2 skip epilogue
 };
 
 int mmad_group_override();
 
-// blocks of the grid mmad_gemm_dispatch launches for this problem
-int mmad_gemm_grid_blocks(int Mp, int Np, int epi);
-
-int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,
-                       int Np, int K, const GemmEpi& ep, hipStream_t s);
-int mmad_pick_tile(int Mp, int Np, int epi);
 int mmad_tile_override();
-// width (columns) of the tile the score epilogue will use for an Np-wide output
-static inline int mmad_score_tile_n() { return 128; }
+int mmad_autotune_enabled();
+int mmad_dbg_override();
+
+// tile configuration a problem will run with (autotuned on first dispatch of
+// the shape; a static heuristic before that / when tuning is off)
+int mmad_gemm_plan(int Mp, int Np, int K, int epi, int dtype, bool atr, bool btr);
+// output tiles of a configuration (= MSE loss partials written)
+int mmad_gemm_ntiles(int cfg, int Mp, int Np);
+// upper bound of mmad_gemm_ntiles over all configurations
+int mmad_gemm_tiles(int Mp, int Np);
+
+// cfg_used (nullable) receives the tile configuration launched
+int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,
+                       int Np, int K, const GemmEpi& ep, hipStream_t s, int* cfg_used = nullptr);
