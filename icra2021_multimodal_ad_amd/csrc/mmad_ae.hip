@@ -15,6 +15,7 @@
 //   (single-GPU fused step) by that layer's Adam update, overlapping the
 //   remaining backward chain on the main stream.
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "mmad_common.h"
@@ -45,6 +46,16 @@ struct mmad_ae {
   std::vector<hipEvent_t> ev_fork, ev_data;
   hipEvent_t ev_join = nullptr;
   int mse_tiles = 0;   // loss partials written by the last MSE GEMM
+  // fused step: dW GEMMs of layers < dw_main run on the caller's stream;
+  // keep_grads: also write dW to the grads buffer
+  int dw_main = [] {
+    const char* e = getenv("MMAD_DW_MAIN");
+    return e ? atoi(e) : 2;
+  }();
+  int keep_grads = [] {
+    const char* e = getenv("MMAD_KEEP_GRADS");
+    return e ? atoi(e) : 0;
+  }();
   ~mmad_ae() {
     for (auto e : ev_fork) (void)hipEventDestroy(e);
     for (auto e : ev_data) (void)hipEventDestroy(e);
@@ -432,7 +443,6 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       // (bwd-data of l); the rest of the chain keeps overlapping it.
       if (l == 0 || !(h->L[l - 1].bn) || (h->vib && l == h->n_enc))
         MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
-      MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_data[l], 0));
       const BiasSrc bs = bias_src(h, w, l, from_mse);
       dwe.ad_p = h->params + a.w_off;
       dwe.ad_m = h->m + a.w_off;
@@ -453,7 +463,18 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       dwe.sm_bstride = bs.stride;
       dwe.sm_bN = a.N;
       dwe.sm_bNp = a.Np;
-      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side));
+      // the gradient is consumed by the fused Adam in registers; materialise
+      // it only when asked (h->keep_grads)
+      dwe.dw_nostore = h->keep_grads ? 0 : 1;
+      // the last dW GEMMs of the chain go to the main stream, which is idle
+      // by then, instead of queueing behind the side stream's backlog
+      const bool on_main = l < h->dw_main;
+      if (on_main) {
+        RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st));
+      } else {
+        MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_data[l], 0));
+        RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side));
+      }
     }
   }
   // join the side stream back into the main stream

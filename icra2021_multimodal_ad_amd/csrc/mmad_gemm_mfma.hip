@@ -485,7 +485,8 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
     const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
     const int row = m0 + rl;
     const int col = n0 + ch * OEPC;
-    *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
+    if (EPI != GEMM_EPI_BWD_WEIGHT || !(ep.ad_p && ep.dw_nostore))
+      *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
     if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
       if (ep.ad_p) {
         // torch.optim.Adam on this dW chunk (4 fp32), same formula as adam_k

@@ -120,29 +120,28 @@ __global__ __launch_bounds__(256) void bn_train_apply_k(int M, int N, int Np, co
 }
 
 // Train-mode BN finalize only: batch mean/rstd, per-column affine for the
-// consumers' normalise-on-load, running-stat update.  One block per 64 cols.
-// 1024 threads = 16 chunk groups x 64 columns; each group merges its chunks
-// (loads issued back to back), then 64 threads merge the 16 group results.
-__global__ __launch_bounds__(1024) void bn_finalize_k(int M, int N, int Np, const float* __restrict__ stats,
-                                                      int nparts, const float* gamma, const float* beta,
-                                                      float* rmean, float* rvar, float momentum,
-                                                      float eps, float* save_mean, float* save_rstd,
-                                                      float* scale, float* shift) {
-  constexpr int G = 16;
-  __shared__ float pm[G][SLAB_COLS], pq[G][SLAB_COLS], pn[G][SLAB_COLS];
-  const int n0 = blockIdx.x * SLAB_COLS, tid = threadIdx.x, c = tid & 63, grp = tid >> 6;
+// consumers' normalise-on-load, running-stat update.  One thread per column:
+// every chunk partial is loaded up front (one memory round trip), then merged
+// sequentially in chunk order (Chan et al. pairwise Welford update).
+__global__ __launch_bounds__(64) void bn_finalize_k(int M, int N, int Np, const float* __restrict__ stats,
+                                                    int nparts, const float* gamma, const float* beta,
+                                                    float* rmean, float* rvar, float momentum,
+                                                    float eps, float* save_mean, float* save_rstd,
+                                                    float* scale, float* shift) {
+  constexpr int U = 16;
+  const int col = blockIdx.x * 64 + threadIdx.x;
   float n = 0.f, mean = 0.f, m2 = 0.f;
-  for (int i0 = grp; i0 < nparts; i0 += 4 * G) {
-    float mb[4], qb[4];
+  for (int i0 = 0; i0 < nparts; i0 += U) {
+    float mb[U], qb[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = i0 + u * G;
-      mb[u] = i < nparts ? stats[(size_t)i * 2 * Np + n0 + c] : 0.f;
-      qb[u] = i < nparts ? stats[((size_t)i * 2 + 1) * Np + n0 + c] : 0.f;
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u < nparts ? i0 + u : nparts - 1;
+      mb[u] = stats[(size_t)i * 2 * Np + col];
+      qb[u] = stats[((size_t)i * 2 + 1) * Np + col];
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = i0 + u * G;
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u;
       int cnt = M - i * MMAD_PART_ROWS;
       cnt = cnt < 0 ? 0 : (cnt > MMAD_PART_ROWS ? MMAD_PART_ROWS : cnt);
       if (i >= nparts || cnt == 0) continue;
@@ -152,38 +151,22 @@ __global__ __launch_bounds__(1024) void bn_finalize_k(int M, int N, int Np, cons
       n = nn;
     }
   }
-  pm[grp][c] = mean;
-  pq[grp][c] = m2;
-  pn[grp][c] = n;
-  __syncthreads();
-  if (tid < SLAB_COLS) {
-    float n1 = 0.f, mu = 0.f, q = 0.f;
-    for (int g = 0; g < G; ++g) {
-      const float nb = pn[g][tid];
-      if (nb == 0.f) continue;
-      const float nn = n1 + nb, d = pm[g][tid] - mu;
-      mu += d * (nb / nn);
-      q += pq[g][tid] + d * d * (n1 * nb / nn);
-      n1 = nn;
-    }
-    const float var = n1 > 0.f ? q / n1 : 0.f;
-    const int col = n0 + tid;
-    if (col < N) {
-      const float rstd = rsqrtf(var + eps);
-      const float sc = gamma[col] * rstd;
-      save_mean[col] = mu;
-      save_rstd[col] = rstd;
-      scale[col] = sc;
-      shift[col] = beta[col] - mu * sc;
-      const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
-      rmean[col] = (1.f - momentum) * rmean[col] + momentum * mu;
-      rvar[col] = (1.f - momentum) * rvar[col] + momentum * unb;
-    } else {
-      save_mean[col] = 0.f;
-      save_rstd[col] = 0.f;
-      scale[col] = 0.f;
-      shift[col] = 0.f;
-    }
+  const float var = n > 0.f ? m2 / n : 0.f;
+  if (col < N) {
+    const float rstd = rsqrtf(var + eps);
+    const float sc = gamma[col] * rstd;
+    save_mean[col] = mean;
+    save_rstd[col] = rstd;
+    scale[col] = sc;
+    shift[col] = beta[col] - mean * sc;
+    const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+    rmean[col] = (1.f - momentum) * rmean[col] + momentum * mean;
+    rvar[col] = (1.f - momentum) * rvar[col] + momentum * unb;
+  } else {
+    save_mean[col] = 0.f;
+    save_rstd[col] = 0.f;
+    scale[col] = 0.f;
+    shift[col] = 0.f;
   }
 }
 
@@ -239,6 +222,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(int M, int Np, const T* _
   }
 }
 
+// dz = act'(a) * gamma*rstd/M * (M*dy - sum(dy) - xhat*sum(dy*xhat)) over one
+// 64-column x 128-row slab; sums from the bwd-data GEMM epilogue partials.
+// Every global load (dy, a, the column constants, the partials) is issued
+// before the first use, so a block costs one memory round trip, not four.
 template <typename T>
 __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int M, int N, int Np,
                                                       int nparts, const T* __restrict__ dy,
@@ -247,58 +234,79 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
                                                       const float* __restrict__ rstd,
                                                       const float* __restrict__ gamma,
                                                       const float* __restrict__ part,
-                                                      T* __restrict__ dz, float* dgamma,
-                                                      float* dbeta, float* dbpart) {
+                                                      T* __restrict__ dz, float* __restrict__ dgamma,
+                                                      float* __restrict__ dbeta, float* __restrict__ dbpart) {
   constexpr int V = Vec<T>::N;
-  constexpr int CPR = SLAB_COLS / V;
-  constexpr int RG = 256 / CPR;
-  __shared__ float s_db[SLAB_COLS], s_dg[SLAB_COLS];
+  constexpr int CPR = SLAB_COLS / V;      // threads per row
+  constexpr int RG = 256 / CPR;           // row groups
+  constexpr int RPT = SLAB_ROWS / RG;     // rows per thread
+  constexpr int PU = 8;                   // partial chunks per group loaded at once
   __shared__ float s_red[RG][SLAB_COLS];
   __shared__ float s_p1[4][SLAB_COLS], s_p2[4][SLAB_COLS];
   const int n0 = blockIdx.x * SLAB_COLS, r0 = blockIdx.y * SLAB_ROWS, tid = threadIdx.x;
+  const int ch = tid % CPR, rg = tid / CPR;
+  // (1) this thread's dy / a rows
+  uint4v rd[RPT], ra[RPT];
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const size_t off = (size_t)(r0 + rg + i * RG) * Np + n0 + ch * V;
+    rd[i] = *(const uint4v*)(dy + off);
+    ra[i] = *(const uint4v*)(a + off);
+  }
+  // (2) column constants
+  float mu[V], rs[V], gm[V];
+#pragma unroll
+  for (int k = 0; k < V; k += 4) {
+    const int col = n0 + ch * V + k;
+    *(floatx4*)&mu[k] = *(const floatx4*)(mean + col);
+    *(floatx4*)&rs[k] = *(const floatx4*)(rstd + col);
+    *(floatx4*)&gm[k] = *(const floatx4*)(gamma + col);
+  }
+  // (3) partial sums: 4 groups of 64 columns, group g sums chunks g, g+4, ...
   {
-    // 4 groups of 64 threads split the partial rows (independent loads)
     const int c = tid & 63, grp = tid >> 6;
     float t1 = 0.f, t2 = 0.f;
-#pragma unroll 4
-    for (int i = grp; i < nparts; i += 4) {
-      t1 += part[((size_t)i * 2) * Np + n0 + c];
-      t2 += part[((size_t)i * 2 + 1) * Np + n0 + c];
+    for (int i0 = grp; i0 < nparts; i0 += 4 * PU) {
+      float p1[PU], p2[PU];
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const int i = i0 + 4 * u < nparts ? i0 + 4 * u : grp;
+        p1[u] = part[((size_t)i * 2) * Np + n0 + c];
+        p2[u] = part[((size_t)i * 2 + 1) * Np + n0 + c];
+      }
+#pragma unroll
+      for (int u = 0; u < PU; ++u)
+        if (i0 + 4 * u < nparts) { t1 += p1[u]; t2 += p2[u]; }
     }
     s_p1[grp][c] = t1;
     s_p2[grp][c] = t2;
   }
   __syncthreads();
   if (tid < SLAB_COLS) {
-    float t1 = s_p1[0][tid] + s_p1[1][tid] + s_p1[2][tid] + s_p1[3][tid];
-    float t2 = s_p2[0][tid] + s_p2[1][tid] + s_p2[2][tid] + s_p2[3][tid];
+    float t1 = ((s_p1[0][tid] + s_p1[1][tid]) + s_p1[2][tid]) + s_p1[3][tid];
+    float t2 = ((s_p2[0][tid] + s_p2[1][tid]) + s_p2[2][tid]) + s_p2[3][tid];
     const int col = n0 + tid;
     if (col >= N) { t1 = 0.f; t2 = 0.f; }
-    s_db[tid] = t1;
-    s_dg[tid] = t2;
+    s_p1[0][tid] = t1;
+    s_p2[0][tid] = t2;
     if (blockIdx.y == 0) { dbeta[col] = t1; dgamma[col] = t2; }
   }
   __syncthreads();
-  const int ch = tid % CPR, rg = tid / CPR;
-  float mu[V], rs[V], cf[V], dbv[V], dgv[V], accb[V];
   const float invM = 1.f / (float)M;
+  float cf[V], dbv[V], dgv[V], accb[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) {
     const int col = n0 + ch * V + k;
-    mu[k] = mean[col];
-    rs[k] = rstd[col];
-    cf[k] = col < N ? gamma[col] * rs[k] * invM : 0.f;
-    dbv[k] = s_db[ch * V + k];
-    dgv[k] = s_dg[ch * V + k];
+    cf[k] = col < N ? gm[k] * rs[k] * invM : 0.f;
+    dbv[k] = s_p1[0][ch * V + k];
+    dgv[k] = s_p2[0][ch * V + k];
     accb[k] = 0.f;
   }
-  for (int rl = rg; rl < SLAB_ROWS; rl += RG) {
-    const int row = r0 + rl;
-    const size_t off = (size_t)row * Np + n0 + ch * V;
-    uint4v rd = *(const uint4v*)(dy + off);
-    uint4v ra = *(const uint4v*)(a + off);
-    const T* pd = (const T*)&rd;
-    const T* pa = (const T*)&ra;
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int row = r0 + rg + i * RG;
+    const T* pd = (const T*)&rd[i];
+    const T* pa = (const T*)&ra[i];
     uint4v ro;
     T* po = (T*)&ro;
 #pragma unroll
@@ -312,7 +320,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
       po[k] = dt;
       accb[k] += to_f32<T>(dt);
     }
-    *(uint4v*)(dz + off) = ro;
+    *(uint4v*)(dz + (size_t)row * Np + n0 + ch * V) = ro;
   }
 #pragma unroll
   for (int k = 0; k < V; ++k) s_red[rg][ch * V + k] = accb[k];
@@ -672,7 +680,7 @@ int mmad_bn_finalize(int M, int N, int Mp, int Np, const float* stats, const flo
                      void* stream) {
   MMAD_CHECK_ARG(Mp % 128 == 0 && Np % 128 == 0 && M >= 1 && M <= Mp && N <= Np,
                  "bn_finalize: bad sizes");
-  bn_finalize_k<<<Np / SLAB_COLS, 1024, 0, (hipStream_t)stream>>>(
+  bn_finalize_k<<<Np / 64, 64, 0, (hipStream_t)stream>>>(
       M, N, Np, stats, Mp / MMAD_PART_ROWS, gamma, beta, running_mean, running_var, momentum, eps,
       save_mean, save_rstd, scale, shift);
   MMAD_LAUNCH_CHECK();

@@ -268,9 +268,10 @@ def test_vib_decorator_reparam(golden):
     with torch.no_grad():
         zd = reparameterize(mu, lv, 2, False).cpu().numpy()
     assert np.array_equal(zd, np.broadcast_to(g["mu"], zd.shape))
-    zr = reparameterize(mu, lv, 4, True).cpu().numpy()     # Philox draw
+    zr = reparameterize(mu, lv, 256, True).cpu().numpy()   # Philox draw
     e = (zr - g["mu"][None]) / np.exp(0.5 * g["logvar"])[None]
-    assert abs(e.mean()) < 0.1 and abs(e.std() - 1) < 0.1
+    n = e.size                                             # 5-sigma bounds for N(0, 1)
+    assert abs(e.mean()) < 5 / np.sqrt(n) and abs(e.std() - 1) < 5 * np.sqrt(0.5 / n)
 
 
 def test_full_size_properties_bf16():
