@@ -67,6 +67,10 @@ struct mmad_ae {
 struct LayerWS {
   void *out, *y, *dy, *dz;
   float *stats, *mean, *rstd, *scale, *shift, *bnpart, *dbpart, *rowsq;
+  // consumer of a train-mode BN producer: W*scale (GEMM dtype) and the
+  // per-64-column partials of sum_k shift[k] W[n][k]
+  void* wf;
+  float* cpart;
 };
 struct AeWS {
   int B, k, Mpe, Mpd;
@@ -128,6 +132,9 @@ static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
     s.bnpart = (float*)take((int64_t)(Mp / 64) * 2 * a.Np * 4);
     s.dbpart = (float*)take((int64_t)(Mp / 128) * a.Np * 4);
     s.rowsq = (float*)take((int64_t)(a.Np / 128) * Mp * 4);
+    const bool folded = i > 0 && h->L[i - 1].bn;
+    s.wf = folded ? take((int64_t)a.Np * a.Kp * es) : nullptr;
+    s.cpart = folded ? (float*)take((int64_t)(a.Kp / 64) * a.Np * 4) : nullptr;
   }
   w.bytes = (off + 255) / 256 * 256;
 }
@@ -253,8 +260,9 @@ static const void* weights(const mmad_ae* h, const AeLayer& a) {
   return h->params + a.w_off;
 }
 
-// input of layer l; in train mode a BN producer's output stays pre-BN (a) and
-// the consumer normalises it on load with (scale, shift)
+// input of layer l; in train mode a BN producer's output stays pre-BN (a): the
+// forward reads it against the folded weights, the dW GEMM fixes up with
+// (scale, shift) in its epilogue
 static const void* input_of(const mmad_ae* h, const AeWS& w, int l, bool train,
                             const float** scale, const float** shift) {
   *scale = *shift = nullptr;
@@ -286,8 +294,8 @@ static float* running_var(const mmad_ae* h, const AeLayer& a) {
   return h->running + h->n_bn + a.bn_off;
 }
 
-static GemmEpi fwd_epi(const mmad_ae* h, const AeLayer& a, int M, void* out, const float* a_scale,
-                       const float* a_shift) {
+static GemmEpi fwd_epi(const mmad_ae* h, const AeWS& w, const AeLayer& a, const LayerWS& s,
+                       int M, void* out, bool folded) {
   GemmEpi ep{};
   ep.M = M;
   ep.N = a.N;
@@ -297,8 +305,12 @@ static GemmEpi fwd_epi(const mmad_ae* h, const AeLayer& a, int M, void* out, con
   ep.act = a.act;
   ep.slope = h->slope;
   ep.ldpart = a.Np;
-  ep.a_scale = a_scale;
-  ep.a_shift = a_shift;
+  if (folded) {
+    ep.bpart = s.cpart;
+    ep.bparts = a.Kp / 64;
+    ep.bpstride = a.Np;
+  }
+  (void)w;
   return ep;
 }
 
@@ -316,9 +328,10 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
     const int M = rows_of(w, a), Mp = prows_of(w, a);
     const float *isc, *ish;
     const void* in = input_of(h, w, l, train, &isc, &ish);
-    const void* wt = weights(h, a);
+    const bool folded = isc != nullptr;             // train mode, BN producer
+    const void* wt = folded ? s.wf : weights(h, a);
     if (mode == 0 && l == nL - 1) {
-      GemmEpi ep = fwd_epi(h, a, M, s.out, isc, ish);
+      GemmEpi ep = fwd_epi(h, w, a, s, M, s.out, folded);
       ep.act = MMAD_ACT_NONE;
       ep.part = s.stats;
       ep.target = x;
@@ -330,22 +343,32 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
       RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_MSE, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st, &cfg));
       h->mse_tiles = mmad_gemm_ntiles(cfg, Mp, a.Np);
     } else if (a.bn && train) {
-      GemmEpi ep = fwd_epi(h, a, M, s.out, isc, ish);
+      GemmEpi ep = fwd_epi(h, w, a, s, M, s.out, folded);
       ep.part = s.stats;
       RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
-      RET_IF(mmad_bn_finalize(M, a.N, Mp, a.Np, s.stats, h->params + a.g_off,
-                              h->params + a.be_off, running_mean(h, a), running_var(h, a),
-                              h->bn_mom, h->bn_eps, s.mean, s.rstd, s.scale, s.shift, st));
+      if (l + 1 < nL) {
+        // statistics -> (scale, shift) -> folded into layer l+1's weights/bias
+        const AeLayer& c = h->L[l + 1];
+        LayerWS& cs = w.l[l + 1];
+        RET_IF(mmad_bn_finalize_fold(dt, M, a.N, Mp, a.Np, s.stats, h->params + a.g_off,
+                                     h->params + a.be_off, running_mean(h, a), running_var(h, a),
+                                     h->bn_mom, h->bn_eps, s.mean, s.rstd, s.scale, s.shift,
+                                     h->params + c.w_off, c.Np, cs.wf, cs.cpart, st));
+      } else {
+        RET_IF(mmad_bn_finalize(M, a.N, Mp, a.Np, s.stats, h->params + a.g_off,
+                                h->params + a.be_off, running_mean(h, a), running_var(h, a),
+                                h->bn_mom, h->bn_eps, s.mean, s.rstd, s.scale, s.shift, st));
+      }
     } else if (a.bn) {
       RET_IF(mmad_bn_eval_affine(a.N, a.Np, h->params + a.g_off, h->params + a.be_off,
                                  running_mean(h, a), running_var(h, a), h->bn_eps, s.scale,
                                  s.shift, st));
-      GemmEpi ep = fwd_epi(h, a, M, s.y, isc, ish);
+      GemmEpi ep = fwd_epi(h, w, a, s, M, s.y, folded);
       ep.bn_scale = s.scale;
       ep.bn_shift = s.shift;
       RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
     } else {
-      GemmEpi ep = fwd_epi(h, a, M, s.out, isc, ish);
+      GemmEpi ep = fwd_epi(h, w, a, s, M, s.out, folded);
       RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
     }
     if (h->vib && l == h->n_enc - 1) {
@@ -393,8 +416,15 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     dwe.N = a.Kp;
     dwe.out = h->grads + a.w_off;
     dwe.ldo = a.Kp;
-    dwe.b_scale = isc;
-    dwe.b_shift = ish;
+    if (isc) {
+      // dW against the raw producer activation, fixed up in the epilogue
+      const BiasSrc gs = bias_src(h, w, l, from_mse);
+      dwe.b_scale = isc;
+      dwe.b_shift = ish;
+      dwe.gb_src = gs.src;
+      dwe.gb_parts = gs.nparts;
+      dwe.gb_stride = gs.stride;
+    }
     if (!adam) {
       // fork: dz_l is complete on the main stream; dW_l overlaps the chain below
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
@@ -458,9 +488,9 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       dwe.sm_m = h->m + a.b_off;
       dwe.sm_v = h->v + a.b_off;
       dwe.sm_n = a.bn ? 3 * a.Np : a.Np;
-      dwe.sm_bsrc = bs.src;
-      dwe.sm_bparts = bs.nparts;
-      dwe.sm_bstride = bs.stride;
+      dwe.gb_src = bs.src;
+      dwe.gb_parts = bs.nparts;
+      dwe.gb_stride = bs.stride;
       dwe.sm_bN = a.N;
       dwe.sm_bNp = a.Np;
       // the gradient is consumed by the fused Adam in registers; materialise
@@ -625,7 +655,7 @@ int mmad_ae_score(mmad_ae* h, const float* x, int ld_x, int B, float* layer_sq, 
     const int M = rows_of(w, a), Mp = prows_of(w, a);
     const float *isc, *ish;
     const void* in = input_of(h, w, l, false, &isc, &ish);
-    GemmEpi ep = fwd_epi(h, a, M, a.bn ? s.y : s.out, nullptr, nullptr);
+    GemmEpi ep = fwd_epi(h, w, a, s, M, a.bn ? s.y : s.out, false);
     if (a.bn) {
       RET_IF(mmad_bn_eval_affine(a.N, a.Np, h->params + a.g_off, h->params + a.be_off,
                                  running_mean(h, a), running_var(h, a), h->bn_eps, s.scale,
@@ -657,7 +687,7 @@ int mmad_ae_score(mmad_ae* h, const float* x, int ld_x, int B, float* layer_sq, 
   for (int e = 0; e < h->n_enc; ++e) {
     const AeLayer& a = h->L[e];
     LayerWS& s = w.l[e];
-    GemmEpi ep = fwd_epi(h, a, B, s.dy, nullptr, nullptr);
+    GemmEpi ep = fwd_epi(h, w, a, s, B, s.dy, false);
     if (a.bn) {
       ep.bn_scale = s.scale;
       ep.bn_shift = s.shift;

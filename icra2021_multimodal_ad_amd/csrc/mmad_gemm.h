@@ -31,11 +31,15 @@ struct GemmEpi {
   int ldrow;
   float* diff;           // SCORE optional fp32 diff output
   int lddiff;
-  // BatchNorm normalise-on-load (train mode: y = a*scale + shift per feature)
-  const float* a_scale;  // A operand (K-major), indexed by k (nullable)
-  const float* a_shift;
-  const float* b_scale;  // B operand (MN-major), indexed by n (nullable)
+  // FWD/MSE: folded train-mode BN of the producer: bias += sum_p bpart[p][n]
+  const float* bpart;    // [bparts][bpstride] (nullable)
+  int bparts, bpstride;
+  // BWD_WEIGHT on a train-mode BN producer's raw activation a (x = a*s + t):
+  // dW = b_scale[k] * (dz^T a) + b_shift[k] * db[n], db[n] = sum_p gb_src[p][n]
+  const float* b_scale;  // indexed by k (nullable)
   const float* b_shift;
+  const float* gb_src;
+  int gb_parts, gb_stride;
   // BWD_DATA: BatchNorm-backward column partials of the produced dy
   const void* bn_a;      // pre-BN activation, same shape/ld as out (nullable)
   const float* bn_mean;
@@ -58,8 +62,7 @@ struct GemmEpi {
   float* sm_m;
   float* sm_v;
   int sm_n;
-  const float* sm_bsrc;
-  int sm_bparts, sm_bstride, sm_bN, sm_bNp;
+  int sm_bN, sm_bNp;     // bias entries (valid / padded); their g = db from gb_src
   // set by the launcher: XCD-aware grouped tile order
   int tiles_n, group_m;
   int dbg;               // diagnostics (tools/gemm_sweep): 1 skip main loop, 2 skip epilogue
@@ -73,7 +76,7 @@ int mmad_dbg_override();
 
 // tile configuration a problem will run with (autotuned on first dispatch of
 // the shape; a static heuristic before that / when tuning is off)
-int mmad_gemm_plan(int Mp, int Np, int K, int epi, int dtype, bool atr, bool btr);
+int mmad_gemm_plan(int Mp, int Np, int K, int epi, int dtype);
 // output tiles of a configuration (= MSE loss partials written)
 int mmad_gemm_ntiles(int cfg, int Mp, int Np);
 // upper bound of mmad_gemm_ntiles over all configurations

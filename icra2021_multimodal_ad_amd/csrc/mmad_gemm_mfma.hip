@@ -161,21 +161,6 @@ __device__ __forceinline__ floatx4 frag_f32(const char* img, int rbase, int kc, 
   }
 }
 
-__device__ __forceinline__ bf16x8 affine8(bf16x8 v, floatx4 s0, floatx4 s1, floatx4 t0, floatx4 t1) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    v[e] = (bf16)((float)v[e] * s0[e] + t0[e]);
-    v[4 + e] = (bf16)((float)v[4 + e] * s1[e] + t1[e]);
-  }
-  return v;
-}
-
-__device__ __forceinline__ bf16x8 affine8c(bf16x8 v, float s, float t) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = (bf16)((float)v[e] * s + t);
-  return v;
-}
-
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -190,10 +175,13 @@ __device__ __forceinline__ void block_barrier() {
 }  // namespace
 
 // -------------------------------------------------------------------------
-// TR: BatchNorm normalise-on-load -- A operand (K-major, indexed by k) for the
-// forward GEMMs, B operand (MN-major, indexed by n) for the dW GEMM; applied
-// to the MFMA fragments right after the LDS read.
-template <typename T, typename TO, bool AK, bool BK_, int CFG, int EPI, bool TR>
+// Train-mode BatchNorm of the producer layer never touches the operands here:
+// the forward folds it into the consumer's weights and bias (bn_fold_k: the
+// B operand is W*scale, the bias gets sum_k shift*W via bpart partials), the
+// dW GEMM contracts the raw activation and fixes up in the epilogue
+// (dW = scale[k] * acc + shift[k] * db[n]).  Every GEMM is a plain MFMA
+// contraction.
+template <typename T, typename TO, bool AK, bool BK_, int CFG, int EPI>
 __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __restrict__ A, int lda,
                                                            const T* __restrict__ B, int ldb, int K,
                                                            GemmEpi ep) {
@@ -205,11 +193,11 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   using IA = Img<T, AK, BM, NT>;
   using IB = Img<T, BK_, BN, NT>;
   constexpr bool NAT = AK && BK_;
-  constexpr bool ATR = TR && AK;
-  constexpr bool BTR = TR && !BK_;
-  constexpr int AFF = ATR ? 1024 : 0;                   // [scale | shift] copy per stage
-  constexpr int SLOT = IA::BYTES + IB::BYTES + AFF;
-  constexpr int NL = IA::CHUNKS + IB::CHUNKS;          // vm ops per thread per stage (+1 wave 0 ATR)
+  constexpr int SLOT = IA::BYTES + IB::BYTES;
+  constexpr int NL = IA::CHUNKS + IB::CHUNKS;          // vm ops per thread per stage
+  constexpr bool FWDLIKE = EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_MSE || EPI == GEMM_EPI_SCORE;
+  constexpr int QB = 8;                                // prefetched bias partials per lane
+  constexpr int QG = 32;                               // prefetched dW row-sum partials
   constexpr int OSTRIDE = BN * (int)sizeof(TO) + 16;
   constexpr int OBYTES = BM * OSTRIDE + (EPI == GEMM_EPI_BWD_DATA ? BM * BN / 2 : 0);
   constexpr int LDS_BYTES = (NS * SLOT > OBYTES) ? NS * SLOT : OBYTES;
@@ -244,16 +232,53 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  // B-side BatchNorm affine: one (scale, shift) per lane per n-tile, loaded
-  // (and waited for) before any LDS-DMA is in flight
-  float sbn[TN], tbn[TN];
-  if constexpr (BTR) {
+  // ---- epilogue constants, loaded before the main loop: their latency hides
+  // under it instead of stalling the epilogue.  (Ordinary loads older than
+  // every LDS-DMA of the ring; only used after the loop.)
+  const int g = lane >> 4, c = lane & 15;
+  const int rw = m0 + wm * 16 * TM;  // first row of this wave
+  const int cw = n0 + wn * 16 * TN;  // first col of this wave
+  float e_b[TN], e_s[TN], e_t[TN], e_p[TN][QB];
+  if constexpr (FWDLIKE) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * 16 * TN + j * 16 + (lane & 15);
-      sbn[j] = ep.b_scale[n];
-      tbn[j] = ep.b_shift[n];
-      asm volatile("" ::"v"(sbn[j]), "v"(tbn[j]));
+      const int col = cw + j * 16 + c;
+      e_b[j] = ep.bias ? ep.bias[col] : 0.f;
+      e_s[j] = ep.bn_scale ? ep.bn_scale[col] : 1.f;
+      e_t[j] = ep.bn_shift ? ep.bn_shift[col] : 0.f;
+      if (EPI != GEMM_EPI_SCORE && ep.bpart) {
+        // folded-BN bias partials: lane group g takes partials g, g+4, ...
+#pragma unroll
+        for (int q = 0; q < QB; ++q) {
+          const int pp = min(g + 4 * q, ep.bparts - 1);
+          e_p[j][q] = ep.bpart[(size_t)pp * ep.bpstride + col];
+        }
+      }
+    }
+  }
+  float e_g[QG];
+  // db[n] (bias gradient of this layer's output n) is needed by the dW fix-up
+  // (BN producer) and by the fused bias Adam (column-tile-0 blocks)
+  const bool need_db = EPI == GEMM_EPI_BWD_WEIGHT && ep.gb_src &&
+                       (ep.b_scale || (ep.ad_p && ep.sm_p && tn == 0));
+  if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
+    if (ep.b_scale) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = cw + j * 16 + c;
+        e_s[j] = ep.b_scale[col];
+        e_t[j] = ep.b_shift[col];
+      }
+    }
+    if (need_db) {
+      // db[n] partials of this block's rows, one row per thread (tid < BM)
+      if (tid < BM) {
+#pragma unroll
+        for (int q = 0; q < QG; ++q) {
+          const int pp = min(q, ep.gb_parts - 1);
+          e_g[q] = ep.gb_src[(size_t)pp * ep.gb_stride + m0 + tid];
+        }
+      }
     }
   }
 
@@ -262,17 +287,6 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
     const int k0 = s * IA::BK;
     issue_stage<T, AK, BM, NT>(base, A, lda, m0, k0, tid);
     issue_stage<T, BK_, BN, NT>(base + IA::BYTES, B, ldb, n0, k0, tid);
-    if constexpr (ATR) {
-      // one copy of [scale(k0..k0+BK) | shift(k0..k0+BK)] for the A-side
-      // affine, by wave 0 (its extra DMA only makes its counted wait stricter)
-      if (w == 0) {
-        constexpr int Q = IA::BK / 4;
-        const float* src = lane < Q ? ep.a_scale + k0 + 4 * lane
-                                    : (lane < 2 * Q ? ep.a_shift + k0 + 4 * (lane - Q) : ep.a_scale + k0);
-        __builtin_amdgcn_global_load_lds((const void*)src,
-                                         (MMAD_LDS void*)(base + IA::BYTES + IB::BYTES), 16, 0, 0);
-      }
-    }
   };
 
 #pragma unroll
@@ -286,7 +300,6 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
     if (t + NS - 1 < nt) issue(t + NS - 1);
     const char* sa = smem + (t % NS) * SLOT;
     const char* sb = sa + IA::BYTES;
-    const char* sc = sb + IB::BYTES;       // affine copy (ATR)
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
       for (int kk = 0; kk < IA::BK / 32; ++kk) {
@@ -295,21 +308,6 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         for (int i = 0; i < TM; ++i) fa[i] = frag_bf16<AK, NAT, BM>(sa, wm * 16 * TM + i * 16, kk, lane);
 #pragma unroll
         for (int j = 0; j < TN; ++j) fb[j] = frag_bf16<BK_, NAT, BN>(sb, wn * 16 * TN + j * 16, kk, lane);
-        if constexpr (ATR) {
-          const int g = lane >> 4;
-          const int k1 = NAT ? kk * 32 + 8 * g : kk * 32 + 4 * g;
-          const int k2 = NAT ? k1 + 4 : k1 + 16;
-          const floatx4 s0 = *(const floatx4*)(sc + k1 * 4);
-          const floatx4 s1 = *(const floatx4*)(sc + k2 * 4);
-          const floatx4 t0 = *(const floatx4*)(sc + (IA::BK + k1) * 4);
-          const floatx4 t1 = *(const floatx4*)(sc + (IA::BK + k2) * 4);
-#pragma unroll
-          for (int i = 0; i < TM; ++i) fa[i] = affine8(fa[i], s0, s1, t0, t1);
-        }
-        if constexpr (BTR) {
-#pragma unroll
-          for (int j = 0; j < TN; ++j) fb[j] = affine8c(fb[j], sbn[j], tbn[j]);
-        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -324,21 +322,6 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         for (int i = 0; i < TM; ++i) fa[i] = frag_f32<AK, BM>(sa, wm * 16 * TM + i * 16, kc, lane);
 #pragma unroll
         for (int j = 0; j < TN; ++j) fb[j] = frag_f32<BK_, BN>(sb, wn * 16 * TN + j * 16, kc, lane);
-        if constexpr (ATR) {
-          const int g4 = (lane >> 4) * 4;
-          const floatx4 s0 = *(const floatx4*)(sc + (kc * 16 + g4) * 4);
-          const floatx4 t0 = *(const floatx4*)(sc + (IA::BK + kc * 16 + g4) * 4);
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) fa[i][e] = fa[i][e] * s0[e] + t0[e];
-        }
-        if constexpr (BTR) {
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) fb[j][e] = fb[j][e] * sbn[j] + tbn[j];
-        }
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -360,17 +343,48 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
     return;
   }
   // ===================== epilogue, register phase ==========================
-  const int g = lane >> 4, c = lane & 15;
-  const int rw = m0 + wm * 16 * TM;  // first row of this wave
-  const int cw = n0 + wn * 16 * TN;  // first col of this wave
+  float db_own = 0.f;                        // db[m0 + tid] (tid < BM, need_db)
+  if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
+    if (need_db && tid < BM) {
+      // sequential partial order (= the flat reduction's)
+#pragma unroll
+      for (int q = 0; q < QG; ++q) db_own += q < ep.gb_parts ? e_g[q] : 0.f;
+      for (int q = QG; q < ep.gb_parts; ++q) db_own += ep.gb_src[(size_t)q * ep.gb_stride + m0 + tid];
+    }
+    if (ep.b_scale) {
+      __syncthreads();                       // ring LDS no longer read
+      float* gbl = (float*)smem;
+      if (tid < BM) gbl[tid] = db_own;
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float db = gbl[wm * 16 * TM + i * 16 + 4 * g + r];
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j][r] = fmaf(e_s[j], acc[i][j][r], e_t[j] * db);
+        }
+    }
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = cw + j * 16 + c;
     const bool cvalid = col < ep.N;
     float bias = 0.f, sc = 1.f, sh = 0.f;
-    if (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_MSE || EPI == GEMM_EPI_SCORE) {
-      if (ep.bias) bias = ep.bias[col];
-      if (ep.bn_scale) { sc = ep.bn_scale[col]; sh = ep.bn_shift[col]; }
+    if constexpr (FWDLIKE) {
+      bias = e_b[j];
+      sc = e_s[j];
+      sh = e_t[j];
+      if (EPI != GEMM_EPI_SCORE && ep.bpart) {
+        // + sum_k shift[k] W[n][k]: lane-group sums, then ((g0+g1)+(g2+g3))
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < QB; ++q) t += g + 4 * q < ep.bparts ? e_p[j][q] : 0.f;
+        for (int p = 4 * QB + g; p < ep.bparts; p += 4) t += ep.bpart[(size_t)p * ep.bpstride + col];
+        t += __shfl_xor(t, 16);
+        t += __shfl_xor(t, 32);
+        bias += t;
+      }
     }
     float s1[TM / 2], s2[TM / 2];
 #pragma unroll
@@ -383,7 +397,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         const bool valid = cvalid && row < ep.M;
         float v = acc[i][j][r];
         if (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_SCORE) {
-          v = apply_act(v + bias, ep.act, ep.slope) * sc + sh;
+          v = fmaf(apply_act(v + bias, ep.act, ep.slope), sc, sh);   // pinned: tile-independent
           v = valid ? v : 0.f;
           s1[i >> 1] += v;
         } else if (EPI == GEMM_EPI_MSE) {
@@ -478,76 +492,105 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   constexpr int ITERS = BM * CPR / NT;
   constexpr int CPR128 = 128 * (int)sizeof(TO) / 16;  // chunks per 128-column score group
   TO* out = (TO*)ep.out;
+  if (EPI == GEMM_EPI_BWD_WEIGHT && ep.ad_p) {
+    // torch.optim.Adam on the dW tile (4 fp32 per chunk), same formula as
+    // adam_k.  p/m/v of AG chunks are loaded before any of them is stored
+    // (the three state arrays may alias as far as the compiler knows).
+    constexpr int AG = ITERS < 4 ? ITERS : 4;
+    static_assert(ITERS % AG == 0, "Adam chunk groups");
 #pragma unroll
-  for (int it = 0; it < ITERS; ++it) {
-    const int idx = it * NT + tid;
-    const int rl = idx / CPR, ch = idx % CPR;
-    const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
-    const int row = m0 + rl;
-    const int col = n0 + ch * OEPC;
-    if (EPI != GEMM_EPI_BWD_WEIGHT || !(ep.ad_p && ep.dw_nostore))
-      *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
-    if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
-      if (ep.ad_p) {
-        // torch.optim.Adam on this dW chunk (4 fp32), same formula as adam_k
-        const size_t off = (size_t)row * ep.ldo + col;
-        floatx4 gg = __builtin_bit_cast(floatx4, v);
-        floatx4 pp = *(floatx4*)(ep.ad_p + off), mm = *(floatx4*)(ep.ad_m + off);
-        floatx4 vv = *(floatx4*)(ep.ad_v + off);
-        adam4(pp, mm, vv, gg, ep.ad_b1, ep.ad_b2, ep.ad_eps, ep.ad_step, ep.ad_bc2);
-        *(floatx4*)(ep.ad_p + off) = pp;
-        *(floatx4*)(ep.ad_m + off) = mm;
-        *(floatx4*)(ep.ad_v + off) = vv;
+    for (int i0 = 0; i0 < ITERS; i0 += AG) {
+      floatx4 P[AG], Mm[AG], Vv[AG];
+      size_t off[AG];
+#pragma unroll
+      for (int u = 0; u < AG; ++u) {
+        const int idx = (i0 + u) * NT + tid;
+        const int rl = idx / CPR, ch = idx % CPR;
+        off[u] = (size_t)(m0 + rl) * ep.ldo + n0 + ch * OEPC;
+        P[u] = *(const floatx4*)(ep.ad_p + off[u]);
+        Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
+        Vv[u] = *(const floatx4*)(ep.ad_v + off[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < AG; ++u) {
+        const int idx = (i0 + u) * NT + tid;
+        const int rl = idx / CPR, ch = idx % CPR;
+        const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
+        if (!ep.dw_nostore) *(uint4v*)(out + off[u]) = v;
+        adam4(P[u], Mm[u], Vv[u], __builtin_bit_cast(floatx4, v), ep.ad_b1, ep.ad_b2, ep.ad_eps,
+              ep.ad_step, ep.ad_bc2);
+        *(floatx4*)(ep.ad_p + off[u]) = P[u];
+        *(floatx4*)(ep.ad_m + off[u]) = Mm[u];
+        *(floatx4*)(ep.ad_v + off[u]) = Vv[u];
         if (ep.ad_shadow) {
           bf16x4 sh;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) sh[e] = (bf16)pp[e];
-          *(bf16x4*)((bf16*)ep.ad_shadow + off) = sh;
+          for (int e = 0; e < 4; ++e) sh[e] = (bf16)P[u][e];
+          *(bf16x4*)((bf16*)ep.ad_shadow + off[u]) = sh;
         }
       }
     }
-    if (EPI == GEMM_EPI_SCORE) {
-      const TO* ref = (const TO*)ep.ref + (size_t)row * ep.ldref + col;
-      const uint4v rv = *(const uint4v*)ref;
-      const TO* pv = (const TO*)&v;
-      const TO* pr = (const TO*)&rv;
-      float sq = 0.f;
-      float dd[OEPC];
+  } else {
+    // SCORE: every reference chunk loaded before the loop's stores
+    uint4v rvs[EPI == GEMM_EPI_SCORE ? ITERS : 1];
+    if constexpr (EPI == GEMM_EPI_SCORE) {
 #pragma unroll
-      for (int e = 0; e < OEPC; ++e) {
-        dd[e] = to_f32<TO>(pv[e]) - to_f32<TO>(pr[e]);
-        sq += dd[e] * dd[e];
+      for (int it = 0; it < ITERS; ++it) {
+        const int idx = it * NT + tid;
+        const int rl = idx / CPR, ch = idx % CPR;
+        rvs[it] = *(const uint4v*)((const TO*)ep.ref + (size_t)(m0 + rl) * ep.ldref + n0 + ch * OEPC);
       }
-      if (ep.diff && row < ep.M) {
-        float* dp = ep.diff + (size_t)row * ep.lddiff + col;
+    }
 #pragma unroll
-        for (int e = 0; e < OEPC; ++e)
-          if (col + e < ep.N) dp[e] = dd[e];
+    for (int it = 0; it < ITERS; ++it) {
+      const int idx = it * NT + tid;
+      const int rl = idx / CPR, ch = idx % CPR;
+      const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
+      const int row = m0 + rl;
+      const int col = n0 + ch * OEPC;
+      *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
+      if constexpr (EPI == GEMM_EPI_SCORE) {
+        const uint4v rv = rvs[it];
+        const TO* pv = (const TO*)&v;
+        const TO* pr = (const TO*)&rv;
+        float sq = 0.f;
+        float dd[OEPC];
+#pragma unroll
+        for (int e = 0; e < OEPC; ++e) {
+          dd[e] = to_f32<TO>(pv[e]) - to_f32<TO>(pr[e]);
+          sq += dd[e] * dd[e];
+        }
+        if (ep.diff && row < ep.M) {
+          float* dp = ep.diff + (size_t)row * ep.lddiff + col;
+#pragma unroll
+          for (int e = 0; e < OEPC; ++e)
+            if (col + e < ep.N) dp[e] = dd[e];
+        }
+#pragma unroll
+        for (int o = 1; o < CPR128; o <<= 1) sq += __shfl_xor(sq, o);
+        if (ch % CPR128 == 0) ep.rowsq[(size_t)(col / 128) * ep.ldrow + row] = sq;
       }
-#pragma unroll
-      for (int o = 1; o < CPR128; o <<= 1) sq += __shfl_xor(sq, o);
-      if (ch % CPR128 == 0) ep.rowsq[(size_t)(col / 128) * ep.ldrow + row] = sq;
     }
   }
   if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
     if (ep.ad_p && ep.sm_p) {
-      // the layer's bias/gamma/beta Adam, 4 elements per thread, spread over
-      // the output tiles (one epilogue block per tile)
-      for (int q = lt * NT + tid; q * 4 < ep.sm_n; q += nblk * NT) {
-        const int i4 = q * 4;
-        floatx4 gg;
-        if (ep.sm_bsrc && i4 < ep.sm_bNp) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float t = 0.f;
-            if (i4 + e < ep.sm_bN)
-              for (int i = 0; i < ep.sm_bparts; ++i) t += ep.sm_bsrc[(size_t)i * ep.sm_bstride + i4 + e];
-            gg[e] = t;
-          }
-          *(floatx4*)(ep.sm_g + i4) = gg;
-        } else {
-          gg = *(const floatx4*)(ep.sm_g + i4);
-        }
+      // the layer's small segment [bias | gamma | beta].  Bias: the
+      // column-tile-0 blocks, one output row per thread, g = db (computed
+      // above from the same partials the flat path reduces, same order).
+      if (tn == 0 && tid < BM && m0 + tid < ep.sm_bNp) {
+        const int n = m0 + tid;
+        float g = ep.gb_src ? (n < ep.sm_bN ? db_own : 0.f) : ep.sm_g[n];
+        if (ep.gb_src) ep.sm_g[n] = g;
+        float pp = ep.sm_p[n], mm = ep.sm_m[n], vv = ep.sm_v[n];
+        adam_elem(pp, mm, vv, g, ep.ad_b1, ep.ad_b2, ep.ad_eps, ep.ad_step, ep.ad_bc2);
+        ep.sm_p[n] = pp;
+        ep.sm_m[n] = mm;
+        ep.sm_v[n] = vv;
+      }
+      // gamma | beta (grads already final), 4 per thread over all tiles
+      for (int q = lt * NT + tid; ep.sm_bNp + q * 4 < ep.sm_n; q += nblk * NT) {
+        const int i4 = ep.sm_bNp + q * 4;
+        const floatx4 gg = *(const floatx4*)(ep.sm_g + i4);
         floatx4 pp = *(floatx4*)(ep.sm_p + i4), mm = *(floatx4*)(ep.sm_m + i4);
         floatx4 vv = *(floatx4*)(ep.sm_v + i4);
         adam4(pp, mm, vv, gg, ep.ad_b1, ep.ad_b2, ep.ad_eps, ep.ad_step, ep.ad_bc2);
@@ -624,7 +667,7 @@ static int heuristic_cfg(int Mp, int Np, int epi) {
   return cfg_fits(4, Mp, Np, epi) ? 4 : 0;
 }
 
-template <typename T, typename TO, bool AK, bool BK_, int EPI, bool TR>
+template <typename T, typename TO, bool AK, bool BK_, int EPI>
 static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np, int K,
                         const GemmEpi& ep_in, int cfg, hipStream_t s) {
   const int BM = CFG_BM[cfg], BN = CFG_BN[cfg];
@@ -640,12 +683,12 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
   ep.group_m = gm < 1 ? 1 : (gm > tiles_m ? tiles_m : gm);
   dim3 grd(ntiles), blk(CFG_NT[cfg]);
   switch (cfg) {
-    case 0: mmad_gemm_kernel<T, TO, AK, BK_, 0, EPI, TR><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
-    case 1: mmad_gemm_kernel<T, TO, AK, BK_, 1, EPI, TR><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
-    case 2: mmad_gemm_kernel<T, TO, AK, BK_, 2, EPI, TR><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
-    case 3: mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI, TR><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
-    case 4: mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI, TR><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
-    default: mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI, TR><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
+    case 0: mmad_gemm_kernel<T, TO, AK, BK_, 0, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
+    case 1: mmad_gemm_kernel<T, TO, AK, BK_, 1, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
+    case 2: mmad_gemm_kernel<T, TO, AK, BK_, 2, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
+    case 3: mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
+    case 4: mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
+    default: mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
   }
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
@@ -653,25 +696,15 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
 
 static int launch_cfg(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,
                       int Np, int K, const GemmEpi& ep, int cfg, hipStream_t s) {
-  const bool atr = ep.a_scale != nullptr, btr = ep.b_scale != nullptr;
-#define MMAD_LT(T, TO, AK, BK_, EPI, TR)                                                  \
-  return launch_tiled<T, TO, AK, BK_, EPI, TR>((const T*)A, lda, (const T*)B, ldb, Mp, Np, K, ep, \
-                                               cfg, s)
+#define MMAD_LT(T, TO, AK, BK_, EPI)                                                      \
+  return launch_tiled<T, TO, AK, BK_, EPI>((const T*)A, lda, (const T*)B, ldb, Mp, Np, K, ep, cfg, s)
 #define MMAD_DISPATCH_T(T)                                                               \
   switch (epi) {                                                                         \
-    case GEMM_EPI_FWD:                                                                   \
-      if (atr) MMAD_LT(T, T, true, true, GEMM_EPI_FWD, true);                            \
-      MMAD_LT(T, T, true, true, GEMM_EPI_FWD, false);                                    \
-    case GEMM_EPI_MSE:                                                                   \
-      if (atr) MMAD_LT(T, T, true, true, GEMM_EPI_MSE, true);                            \
-      MMAD_LT(T, T, true, true, GEMM_EPI_MSE, false);                                    \
-    case GEMM_EPI_SCORE:                                                                 \
-      MMAD_LT(T, T, true, true, GEMM_EPI_SCORE, false);                                  \
-    case GEMM_EPI_BWD_DATA:                                                              \
-      MMAD_LT(T, T, true, false, GEMM_EPI_BWD_DATA, false);                              \
-    case GEMM_EPI_BWD_WEIGHT:                                                            \
-      if (btr) MMAD_LT(T, float, false, false, GEMM_EPI_BWD_WEIGHT, true);               \
-      MMAD_LT(T, float, false, false, GEMM_EPI_BWD_WEIGHT, false);                       \
+    case GEMM_EPI_FWD: MMAD_LT(T, T, true, true, GEMM_EPI_FWD);                          \
+    case GEMM_EPI_MSE: MMAD_LT(T, T, true, true, GEMM_EPI_MSE);                          \
+    case GEMM_EPI_SCORE: MMAD_LT(T, T, true, true, GEMM_EPI_SCORE);                      \
+    case GEMM_EPI_BWD_DATA: MMAD_LT(T, T, true, false, GEMM_EPI_BWD_DATA);               \
+    case GEMM_EPI_BWD_WEIGHT: MMAD_LT(T, float, false, false, GEMM_EPI_BWD_WEIGHT);      \
     default: mmad_set_error("gemm: bad epilogue %d", epi); return MMAD_EINVAL;          \
   }
   if (dtype == MMAD_BF16) {
@@ -686,10 +719,10 @@ static int launch_cfg(int dtype, int epi, const void* A, int lda, const void* B,
 // ---- autotune: time every fitting tile config once per problem shape -------
 namespace {
 struct TuneKey {
-  int dtype, epi, atr, btr, Mp, Np, K;
+  int dtype, epi, Mp, Np, K;
   bool operator<(const TuneKey& o) const {
-    const int a[7] = {dtype, epi, atr, btr, Mp, Np, K}, b[7] = {o.dtype, o.epi, o.atr, o.btr, o.Mp, o.Np, o.K};
-    for (int i = 0; i < 7; ++i)
+    const int a[5] = {dtype, epi, Mp, Np, K}, b[5] = {o.dtype, o.epi, o.Mp, o.Np, o.K};
+    for (int i = 0; i < 5; ++i)
       if (a[i] != b[i]) return a[i] < b[i];
     return false;
   }
@@ -733,11 +766,11 @@ static int tune_cfg(int dtype, int epi, const void* A, int lda, const void* B, i
   return MMAD_OK;
 }
 
-int mmad_gemm_plan(int Mp, int Np, int K, int epi, int dtype, bool atr, bool btr) {
+int mmad_gemm_plan(int Mp, int Np, int K, int epi, int dtype) {
   const int env = mmad_tile_override();
   if (env >= 0 && env < NCFG && cfg_fits(env, Mp, Np, epi)) return env;
   std::lock_guard<std::mutex> lk(g_tune_mu);
-  auto it = g_tune.find(TuneKey{dtype, epi, atr, btr, Mp, Np, K});
+  auto it = g_tune.find(TuneKey{dtype, epi, Mp, Np, K});
   return it != g_tune.end() ? it->second : heuristic_cfg(Mp, Np, epi);
 }
 
@@ -749,13 +782,12 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   MMAD_CHECK_ARG(dtype == MMAD_BF16 || dtype == MMAD_F32, "gemm: bad dtype %d", dtype);
   GemmEpi ep = ep_in;
   ep.dbg = mmad_dbg_override();
-  const bool atr = ep.a_scale != nullptr, btr = ep.b_scale != nullptr;
   const int env = mmad_tile_override();
   int cfg;
   if (env >= 0 && env < NCFG && cfg_fits(env, Mp, Np, epi)) {
     cfg = env;   // forced tile (tuning / tests); a shape it does not fit falls through
   } else {
-    const TuneKey key{dtype, epi, atr, btr, Mp, Np, K};
+    const TuneKey key{dtype, epi, Mp, Np, K};
     int found = -1;
     {
       std::lock_guard<std::mutex> lk(g_tune_mu);

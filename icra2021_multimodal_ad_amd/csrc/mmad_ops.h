@@ -39,6 +39,15 @@ int mmad_bn_finalize(int M, int N, int Mp, int Np, const float* stats, const flo
                      const float* beta, float* running_mean, float* running_var, float momentum,
                      float eps, float* save_mean, float* save_rstd, float* scale, float* shift,
                      void* stream);
+// train-mode BN finalize of a producer layer (Np columns) fused with the
+// fold into its consumer's weights: wout[n][k] = W[n][k] * scale[k] (dtype of
+// the GEMM), cpart[k/64][n] = sum_{k in block} shift[k] * W[n][k].
+// W: fp32 master [Nc_p][Np]; grid (Np/64) x (Nc_p/64).
+int mmad_bn_finalize_fold(int dtype, int M, int N, int Mp, int Np, const float* stats,
+                          const float* gamma, const float* beta, float* running_mean,
+                          float* running_var, float momentum, float eps, float* save_mean,
+                          float* save_rstd, float* scale, float* shift, const float* W, int Nc_p,
+                          void* wout, float* cpart, void* stream);
 int mmad_bn_act_bwd_apply(int dtype, int act, float slope, int M, int N, int Mp, int Np,
                           const void* dy, const void* a, const float* save_mean,
                           const float* save_rstd, const float* gamma, const float* part,

@@ -170,6 +170,112 @@ __global__ __launch_bounds__(64) void bn_finalize_k(int M, int N, int Np, const 
   }
 }
 
+// Finalize + fold.  Block (kb, nb): the 64 producer columns k0..k0+63 (its
+// Welford merge is recomputed per n-block: 16 KB of L2 reads) and the 64
+// consumer rows n0..n0+63 of W.  Merge order: 4 chunk groups (g, g+4, ...)
+// each sequential, then groups 0..3 in order.
+template <typename TW>
+__global__ __launch_bounds__(256) void bn_fold_k(int M, int N, int Np, const float* __restrict__ stats,
+                                                 int nparts, const float* __restrict__ gamma,
+                                                 const float* __restrict__ beta, float* rmean,
+                                                 float* rvar, float momentum, float eps,
+                                                 float* save_mean, float* save_rstd, float* scale,
+                                                 float* shift, const float* __restrict__ W,
+                                                 TW* __restrict__ wout, float* __restrict__ cpart) {
+  constexpr int U = 8;
+  __shared__ float pm[4][64], pq[4][64], pn[4][64], s_sc[64], s_sh[64];
+  const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64, tid = threadIdx.x;
+  // W tile loads first (independent of the statistics): row r, 16 columns
+  const int r = tid >> 2, cq = (tid & 3) * 16;
+  floatx4 wv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) wv[u] = *(const floatx4*)(W + (size_t)(n0 + r) * Np + k0 + cq + 4 * u);
+  {
+    const int c = tid & 63, grp = tid >> 6;
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+    for (int i0 = grp; i0 < nparts; i0 += 4 * U) {
+      float mb[U], qb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = min(i0 + 4 * u, nparts - 1);
+        mb[u] = stats[(size_t)i * 2 * Np + k0 + c];
+        qb[u] = stats[((size_t)i * 2 + 1) * Np + k0 + c];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + 4 * u;
+        int cnt = M - i * MMAD_PART_ROWS;
+        cnt = cnt < 0 ? 0 : (cnt > MMAD_PART_ROWS ? MMAD_PART_ROWS : cnt);
+        if (i >= nparts || cnt == 0) continue;
+        const float nb = (float)cnt, nn = n + nb, d = mb[u] - mean;
+        mean += d * (nb / nn);
+        m2 += qb[u] + d * d * (n * nb / nn);
+        n = nn;
+      }
+    }
+    pm[grp][c] = mean;
+    pq[grp][c] = m2;
+    pn[grp][c] = n;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float n1 = 0.f, mu = 0.f, q = 0.f;
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const float nb = pn[gq][tid];
+      if (nb == 0.f) continue;
+      const float nn = n1 + nb, d = pm[gq][tid] - mu;
+      mu += d * (nb / nn);
+      q += pq[gq][tid] + d * d * (n1 * nb / nn);
+      n1 = nn;
+    }
+    const float var = n1 > 0.f ? q / n1 : 0.f;
+    const int col = k0 + tid;
+    float sc = 0.f, sh = 0.f;
+    if (col < N) {
+      const float rstd = rsqrtf(var + eps);
+      sc = gamma[col] * rstd;
+      sh = beta[col] - mu * sc;
+      if (blockIdx.y == 0) {
+        save_mean[col] = mu;
+        save_rstd[col] = rstd;
+        const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+        rmean[col] = (1.f - momentum) * rmean[col] + momentum * mu;
+        rvar[col] = (1.f - momentum) * rvar[col] + momentum * unb;
+      }
+    } else if (blockIdx.y == 0) {
+      save_mean[col] = 0.f;
+      save_rstd[col] = 0.f;
+    }
+    if (blockIdx.y == 0) {
+      scale[col] = sc;
+      shift[col] = sh;
+    }
+    s_sc[tid] = sc;
+    s_sh[tid] = sh;
+  }
+  __syncthreads();
+  // W' = W * scale (row r, 16 columns), c = sum shift * W (sequential, then
+  // the 4 quarter-row lanes combined ((q0 + q1) + (q2 + q3)))
+  float cs = 0.f;
+  TW o[16];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int kl = cq + 4 * u + e;
+      o[4 * u + e] = from_f32<TW>(wv[u][e] * s_sc[kl]);
+      cs += s_sh[kl] * wv[u][e];
+    }
+  TW* dst = wout + (size_t)(n0 + r) * Np + k0 + cq;
+#pragma unroll
+  for (int v = 0; v < 16 * (int)sizeof(TW) / 16; ++v)
+    *((uint4v*)dst + v) = *((const uint4v*)o + v);
+  cs += __shfl_xor(cs, 1);
+  cs += __shfl_xor(cs, 2);
+  if ((tid & 3) == 0) cpart[(size_t)blockIdx.x * gridDim.y * 64 + n0 + r] = cs;
+}
+
 // ---------------------------------------------------------------------------
 // BN(train) + activation backward.  Pass 1: per-slab partial sums of dy and
 // dy*xhat.  Pass 2: finalise dgamma/dbeta, dz, and db partials.
@@ -683,6 +789,27 @@ int mmad_bn_finalize(int M, int N, int Mp, int Np, const float* stats, const flo
   bn_finalize_k<<<Np / 64, 64, 0, (hipStream_t)stream>>>(
       M, N, Np, stats, Mp / MMAD_PART_ROWS, gamma, beta, running_mean, running_var, momentum, eps,
       save_mean, save_rstd, scale, shift);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_bn_finalize_fold(int dtype, int M, int N, int Mp, int Np, const float* stats,
+                          const float* gamma, const float* beta, float* running_mean,
+                          float* running_var, float momentum, float eps, float* save_mean,
+                          float* save_rstd, float* scale, float* shift, const float* W, int Nc_p,
+                          void* wout, float* cpart, void* stream) {
+  MMAD_CHECK_ARG(Mp % 128 == 0 && Np % 128 == 0 && Nc_p % 64 == 0 && M >= 1 && M <= Mp && N <= Np,
+                 "bn_finalize_fold: bad sizes");
+  dim3 grd(Np / 64, Nc_p / 64);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMAD_BF16)
+    bn_fold_k<bf16><<<grd, 256, 0, s>>>(M, N, Np, stats, Mp / MMAD_PART_ROWS, gamma, beta,
+                                        running_mean, running_var, momentum, eps, save_mean,
+                                        save_rstd, scale, shift, W, (bf16*)wout, cpart);
+  else
+    bn_fold_k<float><<<grd, 256, 0, s>>>(M, N, Np, stats, Mp / MMAD_PART_ROWS, gamma, beta,
+                                         running_mean, running_var, momentum, eps, save_mean,
+                                         save_rstd, scale, shift, W, (float*)wout, cpart);
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
 }

@@ -18,12 +18,16 @@ def short(name):
         # template args: T, TO, AK, BK_, CFG, EPI, TR
         if name.startswith("_Z"):
             a = re.findall(r"Lb([01])E|Li(\d+)E", name)
-            vals = [x[0] or x[1] for x in a]
+            vals = [x[0] or x[1] for x in a] + ["0"]
             ak, bk, cfg, epi, tr = vals[:5]
         else:
             inner = name[name.index("<") + 1:name.index(">")]
             parts = [p.strip() for p in inner.split(",")]
-            ak, bk, cfg, epi, tr = parts[-5:]
+            if parts[-1] in ("true", "false"):
+                ak, bk, cfg, epi, tr = parts[-5:]
+            else:
+                ak, bk, cfg, epi = parts[-4:]
+                tr = "false"
             tr = "1" if tr == "true" else "0"
         epin = {"0": "fwd", "1": "mse", "2": "bwd_data", "3": "bwd_w", "4": "score"}[epi]
         return f"gemm[{epin} cfg{cfg}{' tr' if tr == '1' else ''}]"
