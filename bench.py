@@ -173,7 +173,10 @@ def main():
         "config": {"workload": f"FC-AE train step (fwd+sum-MSE+bwd+Adam), D={args.dim}, btl=100, "
                                f"n_layers=5, {args.batch} windows/GPU",
                    "global_batch": args.batch * world, "input_dim": args.dim,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}",
+                   "exchange": ("native RCCL per-layer buckets overlapped with backward"
+                                if model.dist is not None and model.dist.native else
+                                ("torch.distributed flat all-reduce" if world > 1 else "none"))},
         "model_tflops": round(value * fpw / 1e12, 2),
         "final_loss": loss_v,
     }
@@ -184,6 +187,9 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()
+        if model.dist is not None and model.dist.native:
+            model._native.set_comm(None)
+            model.dist.close()
         dist.destroy_process_group()
 
 

@@ -209,7 +209,9 @@ class AutoEncoder(AbstractModel):
         self.train()
         nat = self._native
         seed = 0x9E3779B97F4A7C15 & ((1 << 63) - 1)
-        if self.dist is None:
+        if self.dist is None or self.dist.native:
+            # single process, or data parallel with the native RCCL exchange
+            # (per-layer all-reduce + Adam inside the executor's step)
             lr, betas, aeps = self._adam_hyper(optimizer)
             loss = nat.train_step_fused(x, lr=lr, betas=betas, adam_eps=aeps, k=self.k, eps=eps,
                                         seed=seed, offset=self._rng_offset, beta_kl=self.beta_kl)

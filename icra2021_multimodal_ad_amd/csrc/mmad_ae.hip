@@ -21,6 +21,7 @@
 #include "mmad_common.h"
 #include "mmad_gemm.h"
 #include "mmad_ops.h"
+#include "mmad_comm.h"
 
 #define RET_IF(x)                    \
   do {                               \
@@ -46,6 +47,11 @@ struct mmad_ae {
   std::vector<hipEvent_t> ev_fork, ev_data;
   hipEvent_t ev_join = nullptr;
   int mse_tiles = 0;   // loss partials written by the last MSE GEMM
+  // data parallelism: RCCL communicator (not owned), its stream and events
+  mmad_comm* comm = nullptr;
+  hipStream_t cstream = nullptr;
+  std::vector<hipEvent_t> ev_dw;
+  hipEvent_t ev_small = nullptr, ev_cdone = nullptr;
   // fused step: dW GEMMs of layers < dw_main run on the caller's stream;
   // keep_grads: also write dW to the grads buffer
   int dw_main = [] {
@@ -60,6 +66,10 @@ struct mmad_ae {
     for (auto e : ev_fork) (void)hipEventDestroy(e);
     for (auto e : ev_data) (void)hipEventDestroy(e);
     if (ev_join) (void)hipEventDestroy(ev_join);
+    for (auto e : ev_dw) (void)hipEventDestroy(e);
+    if (ev_small) (void)hipEventDestroy(ev_small);
+    if (ev_cdone) (void)hipEventDestroy(ev_cdone);
+    if (cstream) (void)hipStreamDestroy(cstream);
     if (side) (void)hipStreamDestroy(side);
   }
 };
@@ -425,11 +435,13 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       dwe.gb_parts = gs.nparts;
       dwe.gb_stride = gs.stride;
     }
-    if (!adam) {
+    const bool dp = adam && h->comm;
+    if (!adam || dp) {
       // fork: dz_l is complete on the main stream; dW_l overlaps the chain below
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
       MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
       RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side));
+      if (dp) MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l], side));
     }
     if (l > 0) {
       const AeLayer& p = h->L[l - 1];
@@ -467,7 +479,21 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
                                   a.Np, ep, st));
       }
     }
-    if (adam) {
+    if (dp) {
+      // data parallel: all-reduce dW_l on the comm stream as soon as it is
+      // complete, then its Adam update (which rewrites W_l, so it also waits
+      // for the main stream's bwd-data of layer l)
+      if (l == 0 || !(h->L[l - 1].bn) || (h->vib && l == h->n_enc))
+        MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
+      MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_dw[l], 0));
+      MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_data[l], 0));
+      const int64_t n = (int64_t)a.Np * a.Kp;
+      RET_IF(mmad_allreduce_bucket(h->comm, h->grads + a.w_off, n, h->cstream));
+      RET_IF(mmad_adam(n, h->params + a.w_off, h->grads + a.w_off, h->m + a.w_off, h->v + a.w_off,
+                       adam->b1, adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt,
+                       h->dtype == MMAD_BF16 ? (void*)((char*)h->shadow + a.w_off * 2) : nullptr,
+                       h->dtype == MMAD_BF16 ? n : 0, h->cstream));
+    } else if (adam) {
       // dW_l with this layer's Adam update fused into its epilogue.  It rewrites
       // W_l, so it starts only once the main stream has finished reading W_l
       // (bwd-data of l); the rest of the chain keeps overlapping it.
@@ -588,7 +614,38 @@ int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const
   const AdamHyper ah = adam_hyper(lr, beta1, beta2, adam_eps, step);
   RET_IF(run_forward(h, w, x, ld_x, 0, eps, seed, offset, st));
   RET_IF(run_backward(h, w, true, beta_kl, &ah, st));
-  return finish_reductions(h, w, false, true, beta_kl, loss_out, st);
+  if (!h->comm) return finish_reductions(h, w, false, true, beta_kl, loss_out, st);
+  // data parallel tail: bias grads + loss, then one small bucket
+  // [all bias | gamma | beta grads] + the loss, its Adam, join
+  RET_IF(finish_reductions(h, w, true, true, beta_kl, loss_out, st));
+  MMAD_HIP_CHECK(hipEventRecord(h->ev_small, st));
+  MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_small, 0));
+  const int64_t ns = h->n_params - h->n_weight;
+  RET_IF(mmad_allreduce_bucket(h->comm, h->grads + h->n_weight, ns, h->cstream));
+  RET_IF(mmad_allreduce_bucket(h->comm, loss_out, 1, h->cstream));
+  RET_IF(mmad_adam(ns, h->params + h->n_weight, h->grads + h->n_weight, h->m + h->n_weight,
+                   h->v + h->n_weight, ah.b1, ah.b2, ah.eps, ah.step_size, ah.bc2_sqrt, nullptr, 0,
+                   h->cstream));
+  MMAD_HIP_CHECK(hipEventRecord(h->ev_cdone, h->cstream));
+  MMAD_HIP_CHECK(hipStreamWaitEvent(st, h->ev_cdone, 0));
+  return MMAD_OK;
+}
+
+int mmad_ae_set_comm(mmad_ae* h, mmad_comm* c) {
+  MMAD_CHECK_ARG(h, "ae_set_comm: null handle");
+  MMAD_CHECK_ARG(h->side, "ae_set_comm: bind the handle first");
+  if (c && !h->cstream) {
+    // highest priority: the exchange must not queue behind the dW GEMMs
+    int least = 0, greatest = 0;
+    MMAD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    MMAD_HIP_CHECK(hipStreamCreateWithPriority(&h->cstream, hipStreamNonBlocking, greatest));
+    h->ev_dw.resize(h->L.size());
+    for (auto& e : h->ev_dw) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_small, hipEventDisableTiming));
+    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_cdone, hipEventDisableTiming));
+  }
+  h->comm = c;
+  return MMAD_OK;
 }
 
 int mmad_ae_backward(mmad_ae* h, const float* dxhat, int ld, int B, void* ws, int64_t ws_bytes,

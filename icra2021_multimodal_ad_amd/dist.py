@@ -5,8 +5,17 @@ RCCL on ROCm; xGMI between the GPUs of a node).  Sum, not mean: the reference
 loss is sum-reduced (model_builder.py:42), so the global gradient of the
 concatenated batch is the sum of the shard gradients.  BatchNorm statistics
 stay per shard (DDP semantics).  The grad buffer is one
-contiguous tensor, so the whole exchange is a single large all-reduce (the
-shape xGMI rings like)."""
+contiguous tensor.
+
+Two exchange paths:
+* native (GPU, 'nccl' process group): an RCCL communicator of our own
+  (mmad_comm_*, unique id broadcast over the torch process group) attached to
+  the executor; each layer's weight gradient is all-reduced on the executor's
+  comm stream as soon as its dW GEMM completes -- overlapped with the rest of
+  the backward -- then Adam-updated there; biases/gamma/beta + the loss follow
+  in one small bucket.  One host call per step, no host sync.
+* torch (gloo / fallback): train_fwd_bwd, then one torch.distributed
+  all-reduce of the flat gradient buffer, then the flat Adam."""
 import os
 
 import torch
@@ -27,10 +36,75 @@ def init_from_env(backend=None):
     return rank, world, local
 
 
-class DataParallel:
+class NativeComm:
+    """An RCCL communicator owned by libmmad (include/mmad.h, mmad_comm_*)."""
+
     def __init__(self, group=None):
+        import ctypes
+        from . import _native
+        self._lib = _native.load()
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        n = self._lib.mmad_comm_unique_id_bytes()
+        uid = (ctypes.c_char * n)()
+        if self.rank == 0:
+            _native.check(self._lib.mmad_comm_get_unique_id(uid), "mmad_comm_get_unique_id")
+        obj = [bytes(uid) if self.rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        uid = (ctypes.c_char * n).from_buffer_copy(obj[0])
+        h = ctypes.c_void_p()
+        _native.check(self._lib.mmad_comm_create(ctypes.byref(h), uid, self.world, self.rank),
+                      "mmad_comm_create")
+        self.handle = h
+
+    def close(self):
+        if self.handle is not None and self.handle.value:
+            self._lib.mmad_comm_destroy(self.handle)
+        self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DataParallel:
+    def __init__(self, group=None, native=None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.comm = None
+        if native is None:
+            native = (self.world > 1 and torch.cuda.is_available()
+                      and dist.get_backend(group) == "nccl"
+                      and os.environ.get("MMAD_NATIVE_COMM", "1") != "0")
+        if native:
+            # every rank must agree: fall back to the torch path together if
+            # any rank could not build the communicator
+            comm, err = None, None
+            try:
+                comm = NativeComm(group)
+            except Exception as e:  # noqa: BLE001 -- reported below, then fallback
+                err = e
+            ok = torch.tensor([0.0 if comm is None else 1.0], device="cuda")
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+            if float(ok.item()) == 1.0:
+                self.comm = comm
+            else:
+                if comm is not None:
+                    comm.close()
+                if dist.get_rank(group) == 0:
+                    print(f"[mmad] native RCCL exchange unavailable ({err}); using torch.distributed",
+                          flush=True)
+
+    def close(self):
+        if self.comm is not None:
+            self.comm.close()
+            self.comm = None
+
+    @property
+    def native(self):
+        return self.comm is not None
 
     def all_reduce_grads(self, flat_grads):
         if self.world > 1:
@@ -45,11 +119,15 @@ class DataParallel:
             dist.broadcast(model._native.params, src=src, group=self.group)
 
 
-def attach_data_parallel(model, group=None):
-    """Replicate rank-0 weights and make AutoEncoder.step all-reduce grads."""
-    dp = DataParallel(group)
+def attach_data_parallel(model, group=None, native=None):
+    """Replicate rank-0 weights and make AutoEncoder.step all-reduce grads
+    (natively over RCCL, overlapped with the backward, when the process group
+    is 'nccl'; through torch.distributed otherwise)."""
+    dp = DataParallel(group, native=native)
     dp.broadcast_params(model)
     if dp.world > 1:
         model._native.sync_shadow(force=True)
+    if dp.native:
+        model._native.set_comm(dp.comm)
     model.dist = dp if dp.world > 1 else None
     return model

@@ -91,6 +91,12 @@ class NativeAE:
         self._ws = None
         return self
 
+    def set_comm(self, comm):
+        """Attach a dist.NativeComm (or None): mmad_ae_train_step then all-reduces
+        each layer's gradients on the executor's comm stream before its Adam."""
+        self._comm = comm        # keep the communicator alive as long as the handle uses it
+        call("mmad_ae_set_comm", self._h, comm.handle if comm is not None else None)
+
     def __del__(self):
         try:
             if getattr(self, "_h", None) is not None:

@@ -34,7 +34,7 @@ extern "C" {
 
 #define MMAD_ABI_VERSION 1
 
-enum { MMAD_OK = 0, MMAD_EINVAL = -1, MMAD_EUNSUPPORTED = -2, MMAD_EHIP = -3 };
+enum { MMAD_OK = 0, MMAD_EINVAL = -1, MMAD_EUNSUPPORTED = -2, MMAD_EHIP = -3, MMAD_ERCCL = -4 };
 enum { MMAD_F32 = 0, MMAD_BF16 = 1 };
 /* modules/activation.py:20-45 (names 'leakyrelu', 'relu', 'sigmoid', 'tanh', None) */
 enum { MMAD_ACT_NONE = 0, MMAD_ACT_LEAKYRELU = 1, MMAD_ACT_RELU = 2, MMAD_ACT_SIGMOID = 3,
@@ -44,8 +44,12 @@ const char* mmad_last_error_string(void);
 int mmad_abi_version(void);
 int mmad_pad_granule(void);
 /* Tuning knobs (no reference counterpart): knob 0 = GEMM tile override
- * (-1 auto, 0 = 128x128, 1 = 64x128, 2 = 64x64), knob 1 = XCD tile-group
- * height override (-1 auto).  Defaults from MMAD_GEMM_TILE / MMAD_GEMM_GROUP_M. */
+ * (-1 autotuned; 0 = 128x128/512 thr, 1 = 256x128, 2 = 128x256, 3 = 64x64/256
+ * thr, 4 = 64x128, 5 = 128x128/256 thr; a tile that does not divide a shape
+ * falls back to the tuned one), knob 1 = XCD tile-group height override (-1
+ * auto), knob 2 = per-shape autotune on first dispatch (1, default) or static
+ * heuristic (0), knob 3 = diagnostics (tools/gemm_sweep only).  Defaults from
+ * MMAD_GEMM_TILE / MMAD_GEMM_GROUP_M / MMAD_GEMM_AUTOTUNE. */
 int mmad_tune_set(int knob, int value);
 
 /* ------------------------------------------------------------------------
@@ -202,8 +206,9 @@ int mmad_ae_train_fwd_bwd(mmad_ae* h, const float* x, int ld_x, int B, int k, co
  * optimizer.step() fused in: forward + sum-MSE + backward as in
  * mmad_ae_train_fwd_bwd, and each layer's Adam update (hyper-parameters as
  * mmad_ae_adam, step = t) issued on the executor's side stream right after
- * that layer's dW GEMM, overlapping the rest of the backward.  Single-process
- * only (with data parallelism use train_fwd_bwd + all-reduce + mmad_ae_adam).
+ * that layer's dW GEMM, overlapping the rest of the backward.  With a
+ * communicator attached (mmad_ae_set_comm) the gradients are all-reduced per
+ * layer before their Adam update and the returned loss is the global sum.
  * On return every kernel is enqueued and ordered before later work on
  * `stream`. */
 int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const float* eps,
@@ -216,6 +221,30 @@ int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const
  * writes all parameter gradients.  Not for the VIB model. */
 int mmad_ae_backward(mmad_ae* h, const float* dxhat, int ld, int B, void* ws, int64_t ws_bytes,
                      void* stream);
+
+/* ------------------------------------------------------------------------
+ * Data-parallel gradient exchange (RCCL over xGMI)
+ * The reference trains in one process (novelty_detection.py:90); with one
+ * process per GPU the exchange is a sum all-reduce of the gradients (the loss
+ * is sum-reduced, model_builder.py:42).  RCCL is resolved from the copy
+ * already loaded in the process (torch's), so there is one RCCL instance.
+ * ---------------------------------------------------------------------- */
+typedef struct mmad_comm mmad_comm;
+int mmad_comm_unique_id_bytes(void);
+/* rank 0: fills out[mmad_comm_unique_id_bytes()] (host memory) */
+int mmad_comm_get_unique_id(void* out);
+/* every rank, with the current HIP device set to its GPU */
+int mmad_comm_create(mmad_comm** out, const void* unique_id, int nranks, int rank);
+void mmad_comm_destroy(mmad_comm* c);
+/* in-place fp32 sum all-reduce of buf[n] on stream */
+int mmad_allreduce_bucket(mmad_comm* c, float* buf, int64_t n, void* stream);
+/* Attach (c != NULL) or detach a communicator.  With one attached,
+ * mmad_ae_train_step runs the data-parallel step: each layer's dW lands in the
+ * grads buffer, is all-reduced on the executor's comm stream as soon as it is
+ * complete (overlapping the rest of the backward), then Adam-updated there;
+ * bias/gamma/beta grads and the loss follow in one final bucket.  BatchNorm
+ * statistics stay per shard (DDP semantics). */
+int mmad_ae_set_comm(mmad_ae* h, mmad_comm* c);
 
 /* optimizer.step() (models/auto_encoder.py:75) on the bound buffers. */
 int mmad_ae_adam(mmad_ae* h, float lr, float beta1, float beta2, float eps, int step,

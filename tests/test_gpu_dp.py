@@ -76,3 +76,42 @@ def test_dp_two_ranks_equals_summed_gradient_step():
     assert np.array_equal(p0, p1)
     assert abs(l0 - losses) <= 1e-5 * losses and l0 == l1
     np.testing.assert_allclose(p0, ref, rtol=0, atol=1e-6)
+
+
+def test_native_comm_single_rank_step_matches_fused():
+    """The native RCCL data-parallel step (per-layer all-reduce on the comm
+    stream + flat Adam per bucket) with one rank equals the single-process
+    fused step (all-reduce of one rank is the identity).  Multi-rank RCCL needs
+    one GPU per rank; the exchange semantics are pinned on CPU by
+    tests/test_dist_gloo.py."""
+    import ctypes
+    import types as _t
+    from icra2021_multimodal_ad_amd import _native
+    from icra2021_multimodal_ad_amd.data import synth_windows
+    lib = _native.load()
+    n = lib.mmad_comm_unique_id_bytes()
+    uid = (ctypes.c_char * n)()
+    assert lib.mmad_comm_get_unique_id(uid) == 0, lib.mmad_last_error_string()
+    h = ctypes.c_void_p()
+    assert lib.mmad_comm_create(ctypes.byref(h), uid, 1, 0) == 0, lib.mmad_last_error_string()
+    comm = _t.SimpleNamespace(handle=h)
+    try:
+        buf = torch.arange(1000, dtype=torch.float32, device="cuda")
+        ref = buf.clone()
+        assert lib.mmad_allreduce_bucket(h, ctypes.c_void_p(buf.data_ptr()), 1000, None) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(buf, ref)
+        ma, mb = _model(), _model()
+        ma._native.set_comm(comm)
+        for s in range(3):
+            x = torch.from_numpy(synth_windows(200, 192, seed=70 + s)).cuda()
+            la = float(ma._native.train_step_fused(x))
+            lb = float(mb._native.train_step_fused(x))
+            assert abs(la - lb) <= 1e-6 * abs(lb)
+        torch.cuda.synchronize()
+        d = (ma._native.params - mb._native.params).abs().max().item()
+        assert d <= 1e-6, d
+        assert torch.equal(ma._native.running, mb._native.running)
+        ma._native.set_comm(None)
+    finally:
+        lib.mmad_comm_destroy(h)
