@@ -62,6 +62,7 @@ SIGNATURES = {
     "mmad_comm_unique_id_bytes": (_I, []),
     "mmad_comm_get_unique_id": (_I, [_P]),
     "mmad_comm_create": (_I, [ctypes.POINTER(_P), _P, _I, _I]),
+    "mmad_comm_create_loopback": (_I, [ctypes.POINTER(_P), _F]),
     "mmad_comm_destroy": (None, [_P]),
     "mmad_allreduce_bucket": (_I, [_P, _P, _I64, _P]),
     "mmad_ae_set_comm": (_I, [_P, _P]),

@@ -48,7 +48,20 @@ const RcclApi& rccl() {
 struct mmad_comm {
   ncclComm_t comm = nullptr;
   int rank = 0, nranks = 1;
+  float loopback = 0.f;   // > 0: single-GPU loopback, all-reduce = scale by this
 };
+
+namespace {
+// loopback "all-reduce": buf *= s, after a short spin so that a missing
+// dependency on the producer of buf shows up as a wrong result
+__global__ void loopback_k(float* __restrict__ buf, int64_t n, float s) {
+  const long long t0 = clock64();
+  while (clock64() - t0 < 20000) {
+  }
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    buf[i] *= s;
+}
+}  // namespace
 
 #define MMAD_RCCL_CHECK(expr)                                                        \
   do {                                                                               \
@@ -90,6 +103,14 @@ int mmad_comm_create(mmad_comm** out, const void* unique_id, int nranks, int ran
   return MMAD_OK;
 }
 
+int mmad_comm_create_loopback(mmad_comm** out, float scale) {
+  MMAD_CHECK_ARG(out && scale > 0.f, "comm_create_loopback: bad arguments");
+  mmad_comm* c = new mmad_comm;
+  c->loopback = scale;
+  *out = c;
+  return MMAD_OK;
+}
+
 void mmad_comm_destroy(mmad_comm* c) {
   if (!c) return;
   if (c->comm && rccl().ok) (void)rccl().comm_destroy(c->comm);
@@ -99,6 +120,12 @@ void mmad_comm_destroy(mmad_comm* c) {
 int mmad_allreduce_bucket(mmad_comm* c, float* buf, int64_t n, void* stream) {
   MMAD_CHECK_ARG(c && (buf || n == 0) && n >= 0, "allreduce_bucket: bad arguments");
   if (n == 0) return MMAD_OK;
+  if (c->loopback > 0.f) {
+    const int64_t blocks = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+    loopback_k<<<(int)blocks, 256, 0, (hipStream_t)stream>>>(buf, n, c->loopback);
+    MMAD_LAUNCH_CHECK();
+    return MMAD_OK;
+  }
   MMAD_RCCL_CHECK(rccl().all_reduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm,
                                     (hipStream_t)stream));
   return MMAD_OK;

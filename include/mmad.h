@@ -235,6 +235,10 @@ int mmad_comm_unique_id_bytes(void);
 int mmad_comm_get_unique_id(void* out);
 /* every rank, with the current HIP device set to its GPU */
 int mmad_comm_create(mmad_comm** out, const void* unique_id, int nranks, int rank);
+/* single-GPU loopback communicator for testing the exchange schedule: its
+ * "all-reduce" scales the bucket by `scale` (= the sum over `scale` identical
+ * shards) after a short delay */
+int mmad_comm_create_loopback(mmad_comm** out, float scale);
 void mmad_comm_destroy(mmad_comm* c);
 /* in-place fp32 sum all-reduce of buf[n] on stream */
 int mmad_allreduce_bucket(mmad_comm* c, float* buf, int64_t n, void* stream);

@@ -115,3 +115,45 @@ def test_native_comm_single_rank_step_matches_fused():
         ma._native.set_comm(None)
     finally:
         lib.mmad_comm_destroy(h)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_native_exchange_schedule_loopback(dtype):
+    """Exchange schedule of the native DP step on one GPU: a loopback
+    communicator whose all-reduce doubles each bucket (= 2 identical shards)
+    after a delay.  Must equal: plain fwd+bwd, grads *= 2, loss *= 2, flat Adam
+    -- i.e. every bucket is reduced after its producer finished and before its
+    Adam, and the small bucket + loss are reduced too."""
+    import ctypes
+    import types as _t
+    from icra2021_multimodal_ad_amd import _native
+    from icra2021_multimodal_ad_amd.data import synth_windows
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    from icra2021_multimodal_ad_amd.common_utils import init_state_dict
+    lib = _native.load()
+    h = ctypes.c_void_p()
+    assert lib.mmad_comm_create_loopback(ctypes.byref(h), 2.0) == 0
+    comm = _t.SimpleNamespace(handle=h)
+
+    def mk():
+        cfg = _t.SimpleNamespace(input_size=700, btl_size=40, n_layers=5, gpu_id=0, dtype=dtype)
+        m = get_model(cfg)
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in
+                           init_state_dict(700, 40, 5, seed=81).items()})
+        return m
+    try:
+        ma, mb = mk(), mk()
+        ma._native.set_comm(comm)
+        for s in range(3):
+            x = torch.from_numpy(synth_windows(384, 700, seed=90 + s)).cuda()
+            la = float(ma._native.train_step_fused(x))
+            lb = mb._native.train_step(x)
+            mb._native.grads.mul_(2.0)
+            mb._native.adam()
+            assert abs(la - 2.0 * float(lb)) <= 1e-5 * abs(la)
+        torch.cuda.synchronize()
+        d = (ma._native.params - mb._native.params).abs().max().item()
+        assert d <= 1e-6, d
+        ma._native.set_comm(None)
+    finally:
+        lib.mmad_comm_destroy(h)
