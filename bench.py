@@ -109,6 +109,8 @@ def main():
     ap.add_argument("--dim", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=1024, help="windows per GPU per step")
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--model", default="ae", choices=["ae", "vib_ae"],
+                    help="vib_ae: BASELINE config C3/C4 (VIB head, k=1, beta_kl=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -123,7 +125,7 @@ def main():
     rank, world, local = mdist.init_from_env()
     torch.cuda.set_device(local)
     cfg = types.SimpleNamespace(input_size=args.dim, btl_size=100, n_layers=5, gpu_id=local,
-                                dtype=args.dtype)
+                                dtype=args.dtype, models=args.model, vib_k=1, beta_kl=1.0)
     torch.manual_seed(0)
     model = get_model(cfg)
     mdist.attach_data_parallel(model)
@@ -170,7 +172,9 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (seeded 4-modal window generator, random-init weights)",
-        "config": {"workload": f"FC-AE train step (fwd+sum-MSE+bwd+Adam), D={args.dim}, btl=100, "
+        "config": {"workload": f"{'VIB-AE' if args.model == 'vib_ae' else 'FC-AE'} train step "
+                               f"(fwd+sum-MSE{'+KL' if args.model == 'vib_ae' else ''}+bwd+Adam), "
+                               f"D={args.dim}, btl=100, "
                                f"n_layers=5, {args.batch} windows/GPU",
                    "global_batch": args.batch * world, "input_dim": args.dim,
                    "parallelism": f"dp{world}",

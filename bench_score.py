@@ -1,0 +1,185 @@
+"""Scoring benchmark (BASELINE config C5: reconstruction_aggregation scoring over
+1M synthetic windows, 1 GPU).  Prints ONE JSON line.
+
+Workload: the RaPP scoring path of the reference (reconstruction_aggregation.py
+:6-37 get_diffs + utils/metric.py:133 BASE and :145-181 SAP), streamed over N
+windows already resident in HBM: one native call per batch (mmad_ae_score:
+eval AE forward, then the encoder over x_hat reusing the encoder activations of
+x; per-layer squared-diff row sums in the GEMM epilogues -- the diffs are never
+materialised).  BASE and SAP per window are reduced on the device.
+--nap adds the NAP score (utils/metric.py:183-238): fit on a train set of diffs,
+then per batch the diffs are materialised and scored by one GEMM
+(mmad_nap_score).
+
+roofline: the dominant score GEMM (decoder last layer with the score
+epilogue, algorithmic flops 2*B*K*N) timed with per-launch HIP event pairs.
+cpu_baseline: the oracle's numpy get_diffs + BASE/SAP on a bounded sample on
+the host (kind "port")."""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+BF16_PEAK_TFLOPS = 2500.0
+F32_PEAK_TFLOPS = 157.3
+
+
+def score_flops_per_window(enc, dec):
+    ae = sum(a * b for a, b in zip(enc[:-1], enc[1:])) + sum(a * b for a, b in zip(dec[:-1], dec[1:]))
+    en = sum(a * b for a, b in zip(enc[:-1], enc[1:]))
+    return 2.0 * (ae + en)
+
+
+def cpu_baseline(d, budget_s=10.0):
+    import numpy as np
+    from threadpoolctl import threadpool_limits
+    from oracle import ae_oracle as O
+    from oracle.model_io import model_from_state_dict
+    from icra2021_multimodal_ad_amd.common_utils import init_state_dict
+    from icra2021_multimodal_ad_amd.data import synth_windows
+    threads = min(16, os.cpu_count() or 1)
+    m = model_from_state_dict(init_state_dict(d, 100, 5, seed=0))
+    x = synth_windows(4096, d, seed=3)
+    n, t0 = 0, time.perf_counter()
+    with threadpool_limits(threads):
+        while time.perf_counter() - t0 < budget_s and n < 64 * 1024:
+            diffs = O.get_diffs(x, m, batch_size=698)
+            O.base_score(diffs)
+            O.sap_score(diffs)
+            n += x.shape[0]
+    el = time.perf_counter() - t0
+    return {"value": n / el, "unit": "windows/sec", "cores": threads, "kind": "port",
+            "sample": f"{n} windows of oracle get_diffs+BASE+SAP (numpy fp32, batch 698) at D={d}, "
+                      f"{el:.1f} s, BLAS threads={threads}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--windows", type=int, default=1 << 20)
+    ap.add_argument("--batch", type=int, default=16384)
+    ap.add_argument("--dim", type=int, default=2048)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--nap", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import types
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    from icra2021_multimodal_ad_amd.data import synth_windows_device
+    from icra2021_multimodal_ad_amd import reconstruction_aggregation as ra
+    from icra2021_multimodal_ad_amd import _native
+    from icra2021_multimodal_ad_amd._native import call, ptr, stream_ptr
+
+    dev = torch.device("cuda", 0)
+    cfg = types.SimpleNamespace(input_size=args.dim, btl_size=100, n_layers=5, gpu_id=0, dtype=args.dtype)
+    torch.manual_seed(0)
+    model = get_model(cfg)
+    # a few train steps so BN running statistics are real
+    for i in range(20):
+        model.train_step_async(synth_windows_device(1024, args.dim, dev, seed=500 + i))
+    model.eval()
+    nat = model._native
+    nat.sync_shadow(force=True)
+    widths = nat.diff_widths()
+
+    # all windows resident in HBM before timing
+    N = args.windows
+    x = torch.empty((N, args.dim), device=dev)
+    for s in range(0, N, 65536):
+        n = min(65536, N - s)
+        x[s:s + n] = synth_windows_device(n, args.dim, dev, seed=7 + s)
+    layer_sq = torch.empty((nat.n_enc + 1, N), device=dev)
+    ra.score_windows(x[: args.batch], model, args.batch, out=layer_sq[:, : args.batch])  # warm/tune
+    torch.cuda.synchronize()
+    best = None
+    for _ in range(args.reps):
+        t0 = time.perf_counter()
+        ra.score_windows(x, model, args.batch, out=layer_sq)
+        base = ra.base_from_layer_sq(layer_sq, widths)
+        sap = ra.sap_from_layer_sq(layer_sq, widths)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        best = el if best is None else min(best, el)
+    value = N / best
+    fpw = score_flops_per_window(nat.enc_widths, nat.dec_widths)
+
+    res = {
+        "metric": "sensor-windows/sec (RaPP scoring: BASE+SAP)",
+        "value": round(value, 1),
+        "unit": "sensor-windows/sec",
+        "n_gpus": 1,
+        "windows": N,
+        "higher_is_better": True,
+        "dtype": args.dtype,
+        "data": "synthetic (seeded 4-modal windows resident in HBM, AE after 20 train steps)",
+        "config": {"workload": f"RaPP scoring (get_diffs + BASE + SAP) D={args.dim}, btl=100, "
+                               f"n_layers=5, batch {args.batch}", "windows": N},
+        "ms_total": round(best * 1e3, 3),
+        "model_tflops": round(value * fpw / 1e12, 2),
+        "score_checksum": {"base_mean": float(base.mean()), "sap_mean": float(sap.mean())},
+    }
+
+    # roofline: the largest score GEMM (last decoder layer, score epilogue vs x)
+    L = nat.layers[-1]
+    B = args.batch
+    Mp = _native.pad(B)
+    tdt = torch.bfloat16 if nat.dt == _native.BF16 else torch.float32
+    xin = torch.randn((Mp, L["Kp"]), device=dev).to(tdt)
+    ref = torch.randn((Mp, L["Np"]), device=dev).to(tdt)
+    out = torch.empty((Mp, L["Np"]), device=dev, dtype=tdt)
+    rowsq = torch.empty((L["Np"] // 128, Mp), device=dev)
+    w = nat.shadow[L["w_off"]:] if nat.shadow is not None else nat.params[L["w_off"]:]
+    bb = nat.params[L["b_off"]:]
+    s = stream_ptr()
+
+    def launch():
+        call("mmad_fc_fwd_score", nat.dt, B, L["N"], L["K"], Mp, L["Np"], L["Kp"], ptr(xin), ptr(w),
+             ptr(bb), 0, 0.2, None, None, ptr(out), ptr(ref), ptr(rowsq), None, 0, s)
+    for _ in range(5):
+        launch()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(30)]
+    for e0, e1 in ev:
+        e0.record()
+        launch()
+        e1.record()
+    torch.cuda.synchronize()
+    avg = sum(e0.elapsed_time(e1) for e0, e1 in ev) / 1e3 / len(ev)
+    fl = 2.0 * B * L["K"] * L["N"]
+    peak = BF16_PEAK_TFLOPS if nat.dt == _native.BF16 else F32_PEAK_TFLOPS
+    res["roofline"] = {"kernel": f"mmad_gemm_kernel score (decoder last layer {B}x{L['K']} . "
+                                 f"{L['N']}x{L['K']}^T + sum (y-x)^2 epilogue)",
+                       "bound": "mfma", "achieved": round(fl / avg / 1e12, 2), "peak": peak,
+                       "unit": "TFLOP/s", "frac": round(fl / avg / 1e12 / peak, 4), "traffic": None,
+                       "avg_us": round(avg * 1e6, 2), "flops_per_launch": fl}
+
+    if args.nap:
+        ntr = 20000
+        xtr = synth_windows_device(ntr, args.dim, dev, seed=99)
+        tr = []
+        for s0 in range(0, ntr, 4096):
+            _, d = nat.score(xtr[s0:s0 + 4096], want_diffs=True)
+            tr.append(d)
+        tr = torch.cat(tr)
+        nap = ra.NapScorer(model).fit(train_diffs=tr)
+        nn_ = min(N, 1 << 18)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s0 in range(0, nn_, args.batch):
+            _, d = nat.score(x[s0:s0 + args.batch], want_diffs=True)
+            nap.score(d)
+        torch.cuda.synchronize()
+        res["nap"] = {"windows": nn_, "windows_per_s": round(nn_ / (time.perf_counter() - t0), 1),
+                      "fit_train_windows": ntr, "rank": int(nap.fit_state["v"].shape[1])}
+
+    if not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(args.dim)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

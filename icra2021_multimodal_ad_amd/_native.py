@@ -33,6 +33,7 @@ SIGNATURES = {
     "mmad_bn_eval_affine": (_I, [_I, _I, _P, _P, _P, _P, _F, _P, _P, _P]),
     "mmad_bn_train_apply": (_I, [_I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P,
                                  _P]),
+    "mmad_nap_score": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "mmad_fc_bwd_data": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "mmad_fc_bwd_weight": (_I, [_I, _I, _I, _I, _P, _P, _P, _P]),
     "mmad_bn_act_bwd_ws": (ctypes.c_size_t, [_I, _I]),

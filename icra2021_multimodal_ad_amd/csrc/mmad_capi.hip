@@ -131,6 +131,19 @@ int mmad_fc_fwd_score(int dtype, int M, int N, int K, int Mp, int Np, int Kp, co
                             (hipStream_t)stream);
 }
 
+int mmad_nap_score(int dtype, int M, int K, int R, int Mp, int Kp, int Rp, const void* x,
+                   const void* vt, const float* bias, const float* w, float* rowsq, float* score,
+                   void* stream) {
+  RET_IF(check_dtype(dtype));
+  RET_IF(check_dims("nap_score", M, R, K, Mp, Rp, Kp));
+  MMAD_CHECK_ARG(x && vt && bias && w && rowsq && score, "nap_score: null operand");
+  GemmEpi ep{};
+  ep.M = M; ep.N = R; ep.out = nullptr; ep.ldo = Rp; ep.bias = bias; ep.act = MMAD_ACT_NONE;
+  ep.ref = nullptr; ep.ldref = Rp; ep.rowsq = rowsq; ep.ldrow = Mp; ep.colw = w;
+  RET_IF(mmad_gemm_dispatch(dtype, GEMM_EPI_SCORE, x, Kp, vt, Kp, Mp, Rp, Kp, ep, (hipStream_t)stream));
+  return mmad_colsum(Rp / 128, M, Mp, rowsq, Mp, 1.f / (float)R, score, stream);
+}
+
 int mmad_fc_bwd_data(int dtype, int M, int N, int K, int Mp, int Np, int Kp, const void* dz,
                      const void* w, void* dx, float* colsum, void* stream) {
   RET_IF(check_dtype(dtype));

@@ -27,7 +27,8 @@ struct GemmEpi {
   float gscale;          // MSE gradient scale (2 for sum-MSE, 2/k for VIB)
   const void* ref;       // SCORE reference activations (same dtype as out)
   int ldref;
-  float* rowsq;          // SCORE row partials [Np/BN][ldrow]
+  float* rowsq;          // SCORE row partials [Np/128][ldrow]: sum_j colw[j]*(y-ref)^2
+  const float* colw;     // SCORE per-column weights (nullable = 1); ref nullable = 0
   int ldrow;
   float* diff;           // SCORE optional fp32 diff output
   int lddiff;

@@ -531,14 +531,16 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
       }
     }
   } else {
-    // SCORE: every reference chunk loaded before the loop's stores
+    // SCORE: every reference chunk loaded before the loop's stores.  ref
+    // null = 0 (NAP run: sum of squared outputs); colw: per-column weights
     uint4v rvs[EPI == GEMM_EPI_SCORE ? ITERS : 1];
     if constexpr (EPI == GEMM_EPI_SCORE) {
 #pragma unroll
       for (int it = 0; it < ITERS; ++it) {
         const int idx = it * NT + tid;
         const int rl = idx / CPR, ch = idx % CPR;
-        rvs[it] = *(const uint4v*)((const TO*)ep.ref + (size_t)(m0 + rl) * ep.ldref + n0 + ch * OEPC);
+        rvs[it] = ep.ref ? *(const uint4v*)((const TO*)ep.ref + (size_t)(m0 + rl) * ep.ldref + n0 + ch * OEPC)
+                         : uint4v{0u, 0u, 0u, 0u};
       }
     }
 #pragma unroll
@@ -548,17 +550,23 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
       const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
       const int row = m0 + rl;
       const int col = n0 + ch * OEPC;
-      *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
+      if (EPI != GEMM_EPI_SCORE || out) *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
       if constexpr (EPI == GEMM_EPI_SCORE) {
         const uint4v rv = rvs[it];
         const TO* pv = (const TO*)&v;
         const TO* pr = (const TO*)&rv;
         float sq = 0.f;
         float dd[OEPC];
+        float wv[OEPC];
+#pragma unroll
+        for (int e = 0; e < OEPC; e += 4) {
+          const floatx4 w4 = ep.colw ? *(const floatx4*)(ep.colw + col + e) : floatx4{1.f, 1.f, 1.f, 1.f};
+          wv[e] = w4[0]; wv[e + 1] = w4[1]; wv[e + 2] = w4[2]; wv[e + 3] = w4[3];
+        }
 #pragma unroll
         for (int e = 0; e < OEPC; ++e) {
           dd[e] = to_f32<TO>(pv[e]) - to_f32<TO>(pr[e]);
-          sq += dd[e] * dd[e];
+          sq = fmaf(dd[e] * dd[e], wv[e], sq);
         }
         if (ep.diff && row < ep.M) {
           float* dp = ep.diff + (size_t)row * ep.lddiff + col;

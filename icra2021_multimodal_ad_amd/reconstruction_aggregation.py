@@ -68,3 +68,93 @@ def sap_from_layer_sq(layer_sq, widths, start_layer_index=0, end_layer_index=Non
         end_layer_index = start_layer_index + 1
     sel = slice(start_layer_index, end_layer_index)
     return layer_sq[sel].sum(0) / float(sum(widths[sel]))
+
+
+class NapScorer:
+    """NAP score (utils/metric.py:183-238 get_d_norm_loss with Rotater
+    utils/normalize.py:47-103 and Standardizer :20-45).
+
+    fit: the rotation (mu_r, V) from the SVD of the centred train diffs and the
+    standardiser (mu_s, ddof=1 variance of the rotated train diffs) -- a
+    one-time host-side fit done with torch.linalg in float64 on the device, as
+    the reference's own Rotater.fit calls torch's SVD.
+    run: ONE native GEMM per batch (mmad_nap_score): the concatenated diffs
+    times V^T with the centring/standardising folded into a bias and a
+    per-column weight, squared-mean reduced in the epilogue -- the rotated
+    diffs are never materialised.
+    """
+
+    def __init__(self, model, start_layer_index=0, end_layer_index=None):
+        self.model = model
+        nat = model._native
+        widths = nat.diff_widths()
+        n = len(widths)
+        if end_layer_index is None:
+            end_layer_index = n + 1
+        if start_layer_index > n - 1:                  # utils/metric.py:197-202 clamping
+            start_layer_index = n - 1
+        if end_layer_index - start_layer_index < 1:
+            end_layer_index = start_layer_index + 1
+        self.sel = slice(start_layer_index, end_layer_index)
+        cuts = np.cumsum([0] + widths)
+        self.c0, self.c1 = int(cuts[self.sel.start]), int(cuts[min(self.sel.stop, n)])
+        self.fit_state = None
+
+    def _cat(self, diffs):
+        if isinstance(diffs, (list, tuple)):
+            diffs = np.concatenate(diffs[self.sel], axis=1)
+        return torch.as_tensor(diffs)
+
+    def fit(self, train_diffs=None, fit_state=None):
+        """train_diffs: list of per-layer arrays (get_diffs) or [N, W]; or a
+        ready fit_state {'mu_r','v','mu_s','var'} (e.g. the reference's)."""
+        dev = self.model._native.device
+        if fit_state is None:
+            x = self._cat(train_diffs).to(dev, torch.float64)
+            mu_r = x.mean(0)
+            xc = x - mu_r
+            _, _, vh = torch.linalg.svd(xc, full_matrices=False)
+            v = vh.T
+            rot = (xc.float() @ v.float()).double()     # Rotater.run is fp32 matmul
+            mu_s = rot.mean(0)
+            var = ((rot - mu_s) ** 2).sum(0) / max(rot.shape[0] - 1, 1)
+            fit_state = {"mu_r": mu_r.float(), "v": v.float(), "mu_s": mu_s.float(), "var": var.float()}
+        fit_state = {k: torch.as_tensor(np.asarray(v) if not torch.is_tensor(v) else v).to(dev)
+                     for k, v in fit_state.items()}
+        self.fit_state = fit_state
+        nat = self.model._native
+        from ._native import pad
+        W, R = fit_state["v"].shape
+        Kp, Rp = pad(W), pad(R)
+        tdt = torch.bfloat16 if nat.dt == 1 else torch.float32
+        vt = torch.zeros((Rp, Kp), device=dev, dtype=tdt)
+        vt[:R, :W] = fit_state["v"].T.to(tdt)
+        # (x - mu_r) V - mu_s = x V + bias, bias = -(mu_r V + mu_s)  (float64 fold)
+        bias = torch.zeros(Rp, device=dev)
+        bias[:R] = (-(fit_state["mu_r"].double() @ fit_state["v"].double())
+                    - fit_state["mu_s"].double()).float()
+        w = torch.zeros(Rp, device=dev)
+        w[:R] = (1.0 / fit_state["var"].double()).float()
+        self._dev = (W, R, Kp, Rp, vt, bias, w)
+        return self
+
+    def score(self, diffs):
+        """diffs: list of per-layer arrays or [N, W] (host or device) -> [N]
+        NAP scores (device fp32)."""
+        from ._native import call, ptr, stream_ptr, pad
+        nat = self.model._native
+        W, R, Kp, Rp, vt, bias, w = self._dev
+        x = self._cat(diffs).to(nat.device, torch.float32).contiguous()
+        N = x.shape[0]
+        assert x.shape[1] == W, (x.shape, W)
+        Mp = pad(N)
+        tdt = torch.bfloat16 if nat.dt == 1 else torch.float32
+        xp = torch.empty((Mp, Kp), device=nat.device, dtype=tdt)
+        dt = nat.dt
+        s = stream_ptr()
+        call("mmad_pack_input", dt, N, W, Mp, Kp, ptr(x), x.stride(0), ptr(xp), s)
+        rowsq = torch.empty((Rp // 128, Mp), device=nat.device)
+        out = torch.empty(N, device=nat.device)
+        call("mmad_nap_score", dt, N, W, R, Mp, Kp, Rp, ptr(xp), ptr(vt), ptr(bias), ptr(w),
+             ptr(rowsq), ptr(out), s)
+        return out

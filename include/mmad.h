@@ -97,6 +97,16 @@ int mmad_bn_train_apply(int dtype, int M, int N, int Mp, int Np, const void* a,
                         float* running_mean, float* running_var, float momentum, float eps,
                         float* save_mean, float* save_rstd, void* y, void* stream);
 
+/* NAP run (utils/metric.py:183-238; Rotater.run utils/normalize.py:72-103 and
+ * Standardizer.run :36-45 folded into one GEMM + epilogue):
+ *   score[m] = (1/R) sum_{j<R} w[j] * (sum_k x[m][k] vt[j][k] + bias[j])^2
+ * with vt = V^T of the rotation, bias = -(mu_r V + mu_s), w = 1/var (0 on
+ * padding).  x: packed concatenated diffs [Mp][Kp] (dtype), vt [Rp][Kp]
+ * (dtype); rowsq: fp32 workspace [Rp/128][Mp]; score fp32 [M]. */
+int mmad_nap_score(int dtype, int M, int K, int R, int Mp, int Kp, int Rp, const void* x,
+                   const void* vt, const float* bias, const float* w, float* rowsq, float* score,
+                   void* stream);
+
 /* Backward of Linear (autograd of layers/fc_layer.py:38):
  * dx[Mp][Kp] = dz[Mp][Np] . w[Np][Kp]; colsum (nullable, [Mp/32][2][Kp]
  * slot 0) = per-chunk column sums of dx (bias grad of a no-BN producer). */

@@ -342,3 +342,25 @@ def test_tile_configs_bit_identical(dtype):
             assert abs(out[2] - ref[2]) <= 1e-5 * abs(ref[2]), cfg   # loss partials are per tile
     finally:
         lib.mmad_tune_set(0, -1)
+
+
+def test_nap_run_native_matches_reference_fit(golden):
+    """NAP run through mmad_nap_score (GEMM + standardise/square-mean epilogue)
+    with the reference's own fit state: scores within 1e-4 (fp32 path), and the
+    on-device fit reproduces the reference's scores on the well-conditioned
+    case."""
+    from icra2021_multimodal_ad_amd.reconstruction_aggregation import NapScorer
+    g = golden("nap")
+    W = g["train"].shape[1]
+    m, _ = _model(W, 8, 2, init_state_dict(W, 8, 2, seed=5), dtype="f32")
+    nap = NapScorer(m)
+    nap.sel = slice(0, 1)
+    fit = {k: g[k] for k in ("mu_r", "v", "mu_s", "var")}
+    nap.fit(fit_state=fit)
+    got = nap.score(torch.from_numpy(g["test"])).cpu().numpy()
+    assert _rel(got, g["score"]) < 1e-4
+    nap2 = NapScorer(m)
+    nap2.sel = slice(0, 1)
+    nap2.fit(train_diffs=torch.from_numpy(g["train"]))
+    got2 = nap2.score(torch.from_numpy(g["test"])).cpu().numpy()
+    assert _rel(got2, g["score"]) < 1e-3
