@@ -97,8 +97,27 @@ def gemm_roofline(model, batch, iters=50):
     return {"kernel": f"mmad_gemm_kernel fwd (encoder layer 1: {batch}x{L['K']} . {L['N']}x{L['K']}^T,"
                       f" bias+LeakyReLU+BN-stat epilogue)",
             "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(ach / peak, 4), "traffic": None, "avg_us": round(avg_s * 1e6, 2),
-            "flops_per_launch": flops}
+            "frac": round(ach / peak, 4), "traffic": _pmc_traffic(L["K"], batch, dt),
+            "avg_us": round(avg_s * 1e6, 2), "flops_per_launch": flops}
+
+
+def _pmc_traffic(dim, batch, dt):
+    """HBM-side bytes per launch of the roofline kernel from the committed
+    rocprofv3 PMC passes (profiles/r01h_pmc_traffic.json: FETCH_SIZE x2 +
+    WRITE_SIZE, gfx950 correction) when they were taken at this workload."""
+    import glob
+    from icra2021_multimodal_ad_amd import _native
+    for f in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                           "*_pmc_traffic.json")))[::-1]:
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        w = d.get("workload", {})
+        if (w.get("dim"), w.get("batch"), w.get("dtype")) == (dim, batch,
+                                                             "bf16" if dt == _native.BF16 else "f32"):
+            return d["traffic_bytes_per_launch"]
+    return None
 
 
 def main():
