@@ -75,6 +75,7 @@ def gemm_roofline(model, batch, iters=50):
     w = nat.shadow[L["w_off"]:] if nat.shadow is not None else nat.params[L["w_off"]:]
     b = nat.params[L["b_off"]:]
     s = stream_ptr()
+    _native.enable_gemm_workspace(dev)   # split-K workspace, as the executor's GEMMs have
 
     def launch():
         call("mmad_fc_fwd", dt, batch, L["N"], L["K"], Mp, L["Np"], L["Kp"], ptr(xin), ptr(w), ptr(b),

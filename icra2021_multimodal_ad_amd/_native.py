@@ -26,6 +26,8 @@ SIGNATURES = {
     "mmad_abi_version": (_I, []),
     "mmad_pad_granule": (_I, []),
     "mmad_tune_set": (_I, [_I, _I]),
+    "mmad_gemm_ws_bytes": (ctypes.c_size_t, []),
+    "mmad_gemm_set_workspace": (_I, [_P, ctypes.c_size_t]),
     "mmad_fc_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P, _P, _P, _P, _P]),
     "mmad_fc_fwd_mse": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _F, _P, _P, _P]),
     "mmad_fc_fwd_score": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P, _P, _P, _P,
@@ -134,6 +136,23 @@ def stream_ptr(stream=None):
     import torch
     s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)
+
+
+_gemm_ws = {}
+
+
+def enable_gemm_workspace(device=None):
+    """Give this thread's layer-operator GEMMs (mmad_fc_*) a split-K workspace
+    on ``device`` (zeroed; kept alive here).  Returns the tensor."""
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    ws = _gemm_ws.get(dev)
+    if ws is None:
+        n = int(load().mmad_gemm_ws_bytes())
+        ws = torch.zeros(n, dtype=torch.uint8, device=dev)
+        _gemm_ws[dev] = ws
+    call("mmad_gemm_set_workspace", ptr(ws), ws.numel())
+    return ws
 
 
 def pad(n, g=128):

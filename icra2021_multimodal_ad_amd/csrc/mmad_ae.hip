@@ -15,6 +15,7 @@
 //   (single-GPU fused step) by that layer's Adam update, overlapping the
 //   remaining backward chain on the main stream.
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -87,6 +88,11 @@ struct AeWS {
   void *xin, *zbuf, *dzin;
   float *eps, *klpart, *misc, *lossp;
   int64_t kl_parts;
+  // split-K workspace per stream (0 = caller's stream, 1 = side stream);
+  // the two control blocks are contiguous (one memset per call)
+  float* sk_slab[2];
+  unsigned* sk_ctl[2];
+  size_t sk_ctl_bytes;
   std::vector<LayerWS> l;
   int64_t bytes;
 };
@@ -120,6 +126,17 @@ static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
     w.klpart = (float*)take(w.kl_parts * 4);
   }
   w.misc = (float*)take(1024 * 4);
+  {
+    size_t slab = 0, ctl = 0;
+    mmad_gemm_splitk_bytes(0, 0, &slab, &ctl);
+    ctl = (ctl + 255) / 256 * 256;
+    w.sk_ctl_bytes = 2 * ctl;
+    char* c = take((int64_t)(2 * ctl));
+    w.sk_ctl[0] = (unsigned*)c;
+    w.sk_ctl[1] = c ? (unsigned*)(c + ctl) : nullptr;
+    w.sk_slab[0] = (float*)take((int64_t)slab);
+    w.sk_slab[1] = (float*)take((int64_t)slab);
+  }
   {
     const AeLayer& last = h->L[nL - 1];
     w.lossp = (float*)take((int64_t)(w.Mpd / 64) * (last.Np / 64) * 4);
@@ -287,14 +304,28 @@ static const void* input_of(const mmad_ae* h, const AeWS& w, int l, bool train,
   return ps.out;
 }
 
-static int prepare_ws(const mmad_ae* h, int B, int k, void* ws, int64_t ws_bytes, AeWS& w) {
+static int prepare_ws(const mmad_ae* h, int B, int k, void* ws, int64_t ws_bytes, AeWS& w,
+                      hipStream_t st) {
   MMAD_CHECK_ARG(B >= 1 && k >= 1, "bad batch B=%d k=%d", B, k);
   MMAD_CHECK_ARG(h->vib || k == 1, "k>1 needs the VIB head");
   carve(h, B, k, (char*)ws, w);
   MMAD_CHECK_ARG(ws && ws_bytes >= w.bytes, "workspace too small (%lld < %lld bytes)",
                  (long long)ws_bytes, (long long)w.bytes);
   MMAD_CHECK_ARG(((uintptr_t)ws) % 256 == 0, "workspace must be 256-byte aligned");
+  // split-K arrival counters / flags start every call at zero (each GEMM
+  // leaves them zero again, this heals a poisoned or reused workspace)
+  MMAD_HIP_CHECK(hipMemsetAsync(w.sk_ctl[0], 0, w.sk_ctl_bytes, st));
   return MMAD_OK;
+}
+
+// GEMM dispatch with the split-K workspace of the stream it runs on
+static int ae_gemm(const mmad_ae* h, const AeWS& w, int dt, int epi, const void* A, int lda,
+                   const void* B, int ldb, int Mp, int Np, int K, GemmEpi ep, hipStream_t s,
+                   int* cfg = nullptr) {
+  const int r = (h->side && s == h->side) ? 1 : 0;
+  ep.sk_slab = w.sk_slab[r];
+  ep.sk_ctl = w.sk_ctl[r];
+  return mmad_gemm_dispatch(dt, epi, A, lda, B, ldb, Mp, Np, K, ep, s, cfg);
 }
 
 static inline int rows_of(const AeWS& w, const AeLayer& a) { return a.enc ? w.B : w.B * w.k; }
@@ -350,12 +381,12 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
       ep.gscale = 2.0f / (float)k;
       ep.lossp = w.lossp;
       int cfg = 0;
-      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_MSE, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st, &cfg));
+      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_MSE, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st, &cfg));
       h->mse_tiles = mmad_gemm_ntiles(cfg, Mp, a.Np);
     } else if (a.bn && train) {
       GemmEpi ep = fwd_epi(h, w, a, s, M, s.out, folded);
       ep.part = s.stats;
-      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
+      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
       if (l + 1 < nL) {
         // statistics -> (scale, shift) -> folded into layer l+1's weights/bias
         const AeLayer& c = h->L[l + 1];
@@ -376,10 +407,10 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
       GemmEpi ep = fwd_epi(h, w, a, s, M, s.y, folded);
       ep.bn_scale = s.scale;
       ep.bn_shift = s.shift;
-      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
+      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
     } else {
       GemmEpi ep = fwd_epi(h, w, a, s, M, s.out, folded);
-      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
+      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
     }
     if (h->vib && l == h->n_enc - 1) {
       const AeLayer& d0 = h->L[h->n_enc];
@@ -440,7 +471,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       // fork: dz_l is complete on the main stream; dW_l overlaps the chain below
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
       MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
-      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side));
+      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side));
       if (dp) MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l], side));
     }
     if (l > 0) {
@@ -455,7 +486,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       ep.ldpart = a.Kp;
       if (h->vib && l == h->n_enc) {
         ep.out = w.dzin;
-        RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
+        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
                                   a.Np, ep, st));
         RET_IF(mmad_vib_reparam_bwd(dt, w.B, h->btl, w.k, ps.out, p.Np, w.eps, w.dzin, a.Kp,
                                     beta_kl, ps.dy, p.Np, ps.dbpart, st));
@@ -465,7 +496,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
         ep.bn_mean = ps.mean;
         ep.bn_rstd = ps.rstd;
         ep.bn_part = ps.bnpart;
-        RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
+        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
                                   a.Np, ep, st));
         if (adam) MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
         RET_IF(mmad_bn_act_bwd_apply(dt, p.act, h->slope, rows_of(w, p), p.N, Mpp, p.Np, ps.dy,
@@ -475,7 +506,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       } else {
         ep.out = ps.dy;
         ep.part = ps.stats;
-        RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
+        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
                                   a.Np, ep, st));
       }
     }
@@ -526,10 +557,10 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       // by then, instead of queueing behind the side stream's backlog
       const bool on_main = l < h->dw_main;
       if (on_main) {
-        RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st));
+        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st));
       } else {
         MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_data[l], 0));
-        RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side));
+        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side));
       }
     }
   }
@@ -587,7 +618,7 @@ int mmad_ae_train_fwd_bwd(mmad_ae* h, const float* x, int ld_x, int B, int k, co
   MMAD_CHECK_ARG(h && h->params && h->grads && h->running, "ae_train: unbound handle");
   MMAD_CHECK_ARG(x && ld_x >= h->L[0].K && loss_out, "ae_train: bad input");
   AeWS w;
-  RET_IF(prepare_ws(h, B, k, ws, ws_bytes, w));
+  RET_IF(prepare_ws(h, B, k, ws, ws_bytes, w, (hipStream_t)stream));
   hipStream_t st = (hipStream_t)stream;
   RET_IF(run_forward(h, w, x, ld_x, 0, eps, seed, offset, st));
   RET_IF(run_backward(h, w, true, beta_kl, nullptr, st));
@@ -609,7 +640,7 @@ int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const
   MMAD_CHECK_ARG(x && ld_x >= h->L[0].K && loss_out, "ae_train_step: bad input");
   MMAD_CHECK_ARG(step >= 1, "ae_train_step: step must be >= 1");
   AeWS w;
-  RET_IF(prepare_ws(h, B, k, ws, ws_bytes, w));
+  RET_IF(prepare_ws(h, B, k, ws, ws_bytes, w, (hipStream_t)stream));
   hipStream_t st = (hipStream_t)stream;
   const AdamHyper ah = adam_hyper(lr, beta1, beta2, adam_eps, step);
   RET_IF(run_forward(h, w, x, ld_x, 0, eps, seed, offset, st));
@@ -653,7 +684,7 @@ int mmad_ae_backward(mmad_ae* h, const float* dxhat, int ld, int B, void* ws, in
   MMAD_CHECK_ARG(h && h->params && h->grads, "ae_backward: unbound handle");
   MMAD_CHECK_ARG(!h->vib, "ae_backward: the VIB model trains through mmad_ae_train_fwd_bwd");
   AeWS w;
-  RET_IF(prepare_ws(h, B, 1, ws, ws_bytes, w));
+  RET_IF(prepare_ws(h, B, 1, ws, ws_bytes, w, (hipStream_t)stream));
   hipStream_t st = (hipStream_t)stream;
   const int nL = (int)h->L.size();
   const AeLayer& last = h->L[nL - 1];
@@ -680,7 +711,7 @@ int mmad_ae_forward(mmad_ae* h, const float* x, int ld_x, int B, int train_bn, f
   MMAD_CHECK_ARG(h && h->params && h->running, "ae_forward: unbound handle");
   MMAD_CHECK_ARG(x && ld_x >= h->L[0].K, "ae_forward: bad input");
   AeWS w;
-  RET_IF(prepare_ws(h, B, 1, ws, ws_bytes, w));
+  RET_IF(prepare_ws(h, B, 1, ws, ws_bytes, w, (hipStream_t)stream));
   hipStream_t st = (hipStream_t)stream;
   RET_IF(run_forward(h, w, x, ld_x, train_bn ? 2 : 1, nullptr, 0x5eed, 0, st));
   const AeLayer& last = h->L.back();
@@ -698,7 +729,7 @@ int mmad_ae_score(mmad_ae* h, const float* x, int ld_x, int B, float* layer_sq, 
   MMAD_CHECK_ARG(h && h->params && h->running, "ae_score: unbound handle");
   MMAD_CHECK_ARG(x && ld_x >= h->L[0].K && layer_sq, "ae_score: bad args");
   AeWS w;
-  RET_IF(prepare_ws(h, B, 1, ws, ws_bytes, w));
+  RET_IF(prepare_ws(h, B, 1, ws, ws_bytes, w, (hipStream_t)stream));
   hipStream_t st = (hipStream_t)stream;
   const int dt = h->dtype;
   const int nL = (int)h->L.size();
@@ -727,10 +758,10 @@ int mmad_ae_score(mmad_ae* h, const float* x, int ld_x, int B, float* layer_sq, 
       ep.ldrow = Mp;
       ep.diff = diffs;
       ep.lddiff = ld_diff;
-      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_SCORE, in, a.Kp, weights(h, a), a.Kp, Mp, a.Np, a.Kp,
+      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_SCORE, in, a.Kp, weights(h, a), a.Kp, Mp, a.Np, a.Kp,
                                 ep, st));
     } else {
-      RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_FWD, in, a.Kp, weights(h, a), a.Kp, Mp, a.Np, a.Kp,
+      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_FWD, in, a.Kp, weights(h, a), a.Kp, Mp, a.Np, a.Kp,
                                 ep, st));
     }
     if (h->vib && l == h->n_enc - 1) {
@@ -755,7 +786,7 @@ int mmad_ae_score(mmad_ae* h, const float* x, int ld_x, int B, float* layer_sq, 
     ep.ldrow = w.Mpe;
     ep.diff = diffs ? diffs + coff : nullptr;
     ep.lddiff = ld_diff;
-    RET_IF(mmad_gemm_dispatch(dt, GEMM_EPI_SCORE, cur, a.Kp, weights(h, a), a.Kp, w.Mpe, a.Np,
+    RET_IF(ae_gemm(h, w, dt, GEMM_EPI_SCORE, cur, a.Kp, weights(h, a), a.Kp, w.Mpe, a.Np,
                               a.Kp, ep, st));
     coff += a.N;
     cur = s.dy;

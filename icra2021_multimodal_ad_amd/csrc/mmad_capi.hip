@@ -47,6 +47,11 @@ int mmad_group_override() { return g_group; }
 int mmad_autotune_enabled() { return g_autotune; }
 static int g_dbg = 0;
 int mmad_dbg_override() { return g_dbg; }
+static int g_splitk = [] {
+  const char* e = getenv("MMAD_GEMM_SPLITK");
+  return e ? atoi(e) : 0;
+}();
+int mmad_splitk_override() { return g_splitk; }
 
 int mmad_tune_set(int knob, int value) {
   switch (knob) {
@@ -54,6 +59,7 @@ int mmad_tune_set(int knob, int value) {
     case 1: g_group = value; return MMAD_OK;
     case 2: g_autotune = value; return MMAD_OK;
     case 3: g_dbg = value; return MMAD_OK;
+    case 4: g_splitk = value; return MMAD_OK;
     default: mmad_set_error("tune_set: unknown knob %d", knob); return MMAD_EINVAL;
   }
 }
@@ -81,6 +87,33 @@ static int check_dtype(int dtype) {
 // ---------------------------------------------------------------------------
 // layer operators
 // ---------------------------------------------------------------------------
+// split-K workspace of the calling thread's layer-operator GEMMs (optional)
+static thread_local char* g_sk_ws = nullptr;
+
+size_t mmad_gemm_ws_bytes(void) {
+  size_t slab = 0, ctl = 0;
+  mmad_gemm_splitk_bytes(0, 0, &slab, &ctl);
+  return slab + ctl;
+}
+
+int mmad_gemm_set_workspace(void* ws, size_t bytes) {
+  MMAD_CHECK_ARG(!ws || bytes >= mmad_gemm_ws_bytes(), "gemm_set_workspace: %zu < %zu bytes",
+                 bytes, mmad_gemm_ws_bytes());
+  MMAD_CHECK_ARG(((uintptr_t)ws) % 256 == 0, "gemm_set_workspace: not 256-byte aligned");
+  g_sk_ws = (char*)ws;
+  return MMAD_OK;
+}
+
+static int layer_gemm(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,
+                      int Np, int K, GemmEpi ep, void* stream) {
+  if (g_sk_ws) {
+    size_t slab = 0, ctl = 0;
+    mmad_gemm_splitk_bytes(0, 0, &slab, &ctl);
+    ep.sk_slab = (float*)g_sk_ws;
+    ep.sk_ctl = (unsigned*)(g_sk_ws + slab);
+  }
+  return mmad_gemm_dispatch(dtype, epi, A, lda, B, ldb, Mp, Np, K, ep, (hipStream_t)stream);
+}
 int mmad_fc_fwd(int dtype, int M, int N, int K, int Mp, int Np, int Kp, const void* x,
                 const void* w, const float* bias, int act, float slope, const float* bn_scale,
                 const float* bn_shift, void* y, float* stats, void* stream) {
@@ -91,8 +124,7 @@ int mmad_fc_fwd(int dtype, int M, int N, int K, int Mp, int Np, int Kp, const vo
   GemmEpi ep{};
   ep.M = M; ep.N = N; ep.out = y; ep.ldo = Np; ep.bias = bias; ep.act = act; ep.slope = slope;
   ep.bn_scale = bn_scale; ep.bn_shift = bn_shift; ep.part = stats; ep.ldpart = Np;
-  return mmad_gemm_dispatch(dtype, GEMM_EPI_FWD, x, Kp, w, Kp, Mp, Np, Kp, ep,
-                            (hipStream_t)stream);
+  return layer_gemm(dtype, GEMM_EPI_FWD, x, Kp, w, Kp, Mp, Np, Kp, ep, stream);
 }
 
 static int fc_fwd_mse_impl(int dtype, int M, int N, int K, int Mp, int Np, int Kp, const void* x,
@@ -104,8 +136,7 @@ static int fc_fwd_mse_impl(int dtype, int M, int N, int K, int Mp, int Np, int K
   GemmEpi ep{};
   ep.M = M; ep.N = N; ep.out = dz; ep.ldo = Np; ep.bias = bias; ep.part = partials;
   ep.ldpart = Np; ep.target = target; ep.ldt = ld_target; ep.tmod = tmod; ep.gscale = grad_scale;
-  return mmad_gemm_dispatch(dtype, GEMM_EPI_MSE, x, Kp, w, Kp, Mp, Np, Kp, ep,
-                            (hipStream_t)stream);
+  return layer_gemm(dtype, GEMM_EPI_MSE, x, Kp, w, Kp, Mp, Np, Kp, ep, stream);
 }
 
 int mmad_fc_fwd_mse(int dtype, int M, int N, int K, int Mp, int Np, int Kp, const void* x,
@@ -127,8 +158,7 @@ int mmad_fc_fwd_score(int dtype, int M, int N, int K, int Mp, int Np, int Kp, co
   ep.M = M; ep.N = N; ep.out = y; ep.ldo = Np; ep.bias = bias; ep.act = act; ep.slope = slope;
   ep.bn_scale = bn_scale; ep.bn_shift = bn_shift; ep.ref = ref; ep.ldref = Np; ep.rowsq = rowsq;
   ep.ldrow = Mp; ep.diff = diff; ep.lddiff = ld_diff;
-  return mmad_gemm_dispatch(dtype, GEMM_EPI_SCORE, x, Kp, w, Kp, Mp, Np, Kp, ep,
-                            (hipStream_t)stream);
+  return layer_gemm(dtype, GEMM_EPI_SCORE, x, Kp, w, Kp, Mp, Np, Kp, ep, stream);
 }
 
 int mmad_nap_score(int dtype, int M, int K, int R, int Mp, int Kp, int Rp, const void* x,
@@ -140,7 +170,7 @@ int mmad_nap_score(int dtype, int M, int K, int R, int Mp, int Kp, int Rp, const
   GemmEpi ep{};
   ep.M = M; ep.N = R; ep.out = nullptr; ep.ldo = Rp; ep.bias = bias; ep.act = MMAD_ACT_NONE;
   ep.ref = nullptr; ep.ldref = Rp; ep.rowsq = rowsq; ep.ldrow = Mp; ep.colw = w;
-  RET_IF(mmad_gemm_dispatch(dtype, GEMM_EPI_SCORE, x, Kp, vt, Kp, Mp, Rp, Kp, ep, (hipStream_t)stream));
+  RET_IF(layer_gemm(dtype, GEMM_EPI_SCORE, x, Kp, vt, Kp, Mp, Rp, Kp, ep, stream));
   return mmad_colsum(Rp / 128, M, Mp, rowsq, Mp, 1.f / (float)R, score, stream);
 }
 
@@ -152,8 +182,7 @@ int mmad_fc_bwd_data(int dtype, int M, int N, int K, int Mp, int Np, int Kp, con
   GemmEpi ep{};
   ep.M = M; ep.N = K; ep.out = dx; ep.ldo = Kp; ep.part = colsum; ep.ldpart = Kp;
   // dx[Mp][Kp] = dz[Mp][Np] . W[Np][Kp]: contraction over Np, W read MN-major
-  return mmad_gemm_dispatch(dtype, GEMM_EPI_BWD_DATA, dz, Np, w, Kp, Mp, Kp, Np, ep,
-                            (hipStream_t)stream);
+  return layer_gemm(dtype, GEMM_EPI_BWD_DATA, dz, Np, w, Kp, Mp, Kp, Np, ep, stream);
 }
 
 int mmad_fc_bwd_weight(int dtype, int Mp, int Np, int Kp, const void* dz, const void* x,
@@ -164,6 +193,5 @@ int mmad_fc_bwd_weight(int dtype, int Mp, int Np, int Kp, const void* dz, const 
   GemmEpi ep{};
   ep.M = Np; ep.N = Kp; ep.out = dw; ep.ldo = Kp;
   // dW[Np][Kp] = dz^T . x, contraction over the batch; both read MN-major
-  return mmad_gemm_dispatch(dtype, GEMM_EPI_BWD_WEIGHT, dz, Np, x, Kp, Np, Kp, Mp, ep,
-                            (hipStream_t)stream);
+  return layer_gemm(dtype, GEMM_EPI_BWD_WEIGHT, dz, Np, x, Kp, Np, Kp, Mp, ep, stream);
 }

@@ -33,8 +33,8 @@ void mmad_set_error(const char* fmt, ...);
   do {                                                                         \
     hipError_t e_ = (expr);                                                    \
     if (e_ != hipSuccess) {                                                    \
-      mmad_set_error("HIP error %s at %s:%d", hipGetErrorString(e_), __FILE__, \
-                     __LINE__);                                                \
+      mmad_set_error("HIP error %d (%s) at %s:%d", (int)e_, hipGetErrorString(e_), \
+                     __FILE__, __LINE__);                                      \
       return MMAD_EHIP;                                                        \
     }                                                                          \
   } while (0)

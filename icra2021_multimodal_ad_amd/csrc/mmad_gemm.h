@@ -64,7 +64,14 @@ struct GemmEpi {
   float* sm_v;
   int sm_n;
   int sm_bN, sm_bNp;     // bias entries (valid / padded); their g = db from gb_src
-  // set by the launcher: XCD-aware grouped tile order
+  // split-K (nullable = off): fp32 partial-tile slabs and the per-tile
+  // arrival counter + flag words (zero before a launch; every launch leaves
+  // them zero).  Sizes: mmad_gemm_splitk_bytes.  The split factor itself is
+  // a deterministic function of the shape (mmad_gemm_splitk).
+  float* sk_slab;
+  unsigned* sk_ctl;
+  // set by the launcher: split factor, XCD-aware grouped tile order
+  int splitk;
   int tiles_n, group_m;
   int dbg;               // diagnostics (tools/gemm_sweep): 1 skip main loop, 2 skip epilogue
 };
@@ -74,6 +81,7 @@ int mmad_group_override();
 int mmad_tile_override();
 int mmad_autotune_enabled();
 int mmad_dbg_override();
+int mmad_splitk_override();   // 0 = shape rule; 1, 2, 4 = forced split factor
 
 // tile configuration a problem will run with (autotuned on first dispatch of
 // the shape; a static heuristic before that / when tuning is off)
@@ -82,6 +90,13 @@ int mmad_gemm_plan(int Mp, int Np, int K, int epi, int dtype);
 int mmad_gemm_ntiles(int cfg, int Mp, int Np);
 // upper bound of mmad_gemm_ntiles over all configurations
 int mmad_gemm_tiles(int Mp, int Np);
+
+// split-K factor the dispatcher uses for a shape when the caller provides
+// split-K workspace (1, 2 or 4; a function of the shape only, so every tile
+// configuration of a shape accumulates in the same order)
+int mmad_gemm_splitk(int Mp, int Np, int K, int dtype);
+// split-K workspace sufficient for every launch (shape-independent bound)
+void mmad_gemm_splitk_bytes(int Mp, int Np, size_t* slab_bytes, size_t* ctl_bytes);
 
 // cfg_used (nullable) receives the tile configuration launched
 int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,

@@ -41,8 +41,10 @@
 #include "mmad_gemm.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <map>
 #include <mutex>
+#include <type_traits>
 
 namespace {
 
@@ -166,6 +168,61 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// ---- pipelined main-loop helpers -------------------------------------------
+// One K stage (128 B of K per operand row) = two sub-steps: 32-deep bf16
+// MFMA steps, or 16-deep f32 steps (4 x 16x16x4 MFMAs each).
+template <typename T> struct SubFrag;
+template <> struct SubFrag<bf16> { using F = bf16x8; };
+template <> struct SubFrag<float> { using F = floatx4; };
+
+template <typename T, bool AK, bool BK_, bool NAT, int BM, int BN, int TM, int TN>
+__device__ __forceinline__ void read_sub(const char* sa, const char* sb, int ra, int rb, int sub,
+                                         int lane, typename SubFrag<T>::F (&fa)[TM],
+                                         typename SubFrag<T>::F (&fb)[TN]) {
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    if constexpr (sizeof(T) == 2) fa[i] = frag_bf16<AK, NAT, BM>(sa, ra + i * 16, sub, lane);
+    else fa[i] = frag_f32<AK, BM>(sa, ra + i * 16, sub, lane);
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    if constexpr (sizeof(T) == 2) fb[j] = frag_bf16<BK_, NAT, BN>(sb, rb + j * 16, sub, lane);
+    else fb[j] = frag_f32<BK_, BN>(sb, rb + j * 16, sub, lane);
+  }
+}
+
+// MFMAs of fragment rows i in [H*TM/2, (H+1)*TM/2): a sub-step is issued as
+// two such groups with the next fragment reads between them
+template <typename T, int TM, int TN, int H>
+__device__ __forceinline__ void mma_half(floatx4 (&acc)[TM][TN], const typename SubFrag<T>::F (&fa)[TM],
+                                         const typename SubFrag<T>::F (&fb)[TN]) {
+#pragma unroll
+  for (int i = H * TM / 2; i < (H + 1) * TM / 2; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if constexpr (sizeof(T) == 2) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+      }
+    }
+}
+
+// lgkmcnt(0) as a real s_waitcnt (vmcnt/expcnt at max) so the compiler's own
+// counter bookkeeping sees it
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+
+// no more issues: stage t+1 must land, rem = nt-t-2 later stages may stay in flight
+template <int NL>
+__device__ __forceinline__ void wait_tail(int rem) {
+  if (rem >= 3) wait_vmcnt<3 * NL>();
+  else if (rem == 2) wait_vmcnt<2 * NL>();
+  else if (rem == 1) wait_vmcnt<NL>();
+  else wait_vmcnt<0>();
+}
+
 __device__ __forceinline__ void block_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -201,7 +258,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   constexpr int OSTRIDE = BN * (int)sizeof(TO) + 16;
   constexpr int OBYTES = BM * OSTRIDE + (EPI == GEMM_EPI_BWD_DATA ? BM * BN / 2 : 0);
   constexpr int LDS_BYTES = (NS * SLOT > OBYTES) ? NS * SLOT : OBYTES;
-  static_assert((NS - 2) * NL <= 63, "vmcnt range");
+  static_assert((NS - 1) * NL <= 63, "vmcnt range");
   static_assert(LDS_BYTES <= 163840, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
@@ -209,22 +266,29 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   const int wm = w / WN, wn = w % WN;
   // XCD-aware order (1-D grid).  Under round-robin dispatch, blocks with equal
   // bid % 8 share an XCD (speed only, never correctness); each such set gets a
-  // contiguous range of logical tiles, grouped group_m M-tiles at a time so
-  // every XCD works on a compact rectangle whose A/B panels stay in its L2.
+  // contiguous range of logical blocks lt; the S split-K blocks of one output
+  // tile are consecutive in lt (one XCD), and tiles are grouped group_m M-tiles
+  // at a time so every XCD works on a compact rectangle whose A/B panels stay
+  // in its L2.
+  const int S = ep.splitk > 1 ? ep.splitk : 1;
   const int nblk = gridDim.x, bid = blockIdx.x;
-  int tm, tn, lt;
+  const int ntl = nblk / S;                 // output tiles
+  int tm, tn, tile, sk;
   {
     const int q = nblk >> 3, r = nblk & 7, xcd = bid & 7;
-    lt = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    const int tiles_m = nblk / ep.tiles_n;
+    const int lt = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    tile = lt / S;
+    sk = lt - tile * S;
+    const int tiles_m = ntl / ep.tiles_n;
     const int per_group = ep.group_m * ep.tiles_n;
-    const int first_m = (lt / per_group) * ep.group_m;
+    const int first_m = (tile / per_group) * ep.group_m;
     const int gsz = min(tiles_m - first_m, ep.group_m);
-    tm = first_m + (lt % per_group) % gsz;
-    tn = (lt % per_group) / gsz;
+    tm = first_m + (tile % per_group) % gsz;
+    tn = (tile % per_group) / gsz;
   }
   const int m0 = tm * BM, n0 = tn * BN;
-  const int nt = (ep.dbg & 1) ? 0 : K / IA::BK;
+  const int Ks = K / S, kbase = sk * Ks;
+  const int nt = (ep.dbg & 1) ? 0 : Ks / IA::BK;
 
   floatx4 acc[TM][TN];
 #pragma unroll
@@ -284,52 +348,153 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
 
   auto issue = [&](int s) {
     char* base = smem + (s % NS) * SLOT;
-    const int k0 = s * IA::BK;
+    const int k0 = kbase + s * IA::BK;
     issue_stage<T, AK, BM, NT>(base, A, lda, m0, k0, tid);
     issue_stage<T, BK_, BN, NT>(base + IA::BYTES, B, ldb, n0, k0, tid);
   };
 
+  // ---- main loop: NS-slot LDS ring, all slots in flight; fragment registers
+  // double-buffered one sub-step ahead.  Per stage t:
+  //   F1 <- (t, sub 1) issued between the two MFMA halves of F0 = (t, sub 0);
+  //   wait stage t+1 landed + own reads of slot t done; barrier; refill slot t
+  //   with stage t+NS; F0 <- (t+1, sub 0) between the two halves of F1.
+  // The loop bodies are straight-line (peeled: issue phase / tail / last) so
+  // hipcc's lgkmcnt bookkeeping stays exact, and sched_barriers pin the order.
+  using FR = typename SubFrag<T>::F;
+  const int ra = wm * 16 * TM, rb = wn * 16 * TN;
+  if (nt > 0) {
 #pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (s < nt) issue(s);
-
-  for (int t = 0; t < nt; ++t) {
-    if (t + NS - 2 < nt) wait_vmcnt<(NS - 2) * NL>();
+    for (int s = 0; s < NS; ++s)
+      if (s < nt) issue(s);
+    if (nt >= NS) wait_vmcnt<(NS - 1) * NL>();
     else wait_vmcnt<0>();
-    block_barrier();                       // stage t landed for every wave; slot t-1 free
-    if (t + NS - 1 < nt) issue(t + NS - 1);
-    const char* sa = smem + (t % NS) * SLOT;
-    const char* sb = sa + IA::BYTES;
-    if constexpr (sizeof(T) == 2) {
+    block_barrier();
+    FR f0a[TM], f0b[TN], f1a[TM], f1b[TN];
+    read_sub<T, AK, BK_, NAT, BM, BN, TM, TN>(smem, smem + IA::BYTES, ra, rb, 0, lane, f0a, f0b);
+    wait_lgkm0();
+    auto step = [&](int t, auto issue_c, auto last_c) {
+      constexpr bool ISSUE = decltype(issue_c)::value, LAST = decltype(last_c)::value;
+      const char* sa = smem + (t % NS) * SLOT;
+      mma_half<T, TM, TN, 0>(acc, f0a, f0b);
+      __builtin_amdgcn_sched_barrier(0);
+      read_sub<T, AK, BK_, NAT, BM, BN, TM, TN>(sa, sa + IA::BYTES, ra, rb, 1, lane, f1a, f1b);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_half<T, TM, TN, 1>(acc, f0a, f0b);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!LAST) {
+        if constexpr (ISSUE) wait_vmcnt<(NS - 2) * NL>();
+        else wait_tail<NL>(nt - t - 2);
+        wait_lgkm0();
+        block_barrier();                     // stage t+1 visible; slot t free
+        if constexpr (ISSUE) issue(t + NS);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      mma_half<T, TM, TN, 0>(acc, f1a, f1b);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!LAST) {
+        const char* sn = smem + ((t + 1) % NS) * SLOT;
+        read_sub<T, AK, BK_, NAT, BM, BN, TM, TN>(sn, sn + IA::BYTES, ra, rb, 0, lane, f0a, f0b);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mma_half<T, TM, TN, 1>(acc, f1a, f1b);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    int t = 0;
+    for (; t < nt - NS; ++t) step(t, T_{}, F_{});
+    for (; t < nt - 1; ++t) step(t, F_{}, F_{});
+    step(nt - 1, F_{}, T_{});
+  }
+
+  // ---- split-K combine (ticket first, no spin on a block that has not run):
+  // the first S-1 blocks of a tile to finish publish their partial tile as an
+  // sc1 (write-through) slab + flag; the last one adds the slabs in split
+  // order (p0 + p1 + ... : independent of arrival order) and runs the
+  // epilogue.  Counters / flags start at 0 (caller memset) and the last block
+  // resets them, so consecutive launches on one stream reuse them.
+  if (S > 1) {
+    unsigned* cnt = ep.sk_ctl + tile;
+    unsigned* flg = ep.sk_ctl + ntl + (size_t)tile * S;
+    __syncthreads();
+    unsigned* shw = (unsigned*)smem;
+    if (tid == 0) shw[0] = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned ticket = shw[0];
+    float* slab_t = ep.sk_slab + (size_t)tile * S * (BM * BN);
+    const int frag0 = w * TM * TN;
+    if (ticket + 1 < (unsigned)S) {
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(slab_t + (size_t)sk * (BM * BN), 0, BM * BN * 4, 0x00020000);
 #pragma unroll
-      for (int kk = 0; kk < IA::BK / 32; ++kk) {
-        bf16x8 fa[TM], fb[TN];
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = frag_bf16<AK, NAT, BM>(sa, wm * 16 * TM + i * 16, kk, lane);
+        for (int j = 0; j < TN; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint4v, acc[i][j]), rs,
+                                                 ((frag0 + i * TN + j) * 64 + lane) * 16, 0, 16 /*sc1*/);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(flg + sk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (tid == 0) {
+      for (int s2 = 0; s2 < S; ++s2) {
+        if (s2 == sk) continue;
+        for (unsigned spins = 0; spins < (1u << 24); ++spins) {
+          if (__hip_atomic_load(flg + s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __hip_atomic_store(flg + s2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    asm volatile("" ::: "memory");           // every slab load below is sc1
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(slab_t, 0, S * BM * BN * 4, 0x00020000);
+    // Every load is unconditional and issued before any use (a select of
+    // "register or load" per fragment would make hipcc branch around each
+    // load and wait for it: one memory round trip per fragment).
+    if (S == 2) {
+      // p0 + p1 == p1 + p0 (IEEE addition commutes): arrival order is irrelevant
+      const int other = (1 - sk) * BM * BN * 4;
+      floatx4 ob[TM][TN];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) fb[j] = frag_bf16<BK_, NAT, BN>(sb, wn * 16 * TN + j * 16, kk, lane);
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          ob[i][j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     rs, other + ((frag0 + i * TN + j) * 64 + lane) * 16, 0, 16));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] += ob[i][j];
+    } else {
+      // ((p0 + p1) + p2) + p3 in split order, one slab per round trip (slot
+      // sk was never written: loaded anyway, then replaced by acc)
+      floatx4 r[TM][TN];
+      for (int t = 0; t < S; ++t) {
+        floatx4 lb[TM][TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < TN; ++j) {
+            lb[i][j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       rs, t * BM * BN * 4 + ((frag0 + i * TN + j) * 64 + lane) * 16, 0, 16));
+            asm volatile("" : "+v"(lb[i][j]));   // materialise: no branch around the load
+          }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const floatx4 e = t == sk ? acc[i][j] : lb[i][j];
+            r[i][j] = t == 0 ? e : r[i][j] + e;
+          }
       }
-    } else {
 #pragma unroll
-      for (int kc = 0; kc < IA::BK / 16; ++kc) {
-        floatx4 fa[TM], fb[TN];
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = frag_f32<AK, BM>(sa, wm * 16 * TM + i * 16, kc, lane);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) fb[j] = frag_f32<BK_, BN>(sb, wn * 16 * TN + j * 16, kc, lane);
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
-      }
+        for (int j = 0; j < TN; ++j) acc[i][j] = r[i][j];
     }
   }
 
@@ -471,7 +636,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         float t = 0.f;
 #pragma unroll
         for (int q = 0; q < NW; ++q) t += red[q];
-        ep.lossp[lt] = t;
+        ep.lossp[tile] = t;
       }
       __syncthreads();
     }
@@ -596,7 +761,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         ep.sm_v[n] = vv;
       }
       // gamma | beta (grads already final), 4 per thread over all tiles
-      for (int q = lt * NT + tid; ep.sm_bNp + q * 4 < ep.sm_n; q += nblk * NT) {
+      for (int q = tile * NT + tid; ep.sm_bNp + q * 4 < ep.sm_n; q += ntl * NT) {
         const int i4 = ep.sm_bNp + q * 4;
         const floatx4 gg = *(const floatx4*)(ep.sm_g + i4);
         floatx4 pp = *(floatx4*)(ep.sm_p + i4), mm = *(floatx4*)(ep.sm_m + i4);
@@ -682,14 +847,15 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
   const int tiles_m = Mp / BM, tiles_n = Np / BN, ntiles = tiles_m * tiles_n;
   GemmEpi ep = ep_in;
   ep.tiles_n = tiles_n;
+  const int S = ep.splitk > 1 ? ep.splitk : 1;
   // group height balancing the per-XCD A-panel (gm*BM rows) and B-panel
   // ((ntiles/8/gm)*BN cols) footprints
-  const double per_xcd = ntiles / 8.0;
-  int gm = (int)(sqrt(per_xcd * BN / BM) + 0.5);
+  const double per_xcd = ntiles * S / 8.0;
+  int gm = (int)(sqrt(per_xcd / S * BN / BM) + 0.5);
   const int env_gm = mmad_group_override();
   if (env_gm > 0) gm = env_gm;
   ep.group_m = gm < 1 ? 1 : (gm > tiles_m ? tiles_m : gm);
-  dim3 grd(ntiles), blk(CFG_NT[cfg]);
+  dim3 grd(ntiles * S), blk(CFG_NT[cfg]);
   switch (cfg) {
     case 0: mmad_gemm_kernel<T, TO, AK, BK_, 0, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
     case 1: mmad_gemm_kernel<T, TO, AK, BK_, 1, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
@@ -757,11 +923,15 @@ static int tune_cfg(int dtype, int epi, const void* A, int lda, const void* B, i
     rc = launch_cfg(dtype, epi, A, lda, B, ldb, Mp, Np, K, et, c, s);   // warm
     if (rc != MMAD_OK) break;
     float ms = 0.f;
-    if (hipEventRecord(e0, s) != hipSuccess) { rc = MMAD_EHIP; break; }
-    for (int r = 0; r < 3 && rc == MMAD_OK; ++r) rc = launch_cfg(dtype, epi, A, lda, B, ldb, Mp, Np, K, et, c, s);
+    hipError_t e = hipEventRecord(e0, s);
+    for (int r = 0; r < 3 && rc == MMAD_OK && e == hipSuccess; ++r)
+      rc = launch_cfg(dtype, epi, A, lda, B, ldb, Mp, Np, K, et, c, s);
     if (rc != MMAD_OK) break;
-    if (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
-        hipEventElapsedTime(&ms, e0, e1) != hipSuccess) {
+    if (e == hipSuccess) e = hipEventRecord(e1, s);
+    if (e == hipSuccess) e = hipEventSynchronize(e1);
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (e != hipSuccess) {
+      mmad_set_error("gemm autotune: HIP error %d (%s)", (int)e, hipGetErrorString(e));
       rc = MMAD_EHIP;
       break;
     }
@@ -772,6 +942,36 @@ static int tune_cfg(int dtype, int epi, const void* A, int lda, const void* B, i
   if (rc != MMAD_OK) return rc;
   *out_cfg = best;
   return MMAD_OK;
+}
+
+// split factor for a shape (1, 2 or 4): a function of the shape only, so every
+// tile configuration of the shape accumulates over K in the same order
+int mmad_gemm_splitk(int Mp, int Np, int K, int dtype) {
+  const int bk = dtype == MMAD_BF16 ? 64 : 32;            // K per stage
+  const int t128 = (Mp / 128) * (Np / 128);              // 128x128 output tiles
+  // workspace bound (mmad_gemm_splitk_bytes): S * t128 <= 320
+  auto ok = [&](int S) { return K % (S * bk) == 0 && K / S >= 4 * bk && S * t128 <= 320; };
+  const int env = mmad_splitk_override();
+  if (env == 1 || env == 2 || env == 4) return ok(env) ? env : 1;
+  // the exact-fp32 parity path keeps one sequential K order per output (the
+  // order closest to the reference's; a different fp32 order can flip the
+  // LeakyReLU branch of a pre-activation at rounding level, e.g. 5.6e-7 in
+  // tests/golden/mm192.npz); split-K is the bf16 performance path's
+  if (dtype != MMAD_BF16) return 1;
+  // measured at the bench shapes (B=1024, widths 2048..100): the in-launch
+  // combine (slab round trip + ticket) costs more than the extra CUs buy back,
+  // so the default is no split; 2 and 4 stay available through the override
+  (void)t128;
+  return 1;
+}
+
+// shape-independent bound: S * Mp * Np <= 320 * 128 * 128 slab floats; per
+// launch (1 + S) control words per 64x64 tile <= 1920
+void mmad_gemm_splitk_bytes(int Mp, int Np, size_t* slab_bytes, size_t* ctl_bytes) {
+  (void)Mp;
+  (void)Np;
+  if (slab_bytes) *slab_bytes = (size_t)320 * 128 * 128 * 4;
+  if (ctl_bytes) *ctl_bytes = (size_t)2048 * 4;
 }
 
 int mmad_gemm_plan(int Mp, int Np, int K, int epi, int dtype) {
@@ -790,6 +990,7 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   MMAD_CHECK_ARG(dtype == MMAD_BF16 || dtype == MMAD_F32, "gemm: bad dtype %d", dtype);
   GemmEpi ep = ep_in;
   ep.dbg = mmad_dbg_override();
+  ep.splitk = (ep.sk_slab && ep.sk_ctl) ? mmad_gemm_splitk(Mp, Np, K, dtype) : 1;
   const int env = mmad_tile_override();
   int cfg;
   if (env >= 0 && env < NCFG && cfg_fits(env, Mp, Np, epi)) {

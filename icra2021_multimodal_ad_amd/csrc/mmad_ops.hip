@@ -171,9 +171,10 @@ __global__ __launch_bounds__(64) void bn_finalize_k(int M, int N, int Np, const 
 }
 
 // Finalize + fold.  Block (kb, nb): the 64 producer columns k0..k0+63 (its
-// Welford merge is recomputed per n-block: 16 KB of L2 reads) and the 64
-// consumer rows n0..n0+63 of W.  Merge order: 4 chunk groups (g, g+4, ...)
-// each sequential, then groups 0..3 in order.
+// Welford merge is recomputed per n-block: 16 KB of L2 reads) and the
+// 64 * FOLD_RPT consumer rows n0.. of W.  Merge order: 4 chunk groups
+// (g, g+4, ...) each sequential, then groups 0..3 in order.
+#define FOLD_RPT 2
 template <typename TW>
 __global__ __launch_bounds__(256) void bn_fold_k(int M, int N, int Np, const float* __restrict__ stats,
                                                  int nparts, const float* __restrict__ gamma,
@@ -181,15 +182,19 @@ __global__ __launch_bounds__(256) void bn_fold_k(int M, int N, int Np, const flo
                                                  float* rvar, float momentum, float eps,
                                                  float* save_mean, float* save_rstd, float* scale,
                                                  float* shift, const float* __restrict__ W,
-                                                 TW* __restrict__ wout, float* __restrict__ cpart) {
+                                                 TW* __restrict__ wout, float* __restrict__ cpart,
+                                                 int cp_stride) {
   constexpr int U = 8;
   __shared__ float pm[4][64], pq[4][64], pn[4][64], s_sc[64], s_sh[64];
-  const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64, tid = threadIdx.x;
-  // W tile loads first (independent of the statistics): row r, 16 columns
+  const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64 * FOLD_RPT, tid = threadIdx.x;
+  // W tile loads first (independent of the statistics): rows r + 64 i, 16 columns
   const int r = tid >> 2, cq = (tid & 3) * 16;
-  floatx4 wv[4];
+  floatx4 wv[FOLD_RPT][4];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) wv[u] = *(const floatx4*)(W + (size_t)(n0 + r) * Np + k0 + cq + 4 * u);
+  for (int i = 0; i < FOLD_RPT; ++i)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      wv[i][u] = *(const floatx4*)(W + (size_t)(n0 + r + 64 * i) * Np + k0 + cq + 4 * u);
   {
     const int c = tid & 63, grp = tid >> 6;
     float n = 0.f, mean = 0.f, m2 = 0.f;
@@ -257,23 +262,27 @@ __global__ __launch_bounds__(256) void bn_fold_k(int M, int N, int Np, const flo
   __syncthreads();
   // W' = W * scale (row r, 16 columns), c = sum shift * W (sequential, then
   // the 4 quarter-row lanes combined ((q0 + q1) + (q2 + q3)))
-  float cs = 0.f;
-  TW o[16];
 #pragma unroll
-  for (int u = 0; u < 4; ++u)
+  for (int i = 0; i < FOLD_RPT; ++i) {
+    const int row = n0 + r + 64 * i;
+    float cs = 0.f;
+    TW o[16];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int kl = cq + 4 * u + e;
-      o[4 * u + e] = from_f32<TW>(wv[u][e] * s_sc[kl]);
-      cs += s_sh[kl] * wv[u][e];
-    }
-  TW* dst = wout + (size_t)(n0 + r) * Np + k0 + cq;
+    for (int u = 0; u < 4; ++u)
 #pragma unroll
-  for (int v = 0; v < 16 * (int)sizeof(TW) / 16; ++v)
-    *((uint4v*)dst + v) = *((const uint4v*)o + v);
-  cs += __shfl_xor(cs, 1);
-  cs += __shfl_xor(cs, 2);
-  if ((tid & 3) == 0) cpart[(size_t)blockIdx.x * gridDim.y * 64 + n0 + r] = cs;
+      for (int e = 0; e < 4; ++e) {
+        const int kl = cq + 4 * u + e;
+        o[4 * u + e] = from_f32<TW>(wv[i][u][e] * s_sc[kl]);
+        cs += s_sh[kl] * wv[i][u][e];
+      }
+    TW* dst = wout + (size_t)row * Np + k0 + cq;
+#pragma unroll
+    for (int v = 0; v < 16 * (int)sizeof(TW) / 16; ++v)
+      *((uint4v*)dst + v) = *((const uint4v*)o + v);
+    cs += __shfl_xor(cs, 1);
+    cs += __shfl_xor(cs, 2);
+    if ((tid & 3) == 0) cpart[(size_t)blockIdx.x * cp_stride + row] = cs;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -500,7 +509,7 @@ __global__ __launch_bounds__(1024) void sum2d_k(int rows, int cols, const float*
 
 template <typename T>
 __global__ void pack_input_k(int M, int K, int Mp, int Kp, const float* __restrict__ x, int ldx,
-                             T* __restrict__ out) {
+                             int vec, T* __restrict__ out) {
   constexpr int V = Vec<T>::N;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int cpr = Kp / V;
@@ -508,10 +517,17 @@ __global__ void pack_input_k(int M, int K, int Mp, int Kp, const float* __restri
   const int row = (int)(idx / cpr), c0 = (int)(idx % cpr) * V;
   uint4v r;
   T* p = (T*)&r;
+  const float* src = x + (size_t)row * ldx + c0;
+  if (vec && row < M && c0 + V <= K) {
+    // 16-B aligned rows (checked by the launcher): V/4 dwordx4 loads
+    floatx4 f[V / 4];
 #pragma unroll
-  for (int k = 0; k < V; ++k) {
-    const int col = c0 + k;
-    p[k] = from_f32<T>((row < M && col < K) ? x[(size_t)row * ldx + col] : 0.f);
+    for (int q = 0; q < V / 4; ++q) f[q] = *(const floatx4*)(src + 4 * q);
+#pragma unroll
+    for (int k = 0; k < V; ++k) p[k] = from_f32<T>(f[k / 4][k % 4]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < V; ++k) p[k] = from_f32<T>((row < M && c0 + k < K) ? src[k] : 0.f);
   }
   *(uint4v*)(out + (size_t)row * Kp + c0) = r;
 }
@@ -800,16 +816,17 @@ int mmad_bn_finalize_fold(int dtype, int M, int N, int Mp, int Np, const float* 
                           void* wout, float* cpart, void* stream) {
   MMAD_CHECK_ARG(Mp % 128 == 0 && Np % 128 == 0 && Nc_p % 64 == 0 && M >= 1 && M <= Mp && N <= Np,
                  "bn_finalize_fold: bad sizes");
-  dim3 grd(Np / 64, Nc_p / 64);
+  MMAD_CHECK_ARG(Nc_p % (64 * FOLD_RPT) == 0, "bn_finalize_fold: consumer rows not a multiple of 128");
+  dim3 grd(Np / 64, Nc_p / (64 * FOLD_RPT));
   hipStream_t s = (hipStream_t)stream;
   if (dtype == MMAD_BF16)
     bn_fold_k<bf16><<<grd, 256, 0, s>>>(M, N, Np, stats, Mp / MMAD_PART_ROWS, gamma, beta,
                                         running_mean, running_var, momentum, eps, save_mean,
-                                        save_rstd, scale, shift, W, (bf16*)wout, cpart);
+                                        save_rstd, scale, shift, W, (bf16*)wout, cpart, Nc_p);
   else
     bn_fold_k<float><<<grd, 256, 0, s>>>(M, N, Np, stats, Mp / MMAD_PART_ROWS, gamma, beta,
                                          running_mean, running_var, momentum, eps, save_mean,
-                                         save_rstd, scale, shift, W, (float*)wout, cpart);
+                                         save_rstd, scale, shift, W, (float*)wout, cpart, Nc_p);
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
 }
@@ -920,12 +937,13 @@ int mmad_pack_input(int dtype, int M, int K, int Mp, int Kp, const float* x, int
                     void* stream) {
   MMAD_CHECK_ARG(M <= Mp && K <= Kp && Kp % 8 == 0 && ld_x >= K, "pack_input: bad sizes");
   hipStream_t s = (hipStream_t)stream;
+  const int vec = ((uintptr_t)x % 16 == 0 && ld_x % 4 == 0) ? 1 : 0;
   if (dtype == MMAD_BF16) {
     const int64_t n = (int64_t)Mp * (Kp / 8);
-    pack_input_k<bf16><<<nblk(n, 256), 256, 0, s>>>(M, K, Mp, Kp, x, ld_x, (bf16*)out);
+    pack_input_k<bf16><<<nblk(n, 256), 256, 0, s>>>(M, K, Mp, Kp, x, ld_x, vec, (bf16*)out);
   } else {
     const int64_t n = (int64_t)Mp * (Kp / 4);
-    pack_input_k<float><<<nblk(n, 256), 256, 0, s>>>(M, K, Mp, Kp, x, ld_x, (float*)out);
+    pack_input_k<float><<<nblk(n, 256), 256, 0, s>>>(M, K, Mp, Kp, x, ld_x, vec, (float*)out);
   }
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;

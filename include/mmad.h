@@ -48,13 +48,25 @@ int mmad_pad_granule(void);
  * thr, 4 = 64x128, 5 = 128x128/256 thr; a tile that does not divide a shape
  * falls back to the tuned one), knob 1 = XCD tile-group height override (-1
  * auto), knob 2 = per-shape autotune on first dispatch (1, default) or static
- * heuristic (0), knob 3 = diagnostics (tools/gemm_sweep only).  Defaults from
- * MMAD_GEMM_TILE / MMAD_GEMM_GROUP_M / MMAD_GEMM_AUTOTUNE. */
+ * heuristic (0), knob 3 = diagnostics (tools/gemm_sweep only), knob 4 = split-K
+ * factor override for GEMMs given split-K workspace (0 = shape rule, 1/2/4).
+ * Defaults from MMAD_GEMM_TILE / MMAD_GEMM_GROUP_M / MMAD_GEMM_AUTOTUNE /
+ * MMAD_GEMM_SPLITK. */
 int mmad_tune_set(int knob, int value);
 
 /* ------------------------------------------------------------------------
  * Layer operators
  * ---------------------------------------------------------------------- */
+
+/* Split-K workspace for the calling thread's layer-operator GEMMs below
+ * (optional; no reference counterpart).  Shapes with few output tiles then
+ * split their K loop over 2 or 4 workgroups (a fixed factor per shape) that
+ * combine in-launch.  ws: device memory of >= mmad_gemm_ws_bytes() bytes,
+ * 256-byte aligned, ZEROED before first use (every launch leaves its control
+ * words zero); it must not be shared by GEMMs running concurrently on
+ * different streams.  ws = NULL turns it off. */
+size_t mmad_gemm_ws_bytes(void);
+int mmad_gemm_set_workspace(void* ws, size_t bytes);
 
 /* FCLayer.forward, layers/fc_layer.py:37-48 (nn.Linear -> Activation -> BN).
  * y[Mp][Np] = bn_affine(act(x[Mp][Kp] . w[Np][Kp]^T + bias[Np])).

@@ -11,6 +11,7 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 widths = [2048, 1658, 1268, 879, 489, 100, 489, 879, 1268, 1658, 2048]
 dev = torch.device("cuda", 0)
 lib = _native.load()
+_native.enable_gemm_workspace(dev)
 s = stream_ptr()
 Mp = pad(B)
 

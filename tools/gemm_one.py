@@ -17,6 +17,7 @@ K, N = widths[li], widths[li + 1]
 Kp, Np, Mp = pad(K), pad(N), pad(B)
 dev = torch.device("cuda", 0)
 lib = _native.load()
+_native.enable_gemm_workspace(dev)
 lib.mmad_tune_set(0, tile)
 lib.mmad_tune_set(1, gm)
 x = torch.randn(Mp, Kp, device=dev).bfloat16()
