@@ -55,6 +55,8 @@ SIGNATURES = {
     "mmad_ae_workspace_bytes": (_I64, [_P, _I, _I]),
     "mmad_ae_bind": (_I, [_P, _P, _P, _P, _P, _P, _P]),
     "mmad_ae_sync_shadow": (_I, [_P, _P]),
+    "mmad_ae_set_shadow_pair": (_I, [_P, _P]),
+    "mmad_ae_current_shadow": (_P, [_P]),
     "mmad_ae_train_fwd_bwd": (_I, [_P, _P, _I, _I, _I, _P, _U64, _U64, _F, _P, _P, _I64, _P]),
     "mmad_ae_train_step": (_I, [_P, _P, _I, _I, _I, _P, _U64, _U64, _F, _F, _F, _F, _F, _I, _P,
                                 _P, _I64, _P]),

@@ -43,6 +43,10 @@ struct mmad_ae {
   int64_t n_params, n_weight, n_bn;
   float *params = nullptr, *grads = nullptr, *m = nullptr, *v = nullptr, *running = nullptr;
   void* shadow = nullptr;
+  // bf16 ping-pong: the fused step's Adam writes the new weights into
+  // shadow_alt while this step's backward still reads shadow, then the two
+  // swap; so a dW GEMM need not wait for its layer's bwd-data GEMM
+  void* shadow_alt = nullptr;
   // side stream + events for the dW / Adam overlap (created at bind time)
   hipStream_t side = nullptr;
   std::vector<hipEvent_t> ev_fork, ev_data;
@@ -275,10 +279,27 @@ int mmad_ae_bind(mmad_ae* h, float* params, float* grads, float* adam_m, float* 
   return MMAD_OK;
 }
 
+int mmad_ae_set_shadow_pair(mmad_ae* h, void* alt) {
+  MMAD_CHECK_ARG(h && h->params, "ae_set_shadow_pair: unbound");
+  MMAD_CHECK_ARG(!alt || h->dtype == MMAD_BF16, "ae_set_shadow_pair: bf16 handles only");
+  MMAD_CHECK_ARG(alt != h->shadow, "ae_set_shadow_pair: alt aliases the shadow");
+  h->shadow_alt = alt;
+  return MMAD_OK;
+}
+
+const void* mmad_ae_current_shadow(const mmad_ae* h) { return h ? h->shadow : nullptr; }
+
 int mmad_ae_sync_shadow(mmad_ae* h, void* stream) {
   MMAD_CHECK_ARG(h && h->params, "ae_sync_shadow: unbound");
   if (h->dtype != MMAD_BF16) return MMAD_OK;
+  if (h->shadow_alt) RET_IF(mmad_to_bf16(h->n_weight, h->params, h->shadow_alt, stream));
   return mmad_to_bf16(h->n_weight, h->params, h->shadow, stream);
+}
+
+// the shadow the fused step's Adam writes (bf16 only)
+static void* adam_shadow(const mmad_ae* h, const AeLayer& a) {
+  if (h->dtype != MMAD_BF16) return nullptr;
+  return (char*)(h->shadow_alt ? h->shadow_alt : h->shadow) + a.w_off * 2;
 }
 
 // ---------------------------------------------------------------------------
@@ -313,8 +334,9 @@ static int prepare_ws(const mmad_ae* h, int B, int k, void* ws, int64_t ws_bytes
                  (long long)ws_bytes, (long long)w.bytes);
   MMAD_CHECK_ARG(((uintptr_t)ws) % 256 == 0, "workspace must be 256-byte aligned");
   // split-K arrival counters / flags start every call at zero (each GEMM
-  // leaves them zero again, this heals a poisoned or reused workspace)
-  MMAD_HIP_CHECK(hipMemsetAsync(w.sk_ctl[0], 0, w.sk_ctl_bytes, st));
+  // leaves them zero again, this heals a poisoned or reused workspace); only
+  // when a split can be chosen at all (the default rule never splits)
+  if (mmad_splitk_override() > 1) MMAD_HIP_CHECK(hipMemsetAsync(w.sk_ctl[0], 0, w.sk_ctl_bytes, st));
   return MMAD_OK;
 }
 
@@ -467,6 +489,12 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       dwe.gb_stride = gs.stride;
     }
     const bool dp = adam && h->comm;
+    // ping-pong shadows (bf16): the fused Adam of dW_l writes the other
+    // shadow, so dW_l may start as soon as dz_l is complete
+    const bool ping = adam && !dp && h->shadow_alt && l >= h->dw_main;
+    if (ping) {
+      MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
+    }
     if (!adam || dp) {
       // fork: dz_l is complete on the main stream; dW_l overlaps the chain below
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
@@ -522,8 +550,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       RET_IF(mmad_allreduce_bucket(h->comm, h->grads + a.w_off, n, h->cstream));
       RET_IF(mmad_adam(n, h->params + a.w_off, h->grads + a.w_off, h->m + a.w_off, h->v + a.w_off,
                        adam->b1, adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt,
-                       h->dtype == MMAD_BF16 ? (void*)((char*)h->shadow + a.w_off * 2) : nullptr,
-                       h->dtype == MMAD_BF16 ? n : 0, h->cstream));
+                       adam_shadow(h, a), h->dtype == MMAD_BF16 ? n : 0, h->cstream));
     } else if (adam) {
       // dW_l with this layer's Adam update fused into its epilogue.  It rewrites
       // W_l, so it starts only once the main stream has finished reading W_l
@@ -534,7 +561,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       dwe.ad_p = h->params + a.w_off;
       dwe.ad_m = h->m + a.w_off;
       dwe.ad_v = h->v + a.w_off;
-      dwe.ad_shadow = h->dtype == MMAD_BF16 ? (void*)((char*)h->shadow + a.w_off * 2) : nullptr;
+      dwe.ad_shadow = adam_shadow(h, a);
       dwe.ad_b1 = adam->b1;
       dwe.ad_b2 = adam->b2;
       dwe.ad_eps = adam->eps;
@@ -559,7 +586,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       if (on_main) {
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st));
       } else {
-        MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_data[l], 0));
+        MMAD_HIP_CHECK(hipStreamWaitEvent(side, ping ? h->ev_fork[l] : h->ev_data[l], 0));
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side));
       }
     }
@@ -645,7 +672,11 @@ int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const
   const AdamHyper ah = adam_hyper(lr, beta1, beta2, adam_eps, step);
   RET_IF(run_forward(h, w, x, ld_x, 0, eps, seed, offset, st));
   RET_IF(run_backward(h, w, true, beta_kl, &ah, st));
-  if (!h->comm) return finish_reductions(h, w, false, true, beta_kl, loss_out, st);
+  if (!h->comm) {
+    RET_IF(finish_reductions(h, w, false, true, beta_kl, loss_out, st));
+    if (h->shadow_alt) std::swap(h->shadow, h->shadow_alt);
+    return MMAD_OK;
+  }
   // data parallel tail: bias grads + loss, then one small bucket
   // [all bias | gamma | beta grads] + the loss, its Adam, join
   RET_IF(finish_reductions(h, w, true, true, beta_kl, loss_out, st));
@@ -659,6 +690,7 @@ int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const
                    h->cstream));
   MMAD_HIP_CHECK(hipEventRecord(h->ev_cdone, h->cstream));
   MMAD_HIP_CHECK(hipStreamWaitEvent(st, h->ev_cdone, 0));
+  if (h->shadow_alt) std::swap(h->shadow, h->shadow_alt);
   return MMAD_OK;
 }
 

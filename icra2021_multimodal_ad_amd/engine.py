@@ -10,6 +10,7 @@ strided views into these buffers, so ``state_dict`` / ``load_state_dict`` /
 ``torch.optim`` all see the same memory the kernels use.
 """
 import ctypes
+import os
 
 import torch
 
@@ -67,8 +68,13 @@ class NativeAE:
         self.exp_avg_sq = torch.zeros(self.n_params, **kw)
         self.running = torch.zeros(2 * self.n_bn, **kw)
         self.running[self.n_bn:] = 1.0
-        self.shadow = (torch.zeros(self.n_weight, device=device, dtype=torch.bfloat16)
-                       if self.dt == _native.BF16 else None)
+        # bf16: MMAD_SHADOW_PAIR=1 keeps two weight shadows, ping-ponged by
+        # the fused step (mmad_ae_set_shadow_pair); off by default: the
+        # earlier dW starts steal CUs from the critical bwd-data chain
+        self._pair = self.dt == _native.BF16 and os.environ.get("MMAD_SHADOW_PAIR", "0") == "1"
+        self._shadow_buf = (torch.zeros((2 if self._pair else 1) * self.n_weight, device=device,
+                                        dtype=torch.bfloat16)
+                            if self.dt == _native.BF16 else None)
         if src is not None:
             for name in ("params", "grads", "exp_avg", "exp_avg_sq", "running"):
                 getattr(self, name).copy_(getattr(src, name))
@@ -78,8 +84,23 @@ class NativeAE:
         self._synced_version = None
         if self.device.type != "cuda":
             return
+        sb = self._shadow_buf
         call("mmad_ae_bind", self._h, ptr(self.params), ptr(self.grads), ptr(self.exp_avg),
-             ptr(self.exp_avg_sq), ptr(self.shadow), ptr(self.running))
+             ptr(self.exp_avg_sq), ptr(sb[: self.n_weight] if sb is not None else None),
+             ptr(self.running))
+        if self._pair:
+            call("mmad_ae_set_shadow_pair", self._h, ptr(sb[self.n_weight:]))
+
+    @property
+    def shadow(self):
+        """The bf16 weight shadow the kernels read next (None for fp32)."""
+        sb = self._shadow_buf
+        if sb is None:
+            return None
+        if not self._pair or self.device.type != "cuda":
+            return sb[: self.n_weight]
+        cur = self._lib.mmad_ae_current_shadow(self._h) or 0
+        return sb[self.n_weight:] if cur != sb.data_ptr() else sb[: self.n_weight]
 
     def to(self, device):
         device = torch.device(device)

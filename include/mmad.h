@@ -217,6 +217,17 @@ int mmad_ae_bind(mmad_ae* h, float* params, float* grads, float* adam_m, float* 
  * load_state_dict or any external parameter write).  No-op for MMAD_F32. */
 int mmad_ae_sync_shadow(mmad_ae* h, void* stream);
 
+/* bf16 only: a second n_weight-element bf16 buffer (NULL turns it off).  The
+ * fused step (mmad_ae_train_step) then writes the updated weights into the
+ * other buffer while its backward still reads the current one, and the two
+ * swap at the end of the step, so each layer's dW+Adam GEMM overlaps that
+ * layer's bwd-data GEMM.  mmad_ae_sync_shadow refreshes both. */
+int mmad_ae_set_shadow_pair(mmad_ae* h, void* alt);
+
+/* the bf16 shadow the next kernels will read (changes after each fused step
+ * when a pair is set) */
+const void* mmad_ae_current_shadow(const mmad_ae* h);
+
 /* AutoEncoder.step forward+backward (models/auto_encoder.py:57-73): x fp32
  * [B][ld_x]; writes grads and loss_out[0] (device fp32; sum-MSE, or
  * recon/k + beta*KL for VIB).  eps (VIB, nullable) as mmad_vib_reparam_fwd. */

@@ -134,3 +134,29 @@ def test_train_step_split_factors_agree(dtype):
         cos = float(torch.nn.functional.cosine_similarity(g.double(), g1.double(), dim=0))
         # bf16: activations re-rounded per layer; the bf16-vs-fp32 bar of test_gpu_parity
         assert cos > (1 - 1e-6 if dtype == "f32" else 0.99), (split, cos)
+
+
+def test_shadow_pair_matches_single_shadow(monkeypatch):
+    """bf16 fused steps with the ping-pong weight shadows (dW+Adam of a layer
+    overlapping its bwd-data GEMM) give the same bits as the single-shadow
+    schedule; the current shadow is always bf16(params)."""
+    import types
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    from icra2021_multimodal_ad_amd.common_utils import init_state_dict
+    from icra2021_multimodal_ad_amd.data import synth_windows
+    sd = init_state_dict(1728, 100, 5, seed=5)
+    xs = [torch.from_numpy(synth_windows(512, 1728, seed=10 + i)).cuda() for i in range(3)]
+    res = {}
+    for pair in ("1", "0"):
+        monkeypatch.setenv("MMAD_SHADOW_PAIR", pair)
+        cfg = types.SimpleNamespace(input_size=1728, btl_size=100, n_layers=5, gpu_id=0, dtype="bf16")
+        m = get_model(cfg)
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+        assert m._native._pair == (pair == "1")
+        losses = [float(m.train_step_async(x)) for x in xs]
+        nat = m._native
+        torch.cuda.synchronize()
+        assert torch.equal(nat.shadow, nat.params[: nat.n_weight].bfloat16()), pair
+        res[pair] = (losses, nat.params.clone())
+    assert res["1"][0] == res["0"][0]
+    assert torch.equal(res["1"][1], res["0"][1])

@@ -15,13 +15,13 @@ HEADER = os.path.join(REPO, "include", "mmad.h")
 
 def header_functions():
     src = open(HEADER).read()
-    return re.findall(r"^\s*(?:const char\*|int64_t|size_t|void|int)\s+(mmad_\w+)\s*\(", src, re.M)
+    return re.findall(r"^\s*(?:const char\*|const void\*|int64_t|size_t|void|int)\s+(mmad_\w+)\s*\(", src, re.M)
 
 
 def header_arg_counts():
     src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
     out = {}
-    for m in re.finditer(r"(?:const char\*|int64_t|size_t|void|int)\s+(mmad_\w+)\s*\(([^;]*?)\);", src,
+    for m in re.finditer(r"(?:const char\*|const void\*|int64_t|size_t|void|int)\s+(mmad_\w+)\s*\(([^;]*?)\);", src,
                          re.S):
         args = m.group(2).strip()
         out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
