@@ -82,16 +82,17 @@ def gemm_roofline(model, batch, iters=50):
              1, 0.2, None, None, ptr(out), ptr(stats), s)
     for _ in range(5):
         launch()
-    # one event pair per launch, on the launch stream: kernel duration without
-    # the host's launch gaps
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(iters)]
-    for e0, e1 in ev:
-        e0.record()
+    # one event pair on the launch stream around `iters` back-to-back launches
+    # (the queue stays full, so this is the kernel duration plus the GPU's
+    # dispatch gap; an event pair per launch adds ~2 us of event overhead and
+    # disagrees with rocprofv3's kernel-trace average)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
         launch()
-        e1.record()
+    e1.record()
     torch.cuda.synchronize()
-    avg_s = sum(e0.elapsed_time(e1) for e0, e1 in ev) / 1e3 / iters
+    avg_s = e0.elapsed_time(e1) / 1e3 / iters
     flops = 2.0 * batch * L["K"] * L["N"]
     peak = BF16_PEAK_TFLOPS if dt == _native.BF16 else F32_PEAK_TFLOPS
     ach = flops / avg_s / 1e12

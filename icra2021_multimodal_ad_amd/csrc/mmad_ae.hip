@@ -7,13 +7,15 @@
 // allocation (caller workspace).
 //
 // Train-mode dataflow per hidden layer l (Linear -> LeakyReLU -> BN):
-//   fwd GEMM (A normalised on load with layer l-1's BN affine) -> a_l + Welford
-//   partials -> bn_finalize (mean, rstd, affine, running stats); y_l is never
-//   written to HBM.  Backward: the bwd-data GEMM epilogue emits the BN-backward
-//   column partials of dy_l; bn_act_bwd_apply produces dz_l; the dW GEMM
-//   (B operand = y_{l-1} normalised on load) runs on a side stream, followed
-//   (single-GPU fused step) by that layer's Adam update, overlapping the
-//   remaining backward chain on the main stream.
+//   fwd GEMM -> a_l + Welford partials in its epilogue -> bn_fold (mean, rstd,
+//   scale s, shift t, running stats; W'_{l+1} = W_{l+1} diag(s) and the
+//   partial bias sum_k t[k] W_{l+1}[n][k]) -> the consumer GEMM contracts the
+//   raw a_l with W'; the normalised y_l is never written to HBM.  Backward: the
+//   bwd-data GEMM epilogue emits the BN-backward column partials of dy_l;
+//   bn_act_bwd_apply produces dz_l; the dW GEMM against the raw a_{l-1}, fixed
+//   up in its epilogue (s[k] acc + t[k] db[n]), runs on a side stream with that
+//   layer's Adam update fused into the epilogue (single-GPU step), overlapping
+//   the remaining backward chain on the main stream.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -61,7 +63,7 @@ struct mmad_ae {
   // keep_grads: also write dW to the grads buffer
   int dw_main = [] {
     const char* e = getenv("MMAD_DW_MAIN");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 1;
   }();
   int keep_grads = [] {
     const char* e = getenv("MMAD_KEEP_GRADS");
