@@ -52,6 +52,13 @@ static int g_splitk = [] {
   return e ? atoi(e) : 0;
 }();
 int mmad_splitk_override() { return g_splitk; }
+// tile for the dW GEMMs with the fused Adam epilogue (the autotuner times
+// them without Adam, which under-weights the epilogue's HBM traffic)
+static int g_tile_adam = [] {
+  const char* e = getenv("MMAD_GEMM_TILE_ADAM");
+  return e ? atoi(e) : -1;
+}();
+int mmad_tile_adam_override() { return g_tile_adam; }
 
 int mmad_tune_set(int knob, int value) {
   switch (knob) {
@@ -60,6 +67,7 @@ int mmad_tune_set(int knob, int value) {
     case 2: g_autotune = value; return MMAD_OK;
     case 3: g_dbg = value; return MMAD_OK;
     case 4: g_splitk = value; return MMAD_OK;
+    case 5: g_tile_adam = value; return MMAD_OK;
     default: mmad_set_error("tune_set: unknown knob %d", knob); return MMAD_EINVAL;
   }
 }

@@ -992,8 +992,11 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   ep.dbg = mmad_dbg_override();
   ep.splitk = (ep.sk_slab && ep.sk_ctl) ? mmad_gemm_splitk(Mp, Np, K, dtype) : 1;
   const int env = mmad_tile_override();
+  const int env_adam = ep.ad_p ? mmad_tile_adam_override() : -1;
   int cfg;
-  if (env >= 0 && env < NCFG && cfg_fits(env, Mp, Np, epi)) {
+  if (env_adam >= 0 && env_adam < NCFG && cfg_fits(env_adam, Mp, Np, epi)) {
+    cfg = env_adam;
+  } else if (env >= 0 && env < NCFG && cfg_fits(env, Mp, Np, epi)) {
     cfg = env;   // forced tile (tuning / tests); a shape it does not fit falls through
   } else {
     const TuneKey key{dtype, epi, Mp, Np, K};

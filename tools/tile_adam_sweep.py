@@ -1,0 +1,37 @@
+"""Step time of the fused train step with the Adam-fused dW GEMMs forced to
+each tile config (tuning knob 5; -1 = the autotuned pick, which is timed
+without the Adam epilogue).  Usage: python tools/tile_adam_sweep.py [dim] [batch] [steps]"""
+import sys
+import time
+import types
+
+sys.path.insert(0, ".")
+import torch
+
+from icra2021_multimodal_ad_amd import _native
+from icra2021_multimodal_ad_amd.model_builder import get_model
+from icra2021_multimodal_ad_amd.data import synth_windows_device
+
+dim = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 300
+dev = torch.device("cuda", 0)
+lib = _native.load()
+pool = [synth_windows_device(B, dim, dev, seed=100 + i) for i in range(8)]
+torch.manual_seed(0)
+m = get_model(types.SimpleNamespace(input_size=dim, btl_size=100, n_layers=5, gpu_id=0, dtype="bf16"))
+for v in (-1, 0, 1, 2, 3, 4, 5, -1):
+    lib.mmad_tune_set(5, v)
+    for i in range(10):
+        m.train_step_async(pool[i % 8])
+    torch.cuda.synchronize()
+    best = None
+    for rep in range(3):
+        t0 = time.perf_counter()
+        for i in range(steps):
+            m.train_step_async(pool[i % 8])
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / steps * 1e3
+        best = el if best is None else min(best, el)
+    print(f"tile_adam={v}: {best:.4f} ms/step", flush=True)
+lib.mmad_tune_set(5, -1)
