@@ -50,7 +50,8 @@ int mmad_pad_granule(void);
  * auto), knob 2 = per-shape autotune on first dispatch (1, default) or static
  * heuristic (0), knob 3 = diagnostics (tools/gemm_sweep only), knob 4 = split-K
  * factor override for GEMMs given split-K workspace (0 = shape rule, 1/2/4),
- * knob 5 = tile of the dW GEMMs with the fused Adam epilogue (-1 = rule).
+ * knob 5 = tile of the dW GEMMs with the fused Adam epilogue (default 3 =
+ * 64x64; -1 = autotuned like the others).
  * Defaults from MMAD_GEMM_TILE / MMAD_GEMM_GROUP_M / MMAD_GEMM_AUTOTUNE /
  * MMAD_GEMM_SPLITK / MMAD_GEMM_TILE_ADAM. */
 int mmad_tune_set(int knob, int value);
