@@ -61,6 +61,20 @@ static int g_tile_adam = [] {
   return e ? atoi(e) : 3;
 }();
 int mmad_tile_adam_override() { return g_tile_adam; }
+// per-epilogue tile overrides (-1 = autotuned): bwd-data GEMMs, forward GEMMs
+static int g_tile_bwd_data = [] {
+  const char* e = getenv("MMAD_GEMM_TILE_BWD_DATA");
+  return e ? atoi(e) : -1;
+}();
+static int g_tile_fwd = [] {
+  const char* e = getenv("MMAD_GEMM_TILE_FWD");
+  return e ? atoi(e) : -1;
+}();
+int mmad_tile_epi_override(int epi) {
+  if (epi == GEMM_EPI_BWD_DATA) return g_tile_bwd_data;
+  if (epi == GEMM_EPI_FWD || epi == GEMM_EPI_MSE) return g_tile_fwd;
+  return -1;
+}
 
 int mmad_tune_set(int knob, int value) {
   switch (knob) {
@@ -70,6 +84,8 @@ int mmad_tune_set(int knob, int value) {
     case 3: g_dbg = value; return MMAD_OK;
     case 4: g_splitk = value; return MMAD_OK;
     case 5: g_tile_adam = value; return MMAD_OK;
+    case 6: g_tile_bwd_data = value; return MMAD_OK;
+    case 7: g_tile_fwd = value; return MMAD_OK;
     default: mmad_set_error("tune_set: unknown knob %d", knob); return MMAD_EINVAL;
   }
 }

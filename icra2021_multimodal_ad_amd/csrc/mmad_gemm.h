@@ -83,6 +83,7 @@ int mmad_autotune_enabled();
 int mmad_dbg_override();
 int mmad_splitk_override();   // 0 = shape rule; 1, 2, 4 = forced split factor
 int mmad_tile_adam_override();  // >= 0: tile of the Adam-fused dW GEMMs
+int mmad_tile_epi_override(int epi);  // >= 0: tile of this epilogue's GEMMs
 
 // tile configuration a problem will run with (autotuned on first dispatch of
 // the shape; a static heuristic before that / when tuning is off)

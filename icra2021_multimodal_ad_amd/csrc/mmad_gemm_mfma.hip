@@ -992,10 +992,10 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   ep.dbg = mmad_dbg_override();
   ep.splitk = (ep.sk_slab && ep.sk_ctl) ? mmad_gemm_splitk(Mp, Np, K, dtype) : 1;
   const int env = mmad_tile_override();
-  const int env_adam = ep.ad_p ? mmad_tile_adam_override() : -1;
+  const int env_epi = ep.ad_p ? mmad_tile_adam_override() : mmad_tile_epi_override(epi);
   int cfg;
-  if (env_adam >= 0 && env_adam < NCFG && cfg_fits(env_adam, Mp, Np, epi)) {
-    cfg = env_adam;
+  if (env_epi >= 0 && env_epi < NCFG && cfg_fits(env_epi, Mp, Np, epi)) {
+    cfg = env_epi;
   } else if (env >= 0 && env < NCFG && cfg_fits(env, Mp, Np, epi)) {
     cfg = env;   // forced tile (tuning / tests); a shape it does not fit falls through
   } else {

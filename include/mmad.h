@@ -51,9 +51,11 @@ int mmad_pad_granule(void);
  * heuristic (0), knob 3 = diagnostics (tools/gemm_sweep only), knob 4 = split-K
  * factor override for GEMMs given split-K workspace (0 = shape rule, 1/2/4),
  * knob 5 = tile of the dW GEMMs with the fused Adam epilogue (default 3 =
- * 64x64; -1 = autotuned like the others).
+ * 64x64; -1 = autotuned like the others), knobs 6 / 7 = tile of the bwd-data /
+ * forward GEMMs (-1 = autotuned).
  * Defaults from MMAD_GEMM_TILE / MMAD_GEMM_GROUP_M / MMAD_GEMM_AUTOTUNE /
- * MMAD_GEMM_SPLITK / MMAD_GEMM_TILE_ADAM. */
+ * MMAD_GEMM_SPLITK / MMAD_GEMM_TILE_ADAM / MMAD_GEMM_TILE_BWD_DATA /
+ * MMAD_GEMM_TILE_FWD. */
 int mmad_tune_set(int knob, int value);
 
 /* ------------------------------------------------------------------------
