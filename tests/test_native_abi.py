@@ -57,7 +57,7 @@ def test_abi_constants_and_errors(lib):
                          None, None)
     assert rc == -1
     assert b"multiples of 128" in lib.mmad_last_error_string()
-    assert lib.mmad_tune_set(7, 0) == -1
+    assert lib.mmad_tune_set(99, 0) == -1
 
 
 def test_executor_layout_matches_reference_shapes(lib):
