@@ -34,8 +34,9 @@
 
 // Executor events only order work between streams of this device, so they
 // skip the system-scope fence (L2 writeback for host visibility) that a
-// default event adds at record time: measured ~6 us of main-stream bubble per
-// record in the backward chain.  Device-scope release/acquire (the same as a
+// default event adds at record time.  Each record still leaves a ~5 us bubble
+// on the main stream (~6 us with the fence; 0.513 vs 0.521 ms/step).
+// Device-scope release/acquire (the same as a
 // kernel boundary on one stream) still orders the data.  MMAD_EVENT_SYSFENCE=1
 // restores the default.
 static const unsigned kEvFlags = [] {
@@ -80,6 +81,13 @@ struct mmad_ae {
   int keep_grads = [] {
     const char* e = getenv("MMAD_KEEP_GRADS");
     return e ? atoi(e) : 0;
+  }();
+  // fused step: record the "bwd-data of l done" event only every ev_every-th
+  // side-stream layer (each record costs a bubble on the main stream); the dW
+  // GEMMs of the layers in between wait for the next recorded one
+  int ev_every = [] {
+    const char* e = getenv("MMAD_EV_EVERY");
+    return e ? atoi(e) : 1;
   }();
   ~mmad_ae() {
     for (auto e : ev_fork) (void)hipEventDestroy(e);
@@ -479,11 +487,18 @@ struct AdamHyper { float b1, b2, eps, step_size, bc2_sqrt; };
 // partials come from the MSE-fused forward epilogue; otherwise the caller has
 // packed dL/dx_hat into the last layer's dy buffer.  adam != null: each
 // layer's Adam update runs on the side stream right after its dW GEMM.
+struct PendingDW {
+  const void *dz, *in;
+  int lda, ldb, M, N, K;
+  GemmEpi ep;
+};
+
 static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const AdamHyper* adam,
                         hipStream_t st) {
   const int dt = h->dtype;
   const int nL = (int)h->L.size();
   hipStream_t side = h->side;
+  std::vector<PendingDW> pending;   // side-stream dW GEMMs waiting for a recorded event
   for (int l = nL - 1; l >= 0; --l) {
     const AeLayer& a = h->L[l];
     LayerWS& s = w.l[l];
@@ -512,6 +527,12 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     if (ping) {
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
     }
+    // does the main stream record ev_data[l] (bwd-data of l done)?  Needed by
+    // the DP exchange and by side-stream dW GEMMs (every ev_every-th layer;
+    // the lowest side layer always records, flushing the deferred ones)
+    const bool side_dw = adam && !dp && !ping && l >= h->dw_main;
+    const bool rec = dp || (side_dw && (h->ev_every <= 1 || l == h->dw_main ||
+                                        (l - h->dw_main) % h->ev_every == 0));
     if (!adam || dp) {
       // fork: dz_l is complete on the main stream; dW_l overlaps the chain below
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
@@ -543,7 +564,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
         ep.bn_part = ps.bnpart;
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
                                   a.Np, ep, st));
-        if (adam) MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
+        if (rec) MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
         RET_IF(mmad_bn_act_bwd_apply(dt, p.act, h->slope, rows_of(w, p), p.N, Mpp, p.Np, ps.dy,
                                      ps.out, ps.mean, ps.rstd, h->params + p.g_off, ps.bnpart,
                                      Mpp / 64, ps.dz, h->grads + p.g_off, h->grads + p.be_off,
@@ -572,7 +593,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       // dW_l with this layer's Adam update fused into its epilogue.  It rewrites
       // W_l, so it starts only once the main stream has finished reading W_l
       // (bwd-data of l); the rest of the chain keeps overlapping it.
-      if (l == 0 || !(h->L[l - 1].bn) || (h->vib && l == h->n_enc))
+      if (rec && (l == 0 || !(h->L[l - 1].bn) || (h->vib && l == h->n_enc)))
         MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
       const BiasSrc bs = bias_src(h, w, l, from_mse);
       dwe.ad_p = h->params + a.w_off;
@@ -602,12 +623,22 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       const bool on_main = l < h->dw_main;
       if (on_main) {
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st));
+      } else if (ping) {
+        MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
+        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side));
+      } else if (!rec) {
+        pending.push_back(PendingDW{dz, in, a.Np, a.Kp, a.Np, a.Kp, Mp, dwe});
       } else {
-        MMAD_HIP_CHECK(hipStreamWaitEvent(side, ping ? h->ev_fork[l] : h->ev_data[l], 0));
+        MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_data[l], 0));
+        for (const PendingDW& q : pending)
+          RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, q.dz, q.lda, q.in, q.ldb, q.M, q.N, q.K, q.ep,
+                         side));
+        pending.clear();
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side));
       }
     }
   }
+  MMAD_CHECK_ARG(pending.empty(), "ae backward: deferred dW GEMMs left unissued");
   // join the side stream back into the main stream
   MMAD_HIP_CHECK(hipEventRecord(h->ev_join, side));
   MMAD_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
