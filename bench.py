@@ -1,11 +1,12 @@
 """Benchmark: sensor-windows/sec of the AE train step (fwd + sum-MSE + bwd +
 Adam) on synthetic 4-modal windows -- BASELINE.json configs[1]: D=2048,
 batch=1024 per GPU, bf16 storage / fp32 accumulate, 1..8 MI355X (weak scaling,
-RCCL all-reduce of the flat gradient per step).
+per-layer RCCL all-reduce of the gradients overlapped with the backward).
 
 Prints ONE JSON line (rank 0) with the driver's fields plus ``roofline`` (the
-encoder's first GEMM, the dominant kernel, timed with HIP events on the
-stream it runs on) and ``cpu_baseline`` (the oracle's numpy fp32 train step on
+encoder's first GEMM, the dominant kernel, timed with a HIP event pair around
+back-to-back launches on the stream it runs on; HBM traffic from the newest
+profiles/*_pmc_traffic.json) and ``cpu_baseline`` (the oracle's numpy fp32 train step on
 host cores, bounded sample).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--dim 2048] [--batch 1024]
@@ -59,7 +60,7 @@ def cpu_baseline(d, batch, budget_s=12.0, threads=16):
 
 def gemm_roofline(model, batch, iters=50):
     """Average duration of the encoder's first-layer forward GEMM (the largest
-    MFMA kernel of the step) via HIP events on the launch stream."""
+    MFMA kernel of the step) from HIP events on the launch stream."""
     import torch
     from icra2021_multimodal_ad_amd import _native
     from icra2021_multimodal_ad_amd._native import call, ptr, stream_ptr
@@ -105,7 +106,7 @@ def gemm_roofline(model, batch, iters=50):
 
 def _pmc_traffic(dim, batch, dt):
     """HBM-side bytes per launch of the roofline kernel from the committed
-    rocprofv3 PMC passes (profiles/r01h_pmc_traffic.json: FETCH_SIZE x2 +
+    rocprofv3 PMC passes (newest profiles/*_pmc_traffic.json: FETCH_SIZE x2 +
     WRITE_SIZE, gfx950 correction) when they were taken at this workload."""
     import glob
     from icra2021_multimodal_ad_amd import _native
