@@ -32,11 +32,13 @@
 //  * K-major operand: [rows][128 B], 16-byte chunk j stored at j ^ ((row>>1)&7)
 //    -> conflict-free ds_read_b128 (natural k order) / ds_read_b64 pairs.
 //  * MN-major operand: [BK][rows*esize], 16-byte chunk XOR-swizzled per k-row
-//    so the tr-reads of 8 consecutive k-rows hit disjoint banks.
-// bf16 k-slot order inside one 32-deep MFMA step: with both operands K-major
-// lane group g (= lane>>4) owns k = 8g..8g+7 (one ds_read_b128); when either
-// operand is MN-major it owns k = {4g..4g+3} U {16+4g..16+4g+3} in both
-// operands (two 4-deep reads), so the contraction is exact either way.
+//    so the tr-reads of one 32-lane half (8 k-rows) hit disjoint banks.
+// bf16 k-slot order inside one 32-deep MFMA step: lane group g (= lane>>4)
+// owns k = 8g..8g+7 in both operands whatever their layout (one ds_read_b128
+// from a K-major image, two ds_read_b64_tr_b16 from an MN-major one).  The
+// backward GEMMs used a permuted order {4g..4g+3} U {16+4g..16+4g+3} before,
+// which cost the K-major operand two ds_read_b64 per fragment and measured
+// 2x the LDS cycles of the forward loop (SQ_LDS_BANK_CONFLICT 1.7M vs 13k).
 #include "mmad_common.h"
 #include "mmad_gemm.h"
 
@@ -76,14 +78,20 @@ struct Img {
 
 // 16-byte-chunk XOR swizzle of LDS row `r` (an involution):
 //  * K-major, 128 B rows: (r>>1)&7;
-//  * MN-major bf16, >=256 B rows: (r&7)<<1; 128 B rows: ((r>>1)&3)<<1
-//    (the XOR must stay inside the row's 8 chunks);
+//  * MN-major bf16 (rows are k): one transposed read of a 32-lane half covers
+//    k rows {0..3, 8..11} (+4 for the second read) of a 32-deep step, 32 B of
+//    each; >= 256 B rows start every k row on bank 0, so the XOR takes
+//    (k&3) | ((k>>3)&1)<<2 (even chunk steps of 8 banks); 128 B rows alternate
+//    bank halves by k parity, so (k>>1)&1 | ((k>>3)&1)<<1 (the XOR must stay
+//    inside the row's 8 chunks).  Conflict-free for both reads of a half;
 //  * MN-major f32 (rows >= 256 B): r&7 (spreads the 4-row-apart ds_read_b32 groups).
 template <typename T, bool KMAJ, int RB>
 __device__ __forceinline__ int swz(int r) {
   static_assert(KMAJ || RB >= (sizeof(T) == 2 ? 128 : 256), "MN-major row too short for its swizzle");
   if constexpr (KMAJ) return (r >> 1) & 7;
-  else if constexpr (sizeof(T) == 2) return RB >= 256 ? ((r & 7) << 1) : (((r >> 1) & 3) << 1);
+  else if constexpr (sizeof(T) == 2)
+    return RB >= 256 ? (((r & 3) | (((r >> 3) & 1) << 2)) << 1)
+                     : ((((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1);
   else return r & 7;
 }
 
@@ -106,8 +114,10 @@ __device__ __forceinline__ void issue_stage(char* img, const T* __restrict__ G, 
 }
 
 // ---- bf16 fragment reads (16x16x32 MFMA operand) ---------------------------
-// NAT: natural k order (both operands K-major): lane group g owns k = 8g..8g+7.
-// otherwise permuted: k = {4g..4g+3} U {16+4g..16+4g+3}.
+// Natural k order for both layouts: lane group g owns k = 8g..8g+7 (K-major:
+// one ds_read_b128; MN-major: two ds_read_b64_tr_b16 of k rows 8g..8g+3 and
+// 8g+4..8g+7).  (NAT = false, the older permuted order {4g..4g+3} U
+// {16+4g..16+4g+3}, is kept for the K-major reader only.)
 template <bool KMAJ, bool NAT, int ROWS>
 __device__ __forceinline__ bf16x8 frag_bf16(const char* img, int rbase, int kk, int lane) {
   using I = Img<bf16, KMAJ, ROWS, 256>;   // RB only
@@ -125,9 +135,9 @@ __device__ __forceinline__ bf16x8 frag_bf16(const char* img, int rbase, int kk, 
       return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     }
   } else {
-    static_assert(!NAT, "MN-major operand needs the permuted k order");
+    static_assert(NAT, "MN-major reads deliver the natural k order");
     const int q = (lane >> 2) & 3, p = lane & 3;
-    const int k1 = kk * 32 + 4 * g + q, k2 = k1 + 16;
+    const int k1 = kk * 32 + 8 * g + q, k2 = k1 + 4;
     const int byte = (rbase + 4 * p) * 2;
     const int j = byte >> 4, within = byte & 15;
     const MMAD_LDS char* base = (const MMAD_LDS char*)img;
@@ -249,7 +259,9 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   static_assert(WM * WN == NW && TM % 2 == 0, "wave grid");
   using IA = Img<T, AK, BM, NT>;
   using IB = Img<T, BK_, BN, NT>;
-  constexpr bool NAT = AK && BK_;
+  // bf16: every operand layout delivers the natural k order (lane group g owns
+  // k = 8g..8g+7), so a K-major operand is one ds_read_b128 per fragment
+  constexpr bool NAT = true;
   constexpr int SLOT = IA::BYTES + IB::BYTES;
   constexpr int NL = IA::CHUNKS + IB::CHUNKS;          // vm ops per thread per stage
   constexpr bool FWDLIKE = EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_MSE || EPI == GEMM_EPI_SCORE;
