@@ -208,7 +208,7 @@ def main():
     }
     if rank == 0:
         res["roofline"] = gemm_roofline(model, args.batch)
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:   # host baseline: rank 0 at N=1 only
             res["cpu_baseline"] = cpu_baseline(args.dim, args.batch, budget_s=args.cpu_budget)
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -3,10 +3,12 @@
 
 Workload: the RaPP scoring path of the reference (reconstruction_aggregation.py
 :6-37 get_diffs + utils/metric.py:133 BASE and :145-181 SAP), streamed over N
-windows already resident in HBM: one native call per batch (mmad_ae_score:
-eval AE forward, then the encoder over x_hat reusing the encoder activations of
-x; per-layer squared-diff row sums in the GEMM epilogues -- the diffs are never
-materialised).  BASE and SAP per window are reduced on the device.
+windows already resident in HBM: ONE native call for the whole pass
+(mmad_ae_score_stream), captured once as a hipGraph and replayed with one
+launch (--no-graph: eager launches).  Per batch: eval AE forward, then the
+encoder over x_hat reusing the encoder activations of x; per-layer
+squared-diff row sums in the GEMM epilogues -- the diffs are never
+materialised.  BASE and SAP per window are reduced on the device.
 --nap adds the NAP score (utils/metric.py:183-238): fit on a train set of diffs,
 then per batch the diffs are materialised and scored by one GEMM
 (mmad_nap_score).
@@ -65,6 +67,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--nap", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     args = ap.parse_args()
 
     import torch
@@ -96,15 +99,31 @@ def main():
     layer_sq = torch.empty((nat.n_enc + 1, N), device=dev)
     ra.score_windows(x[: args.batch], model, args.batch, out=layer_sq[:, : args.batch])  # warm/tune
     torch.cuda.synchronize()
-    best = None
-    for _ in range(args.reps):
-        t0 = time.perf_counter()
-        ra.score_windows(x, model, args.batch, out=layer_sq)
-        base = ra.base_from_layer_sq(layer_sq, widths)
-        sap = ra.sap_from_layer_sq(layer_sq, widths)
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-        best = el if best is None else min(best, el)
+
+    def timed(graph, xs, bs, out, reps):
+        best = None
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ra.score_windows(xs, model, bs, out=out, graph=graph)
+            b_ = ra.base_from_layer_sq(out, widths)
+            s_ = ra.sap_from_layer_sq(out, widths)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            best = el if best is None else min(best, el)
+        return best, b_, s_
+
+    # the first graph call runs eagerly and captures the pass; timed: replays
+    ra.score_windows(x, model, args.batch, out=layer_sq, graph=not args.no_graph)
+    best, base, sap = timed(not args.no_graph, x, args.batch, layer_sq, args.reps)
+    eager, _, _ = timed(False, x, args.batch, layer_sq, 1)
+    # the reference's own scoring batch (get_diffs default 698) over 64k
+    # windows: launch-bound, where the captured graph matters
+    ns = min(N, 1 << 16)
+    small = {}
+    for g_ in (False, True):
+        ra.score_windows(x[:ns], model, 698, out=layer_sq[:, :ns], graph=g_)
+        small["graph" if g_ else "eager"] = timed(g_, x[:ns], 698, layer_sq[:, :ns], 3)[0]
     value = N / best
     fpw = score_flops_per_window(nat.enc_widths, nat.dec_widths)
 
@@ -120,6 +139,10 @@ def main():
         "config": {"workload": f"RaPP scoring (get_diffs + BASE + SAP) D={args.dim}, btl=100, "
                                f"n_layers=5, batch {args.batch}", "windows": N},
         "ms_total": round(best * 1e3, 3),
+        "launch": "eager" if args.no_graph else "hipGraph replay (one graph for the whole pass)",
+        "eager_ms_total": round(eager * 1e3, 3),
+        "batch698": {"windows": ns, "eager_windows_per_s": round(ns / small["eager"], 1),
+                     "graph_windows_per_s": round(ns / small["graph"], 1)},
         "model_tflops": round(value * fpw / 1e12, 2),
         "score_checksum": {"base_mean": float(base.mean()), "sap_mean": float(sap.mean())},
     }

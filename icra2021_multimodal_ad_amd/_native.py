@@ -64,6 +64,9 @@ SIGNATURES = {
     "mmad_ae_adam": (_I, [_P, _F, _F, _F, _F, _I, _P]),
     "mmad_ae_forward": (_I, [_P, _P, _I, _I, _I, _P, _I, _P, _P, _I64, _P]),
     "mmad_ae_score": (_I, [_P, _P, _I, _I, _P, _P, _P, _I64, _P]),
+    "mmad_ae_score_stream": (_I, [_P, _P, _I, _I64, _I, _P, _I64, _P, _I64, _I, _P]),
+    "mmad_ae_graph_count": (_I, [_P]),
+    "mmad_ae_clear_graphs": (_I, [_P]),
     "mmad_comm_unique_id_bytes": (_I, []),
     "mmad_comm_get_unique_id": (_I, [_P]),
     "mmad_comm_create": (_I, [ctypes.POINTER(_P), _P, _I, _I]),

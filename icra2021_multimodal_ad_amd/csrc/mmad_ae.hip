@@ -16,6 +16,7 @@
 //   up in its epilogue (s[k] acc + t[k] db[n]), runs on a side stream with that
 //   layer's Adam update fused into the epilogue (single-GPU step), overlapping
 //   the remaining backward chain on the main stream.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -89,7 +90,18 @@ struct mmad_ae {
     const char* e = getenv("MMAD_EV_EVERY");
     return e ? atoi(e) : 1;
   }();
+  // hipGraph cache for mmad_ae_score_stream: one captured graph per
+  // (input, output, workspace, N, batch) pass, replayed with one launch
+  struct ScoreGraph {
+    const float* x; int64_t ld_x, N; int batch; float* sq; int64_t ld_sq; void* ws;
+    const void* wts;   // weight operand base (the bf16 shadow may be re-pointed)
+    hipGraphExec_t exec;
+  };
+  std::vector<ScoreGraph> graphs;
+  hipStream_t gstream = nullptr;   // capture stream (the caller's may be the null stream)
   ~mmad_ae() {
+    for (auto& g : graphs) (void)hipGraphExecDestroy(g.exec);
+    if (gstream) (void)hipStreamDestroy(gstream);
     for (auto e : ev_fork) (void)hipEventDestroy(e);
     for (auto e : ev_data) (void)hipEventDestroy(e);
     if (ev_join) (void)hipEventDestroy(ev_join);
@@ -804,13 +816,10 @@ int mmad_ae_forward(mmad_ae* h, const float* x, int ld_x, int B, int train_bn, f
   return MMAD_OK;
 }
 
-int mmad_ae_score(mmad_ae* h, const float* x, int ld_x, int B, float* layer_sq, float* diffs,
-                  void* ws, int64_t ws_bytes, void* stream) {
-  MMAD_CHECK_ARG(h && h->params && h->running, "ae_score: unbound handle");
-  MMAD_CHECK_ARG(x && ld_x >= h->L[0].K && layer_sq, "ae_score: bad args");
-  AeWS w;
-  RET_IF(prepare_ws(h, B, 1, ws, ws_bytes, w, (hipStream_t)stream));
-  hipStream_t st = (hipStream_t)stream;
+// one batch of the scoring pass on a prepared workspace; layer_sq row l at
+// layer_sq + l*ld_sq
+static int score_batch(mmad_ae* h, const float* x, int ld_x, int B, float* layer_sq,
+                       int64_t ld_sq, float* diffs, AeWS& w, hipStream_t st) {
   const int dt = h->dtype;
   const int nL = (int)h->L.size();
   RET_IF(mmad_pack_input(dt, B, h->L[0].K, w.Mpe, h->L[0].Kp, x, ld_x, w.xin, st));
@@ -877,8 +886,80 @@ int mmad_ae_score(mmad_ae* h, const float* x, int ld_x, int B, float* layer_sq, 
   jobs.j[0] = MmadReduceJob{w.l[nL - 1].rowsq, layer_sq, last.Np / 128, w.Mpd, B, B, 1.f, 0,
                             nullptr, 0, 0.f};
   for (int e = 0; e < h->n_enc; ++e)
-    jobs.j[e + 1] = MmadReduceJob{w.l[e].rowsq, layer_sq + (size_t)(e + 1) * B, h->L[e].Np / 128,
-                                  w.Mpe, B, B, 1.f, 0, nullptr, 0, 0.f};
+    jobs.j[e + 1] = MmadReduceJob{w.l[e].rowsq, layer_sq + (size_t)(e + 1) * ld_sq,
+                                  h->L[e].Np / 128, w.Mpe, B, B, 1.f, 0, nullptr, 0, 0.f};
   MMAD_CHECK_ARG(h->n_enc + 1 <= MMAD_MAX_REDUCE_JOBS, "too many encoder layers");
   return mmad_reduce_jobs(jobs, h->n_enc + 1, B, st);
+}
+
+int mmad_ae_score(mmad_ae* h, const float* x, int ld_x, int B, float* layer_sq, float* diffs,
+                  void* ws, int64_t ws_bytes, void* stream) {
+  MMAD_CHECK_ARG(h && h->params && h->running, "ae_score: unbound handle");
+  MMAD_CHECK_ARG(x && ld_x >= h->L[0].K && layer_sq, "ae_score: bad args");
+  AeWS w;
+  RET_IF(prepare_ws(h, B, 1, ws, ws_bytes, w, (hipStream_t)stream));
+  return score_batch(h, x, ld_x, B, layer_sq, B, diffs, w, (hipStream_t)stream);
+}
+
+// the whole N-window pass, batch by batch, on stream st
+static int score_pass(mmad_ae* h, const float* x, int ld_x, int64_t N, int batch, float* layer_sq,
+                      int64_t ld_sq, void* ws, int64_t ws_bytes, hipStream_t st) {
+  for (int64_t s0 = 0; s0 < N; s0 += batch) {
+    const int B = (int)std::min<int64_t>(batch, N - s0);
+    AeWS w;
+    RET_IF(prepare_ws(h, B, 1, ws, ws_bytes, w, st));
+    RET_IF(score_batch(h, x + s0 * ld_x, ld_x, B, layer_sq + s0, ld_sq, nullptr, w, st));
+  }
+  return MMAD_OK;
+}
+
+int mmad_ae_score_stream(mmad_ae* h, const float* x, int ld_x, int64_t N, int batch,
+                         float* layer_sq, int64_t ld_sq, void* ws, int64_t ws_bytes, int use_graph,
+                         void* stream) {
+  MMAD_CHECK_ARG(h && h->params && h->running, "ae_score_stream: unbound handle");
+  MMAD_CHECK_ARG(x && ld_x >= h->L[0].K && layer_sq && N >= 1 && batch >= 1 && ld_sq >= N,
+                 "ae_score_stream: bad args (N=%lld batch=%d ld_sq=%lld)", (long long)N, batch,
+                 (long long)ld_sq);
+  hipStream_t st = (hipStream_t)stream;
+  if (!use_graph) return score_pass(h, x, ld_x, N, batch, layer_sq, ld_sq, ws, ws_bytes, st);
+  for (auto& g : h->graphs) {
+    if (g.x == x && g.ld_x == ld_x && g.N == N && g.batch == batch && g.sq == layer_sq &&
+        g.ld_sq == ld_sq && g.ws == ws && g.wts == weights(h, h->L[0])) {
+      MMAD_HIP_CHECK(hipGraphLaunch(g.exec, st));
+      return MMAD_OK;
+    }
+  }
+  // first pass of this shape: run it eagerly (that also settles every GEMM
+  // tile choice, which cannot be timed under capture), then capture the same
+  // launches on the handle's capture stream for the next calls
+  RET_IF(score_pass(h, x, ld_x, N, batch, layer_sq, ld_sq, ws, ws_bytes, st));
+  if (!h->gstream) MMAD_HIP_CHECK(hipStreamCreateWithFlags(&h->gstream, hipStreamNonBlocking));
+  hipGraph_t graph = nullptr;
+  MMAD_HIP_CHECK(hipStreamBeginCapture(h->gstream, hipStreamCaptureModeThreadLocal));
+  const int rc = score_pass(h, x, ld_x, N, batch, layer_sq, ld_sq, ws, ws_bytes, h->gstream);
+  const hipError_t ec = hipStreamEndCapture(h->gstream, &graph);
+  if (rc != MMAD_OK) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return rc;
+  }
+  MMAD_HIP_CHECK(ec);
+  hipGraphExec_t exec = nullptr;
+  const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  MMAD_HIP_CHECK(ei);
+  if (h->graphs.size() >= 8) {   // bounded cache: drop the oldest pass
+    (void)hipGraphExecDestroy(h->graphs.front().exec);
+    h->graphs.erase(h->graphs.begin());
+  }
+  h->graphs.push_back({x, ld_x, N, batch, layer_sq, ld_sq, ws, weights(h, h->L[0]), exec});
+  return MMAD_OK;
+}
+
+int mmad_ae_graph_count(const mmad_ae* h) { return h ? (int)h->graphs.size() : -1; }
+
+int mmad_ae_clear_graphs(mmad_ae* h) {
+  MMAD_CHECK_ARG(h, "ae_clear_graphs: null handle");
+  for (auto& g : h->graphs) (void)hipGraphExecDestroy(g.exec);
+  h->graphs.clear();
+  return MMAD_OK;
 }

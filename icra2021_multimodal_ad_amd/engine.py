@@ -271,6 +271,23 @@ class NativeAE:
              stream_ptr())
         return lsq, diffs
 
+    def score_stream(self, x, batch, out, graph=True):
+        """Whole-dataset scoring pass (mmad_ae_score_stream): x [N, D] fp32 on
+        this device, out [n_enc+1, >=N] fp32 with unit column stride.  With
+        graph=True the pass is captured once and replayed as one hipGraph."""
+        self._require(x)
+        x = self._as_input(x, self.enc_widths[0])
+        N = x.shape[0]
+        if out.device != self.device or out.dtype != torch.float32 or out.stride(1) != 1 \
+                or out.shape[0] != self.n_enc + 1 or out.shape[1] < N:
+            raise ValueError("score_stream: out must be fp32 [n_enc+1, >=N] on the model device")
+        self.sync_shadow()
+        B = min(int(batch), N)
+        ws, nb = self.workspace(B, 1)
+        call("mmad_ae_score_stream", self._h, ptr(x), x.stride(0), N, B, ptr(out), out.stride(0),
+             ws, nb, 1 if graph else 0, stream_ptr())
+        return out
+
     def diff_widths(self):
         return [self.enc_widths[0]] + self.enc_widths[1:]
 

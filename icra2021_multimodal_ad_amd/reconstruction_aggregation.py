@@ -34,9 +34,11 @@ def get_diffs(x, model, batch_size=698):
     return [np.concatenate(o, axis=0) for o in out]
 
 
-def score_windows(x, model, batch_size=16384, out=None):
+def score_windows(x, model, batch_size=16384, out=None, graph=True):
     """Per-window sum of squared diffs per layer, [n_enc+1, N] fp32 on the
-    device.  x: [N, D] tensor (any device; streamed in batches)."""
+    device.  x: [N, D] tensor.  Resident on the model's device: ONE native call
+    for the whole pass (mmad_ae_score_stream), replayed as a captured hipGraph
+    from the second call on (graph=True); elsewhere: streamed in batches."""
     model.eval()
     dev = _device_of(model)
     n = x.shape[0]
@@ -44,6 +46,9 @@ def score_windows(x, model, batch_size=16384, out=None):
     if out is None:
         out = torch.empty((nl, n), device=dev)
     with torch.no_grad():
+        if x.device == dev and x.dtype == torch.float32 and x.dim() == 2 and x.stride(1) == 1 \
+                and out.stride(1) == 1:
+            return model._native.score_stream(x, batch_size, out, graph=graph)
         for s in range(0, n, batch_size):
             xb = x[s:s + batch_size].to(dev, non_blocking=True)
             lsq, _ = model._native.score(xb)

@@ -304,6 +304,24 @@ int mmad_ae_forward(mmad_ae* h, const float* x, int ld_x, int B, int train_bn, f
 int mmad_ae_score(mmad_ae* h, const float* x, int ld_x, int B, float* layer_sq, float* diffs,
                   void* ws, int64_t ws_bytes, void* stream);
 
+/* Streaming scoring pass (NoveltyDetecter.test -> get_diffs over a whole
+ * dataset, novelty_detection.py:15-38 / reconstruction_aggregation.py:6-37,
+ * BASELINE config C5): x fp32 [N][ld_x] in device memory, scored in batches of
+ * `batch` windows (the last one ragged); layer_sq fp32, row l at
+ * layer_sq + l*ld_sq (ld_sq >= N), same values as mmad_ae_score per batch.
+ * ws sized by mmad_ae_workspace_bytes(h, batch, 1).
+ * use_graph != 0: the first call for a given (x, ld_x, N, batch, layer_sq,
+ * ld_sq, ws, weight buffer) runs eagerly and captures the pass as one hipGraph;
+ * later calls replay it with a single hipGraphLaunch on `stream` (up to 8
+ * passes cached per handle; weights and BN running statistics are read at
+ * replay time, so training in between is seen). */
+int mmad_ae_score_stream(mmad_ae* h, const float* x, int ld_x, int64_t N, int batch,
+                         float* layer_sq, int64_t ld_sq, void* ws, int64_t ws_bytes, int use_graph,
+                         void* stream);
+/* number of cached score graphs (-1 for a null handle); drop them all */
+int mmad_ae_graph_count(const mmad_ae* h);
+int mmad_ae_clear_graphs(mmad_ae* h);
+
 #ifdef __cplusplus
 }
 #endif

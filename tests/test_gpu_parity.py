@@ -364,3 +364,52 @@ def test_nap_run_native_matches_reference_fit(golden):
     nap2.fit(train_diffs=torch.from_numpy(g["train"]))
     got2 = nap2.score(torch.from_numpy(g["test"])).cpu().numpy()
     assert _rel(got2, g["score"]) < 1e-3
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_score_stream_graph_matches_per_batch(golden, dtype):
+    """mmad_ae_score_stream (BASELINE C5 streaming pass, hipGraph replay) ==
+    per-batch mmad_ae_score bit for bit, ragged last batch included; a replay
+    after a train step sees the new weights and BN running statistics; fp32
+    scores match the reference's golden BASE/SAP."""
+    from icra2021_multimodal_ad_amd.reconstruction_aggregation import (
+        score_windows, base_from_layer_sq, sap_from_layer_sq)
+    g = golden("mm192")
+    d, btl, nl = int(g["meta_d"]), int(g["meta_btl"]), int(g["meta_n_layers"])
+    steps = int(g["meta_steps"])
+    m, _ = _model(d, btl, nl, _sd(g, f"after{steps - 1}/"), dtype=dtype)
+    nat = m._native
+    x = torch.from_numpy(g["score/test_x"]).cuda()
+    n, bs = x.shape[0], 48          # ragged: n is not a multiple of 48
+
+    def per_batch():
+        m.eval()
+        parts = [nat.score(x[s:s + bs])[0] for s in range(0, n, bs)]
+        return torch.cat(parts, dim=1)
+
+    out = torch.full((nat.n_enc + 1, n + 5), float("nan"), device="cuda")
+    eager = score_windows(x, m, batch_size=bs, out=out[:, :n], graph=False).clone()
+    ref = per_batch()
+    assert torch.equal(eager, ref)
+    assert nat._lib.mmad_ae_graph_count(nat._h) == 0
+    first = score_windows(x, m, batch_size=bs, out=out[:, :n]).clone()   # eager + capture
+    assert nat._lib.mmad_ae_graph_count(nat._h) == 1
+    out[:, :n].fill_(float("nan"))
+    replay = score_windows(x, m, batch_size=bs, out=out[:, :n]).clone()
+    assert nat._lib.mmad_ae_graph_count(nat._h) == 1
+    assert torch.equal(first, ref) and torch.equal(replay, ref)
+    assert torch.isnan(out[:, n:]).all()          # nothing written past N
+    if dtype == "f32":
+        widths = nat.diff_widths()
+        lsq = replay.cpu().numpy()
+        assert _rel(base_from_layer_sq(lsq, widths), g["score/base"]) < 1e-4
+        assert _rel(sap_from_layer_sq(lsq, widths), g["score/sap"]) < 1e-4
+    # train in between: the captured pass reads the updated weights/BN stats
+    m.train()
+    m.train_step_async(x[:64])
+    ref2 = per_batch()
+    assert not torch.equal(ref2, ref)
+    again = score_windows(x, m, batch_size=bs, out=out[:, :n]).clone()
+    assert torch.equal(again, ref2)
+    assert nat._lib.mmad_ae_clear_graphs(nat._h) == 0
+    assert nat._lib.mmad_ae_graph_count(nat._h) == 0
