@@ -61,6 +61,13 @@ static int g_tile_adam = [] {
   return e ? atoi(e) : 3;
 }();
 int mmad_tile_adam_override() { return g_tile_adam; }
+// tile of the Adam-fused dW GEMMs that run on the main stream at the end of
+// the backward (nothing else on the GPU then; -1 = same as knob 5)
+static int g_tile_adam_main = [] {
+  const char* e = getenv("MMAD_GEMM_TILE_ADAM_MAIN");
+  return e ? atoi(e) : -1;
+}();
+int mmad_tile_adam_main_override() { return g_tile_adam_main; }
 // per-epilogue tile overrides (-1 = autotuned): bwd-data GEMMs, forward GEMMs
 static int g_tile_bwd_data = [] {
   const char* e = getenv("MMAD_GEMM_TILE_BWD_DATA");
@@ -86,6 +93,7 @@ int mmad_tune_set(int knob, int value) {
     case 5: g_tile_adam = value; return MMAD_OK;
     case 6: g_tile_bwd_data = value; return MMAD_OK;
     case 7: g_tile_fwd = value; return MMAD_OK;
+    case 8: g_tile_adam_main = value; return MMAD_OK;
     default: mmad_set_error("tune_set: unknown knob %d", knob); return MMAD_EINVAL;
   }
 }

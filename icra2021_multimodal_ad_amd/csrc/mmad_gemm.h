@@ -73,6 +73,7 @@ struct GemmEpi {
   // set by the launcher: split factor, XCD-aware grouped tile order
   int splitk;
   int tiles_n, group_m;
+  int tile_force;        // caller's tile choice + 1 (0 = none; ignored if it does not fit)
   int dbg;               // diagnostics (tools/gemm_sweep): 1 skip main loop, 2 skip epilogue
 };
 
@@ -83,6 +84,7 @@ int mmad_autotune_enabled();
 int mmad_dbg_override();
 int mmad_splitk_override();   // 0 = shape rule; 1, 2, 4 = forced split factor
 int mmad_tile_adam_override();  // >= 0: tile of the Adam-fused dW GEMMs
+int mmad_tile_adam_main_override();  // >= 0: ... of those on the main stream
 int mmad_tile_epi_override(int epi);  // >= 0: tile of this epilogue's GEMMs
 
 // tile configuration a problem will run with (autotuned on first dispatch of

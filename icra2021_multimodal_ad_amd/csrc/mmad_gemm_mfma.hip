@@ -1006,7 +1006,10 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   const int env = mmad_tile_override();
   const int env_epi = ep.ad_p ? mmad_tile_adam_override() : mmad_tile_epi_override(epi);
   int cfg;
-  if (env_epi >= 0 && env_epi < NCFG && cfg_fits(env_epi, Mp, Np, epi)) {
+  const int force = ep.tile_force - 1;
+  if (force >= 0 && force < NCFG && cfg_fits(force, Mp, Np, epi)) {
+    cfg = force;
+  } else if (env_epi >= 0 && env_epi < NCFG && cfg_fits(env_epi, Mp, Np, epi)) {
     cfg = env_epi;
   } else if (env >= 0 && env < NCFG && cfg_fits(env, Mp, Np, epi)) {
     cfg = env;   // forced tile (tuning / tests); a shape it does not fit falls through

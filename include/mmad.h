@@ -52,10 +52,11 @@ int mmad_pad_granule(void);
  * factor override for GEMMs given split-K workspace (0 = shape rule, 1/2/4),
  * knob 5 = tile of the dW GEMMs with the fused Adam epilogue (default 3 =
  * 64x64; -1 = autotuned like the others), knobs 6 / 7 = tile of the bwd-data /
- * forward GEMMs (-1 = autotuned).
+ * forward GEMMs (-1 = autotuned), knob 8 = tile of the Adam-fused dW GEMMs
+ * run on the main stream at the end of the backward (-1 = knob 5).
  * Defaults from MMAD_GEMM_TILE / MMAD_GEMM_GROUP_M / MMAD_GEMM_AUTOTUNE /
  * MMAD_GEMM_SPLITK / MMAD_GEMM_TILE_ADAM / MMAD_GEMM_TILE_BWD_DATA /
- * MMAD_GEMM_TILE_FWD. */
+ * MMAD_GEMM_TILE_FWD / MMAD_GEMM_TILE_ADAM_MAIN. */
 int mmad_tune_set(int knob, int value);
 
 /* ------------------------------------------------------------------------

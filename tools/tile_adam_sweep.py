@@ -1,6 +1,7 @@
 """Step time of the fused train step with one GEMM class forced to each tile
 config: knob 5 = Adam-fused dW GEMMs (default 3), 6 = bwd-data GEMMs, 7 =
-forward GEMMs (-1 = autotuned in isolation).
+forward GEMMs (-1 = autotuned in isolation), 8 = Adam-fused dW GEMMs on the
+main stream (-1 = knob 5).
 Usage: python tools/tile_adam_sweep.py [knobs=5,6,7] [dim=2048] [batch=1024] [steps=300]"""
 import sys
 import time
@@ -17,7 +18,7 @@ knobs = [int(k) for k in (sys.argv[1] if len(sys.argv) > 1 else "5,6,7").split("
 dim = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
 B = int(sys.argv[3]) if len(sys.argv) > 3 else 1024
 steps = int(sys.argv[4]) if len(sys.argv) > 4 else 300
-DEFAULT = {5: 3, 6: -1, 7: -1}
+DEFAULT = {5: 3, 6: -1, 7: -1, 8: -1}
 dev = torch.device("cuda", 0)
 lib = _native.load()
 pool = [synth_windows_device(B, dim, dev, seed=100 + i) for i in range(8)]
