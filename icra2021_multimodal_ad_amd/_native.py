@@ -74,6 +74,8 @@ SIGNATURES = {
     "mmad_comm_destroy": (None, [_P]),
     "mmad_allreduce_bucket": (_I, [_P, _P, _I64, _P]),
     "mmad_ae_set_comm": (_I, [_P, _P]),
+    "mmad_hsr_weight_count": (_I, []),
+    "mmad_hsr_fuse": (_I, [_I, _P, _P, _P, _P, _P, _I, _P, _I, _P]),
 }
 
 

@@ -323,6 +323,22 @@ int mmad_ae_score_stream(mmad_ae* h, const float* x, int ld_x, int64_t N, int ba
 int mmad_ae_graph_count(const mmad_ae* h);
 int mmad_ae_clear_graphs(mmad_ae* h);
 
+/* HSR_Net multimodal fusion producer (utils/data_loaders.py:152-229; replaces
+ * the per-window loop HSR_Net.forward :179-229 that TabularDataset runs at
+ * :400-424).  One call fuses n windows.  Inputs fp32 device rows, each
+ * nullable: r [n][3*32*32] (hand RGB), d [n][32*32] (head depth), t [n] (F/T
+ * scalar), m [n][13] (MFCCs).  weights: fp32 [mmad_hsr_weight_count()] packed
+ * conv1r w,b | conv2r | conv3r | conv1d | conv2d | conv3d | conv1l | conv2l
+ * (torch layouts [co][ci][k..]).  unimodal == 0: r, d, t, m all required, row =
+ * channel-major [27][8][8] = rgb 1024 | depth 512 | F/T 64 | mic 128 (1728);
+ * unimodal != 0: the block of the last non-null modality of (r, d, t, m)
+ * alone, as the reference keeps (:190-221).  out fp32 [n][ld_out]; columns
+ * past the row width are not written.  The LiDAR branch (l) is never fed by
+ * the reference and has no entry point. */
+int mmad_hsr_weight_count(void);
+int mmad_hsr_fuse(int n, const float* r, const float* d, const float* t, const float* m,
+                  const float* weights, int unimodal, float* out, int ld_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,6 +11,7 @@ import sqlite3
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*", "", name) if not name.startswith("void at::") else name[:60]
     m = re.match(r"_Z\d+(\w+?)I(.*)E(v|S)", name)
     return name[:110]
