@@ -1,15 +1,33 @@
 """Benchmark: sensor-windows/sec of the AE train step (fwd + sum-MSE + bwd +
-Adam) on synthetic 4-modal windows -- BASELINE.json configs[1]: D=2048,
-batch=1024 per GPU, bf16 storage / fp32 accumulate, 1..8 MI355X (weak scaling,
-per-layer RCCL all-reduce of the gradients overlapped with the backward).
+Adam) on synthetic 4-modal windows, 1..8 MI355X (BASELINE.json metric).
 
-Prints ONE JSON line (rank 0) with the driver's fields plus ``roofline`` (the
-encoder's first GEMM, the dominant kernel, timed with a HIP event pair around
-back-to-back launches on the stream it runs on; HBM traffic from the newest
-profiles/*_pmc_traffic.json) and ``cpu_baseline`` (the oracle's numpy fp32 train step on
-host cores, bounded sample).
+Workloads (``--config``; ``auto`` = c2 on one GPU, c4 on several):
+  c2  BASELINE configs[1]: FC-AE, D=2048, 1024 windows, bf16, 1 GPU
+  c3  BASELINE configs[2]: VIB-AE (k=1, beta_kl=1), D=2048, 4096 windows, bf16
+  c4  BASELINE configs[3]: the c3 model, 4096 windows PER GPU (global 4096*N),
+      one process per GPU, per-layer RCCL all-reduce of the gradients over xGMI
+      overlapped with the backward (weak scaling)
+``--model/--dim/--batch`` override the chosen config's fields.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--dim 2048] [--batch 1024]
+``python bench.py --gpus N`` without torchrun env vars spawns the N ranks itself
+(torch.multiprocessing, before any GPU call); under torchrun it reads
+RANK/WORLD_SIZE/LOCAL_RANK.  W untimed steps, then K timed steps between
+barrier + synchronize pairs, the max over ranks; rank 0 prints ONE JSON line:
+
+* ``roofline``: the kernel that dominates the step -- the dW GEMM with the
+  fused Adam epilogue of the largest layer, HBM-bound (26 B of Adam state per
+  parameter + its two bf16 operands).  Its duration is measured IN the timed
+  region by the executor's probe (mmad_ae_probe: a HIP event pair around that
+  one launch, on the stream it runs on); ``traffic`` = PMC HBM bytes per launch
+  from the newest matching profiles/*_pmc_dw.json.
+* ``roofline_encoder_gemm``: the encoder's first forward GEMM (the north-star
+  MFMA target), launched back to back between one event pair.
+* ``cpu_baseline`` (rank 0, N=1): the torch-CPU fp32 restatement of the
+  reference's modules (oracle/torch_ref.py) timed on this host's cores on a
+  bounded sample of the same workload.
+* N>1: ``n1_same_workload`` = the same ranks' windows/s per GPU with the
+  exchange switched off (same process, after the timed region), so scaling
+  can be read against the same workload.
 """
 import argparse
 import json
@@ -22,6 +40,13 @@ sys.path.insert(0, REPO)
 
 BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 F32_PEAK_TFLOPS = 157.3     # f32 MFMA = vector rate
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    "c2": dict(model="ae", dim=2048, batch=1024, name="BASELINE configs[1]"),
+    "c3": dict(model="vib_ae", dim=2048, batch=4096, name="BASELINE configs[2]"),
+    "c4": dict(model="vib_ae", dim=2048, batch=4096, name="BASELINE configs[3]"),
+}
 
 
 def ae_flops_per_window(widths_enc, widths_dec):
@@ -30,37 +55,75 @@ def ae_flops_per_window(widths_enc, widths_dec):
     return 6.0 * macs, macs   # fwd 2*MAC + bwd-data 2*MAC + bwd-weight 2*MAC
 
 
-def cpu_baseline(d, batch, budget_s=12.0, threads=16):
-    """Oracle (numpy fp32) train step timed on host cores: a bounded sample of
-    the same workload (whole steps at the same D and batch)."""
-    import numpy as np
-    from threadpoolctl import threadpool_limits
-    from oracle import ae_oracle as O
-    from oracle.model_io import model_from_state_dict
-    from icra2021_multimodal_ad_amd.common_utils import init_state_dict
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(d, batch, vib, budget_s=12.0):
+    """The reference's modules in torch-CPU fp32 (oracle/torch_ref.py): whole
+    train steps (fwd + loss + bwd + Adam) at the same D and batch, timed on
+    this host's cores for a bounded sample."""
+    import torch
+    from oracle import torch_ref
+    from icra2021_multimodal_ad_amd.common_utils import init_state_dict, ae_widths
     from icra2021_multimodal_ad_amd.data import synth_windows
-    threads = min(threads, os.cpu_count() or 1)
-    model = model_from_state_dict(init_state_dict(d, 100, 5, seed=0))
-    x = synth_windows(batch, d, seed=1)
-    st = {}
-    with threadpool_limits(limits=threads):
-        O.train_step(x, model, st)            # warm-up
-        n, t0 = 0, time.perf_counter()
-        while True:
-            O.train_step(x, model, st)
-            n += 1
-            el = time.perf_counter() - t0
-            if el > budget_s or n >= 50:
-                break
-    return {"value": n * batch / el, "unit": "sensor-windows/sec", "cores": threads,
-            "kind": "port",
-            "sample": f"{n} oracle train steps (numpy fp32 fwd+bwd+Adam) at D={d}, batch={batch}, "
-                      f"{el:.1f} s, BLAS threads={threads}"}
+    threads = torch.get_num_threads()
+    enc_out = 200 if vib else None
+    enc, dec = ae_widths(d, 100, 5, enc_out=enc_out)
+    sd = init_state_dict(d, 100, 5, seed=0, enc_out=enc_out)
+    m = torch_ref.build(sd, enc, dec, vib=vib)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    x = torch.from_numpy(synth_windows(batch, d, seed=1))
+    torch_ref.train_step(m, opt, x)            # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        torch_ref.train_step(m, opt, x)
+        n += 1
+        el = time.perf_counter() - t0
+        if el > budget_s or n >= 200:
+            break
+    return {"value": round(n * batch / el, 1), "unit": "sensor-windows/sec", "cores": threads,
+            "kind": "port", "cpu": cpu_model(),
+            "sample": f"{n} train steps of the reference's modules in torch-CPU fp32 "
+                      f"(nn.Linear/LeakyReLU/BatchNorm1d, MSELoss(sum), optim.Adam; "
+                      f"oracle/torch_ref.py{', VIB-AE' if vib else ''}) at D={d}, batch={batch}, "
+                      f"{el:.1f} s, torch threads={threads}"}
+
+
+def dw_adam_bytes(N, K, B, es=2):
+    """Algorithmic HBM bytes of one dW GEMM with the fused Adam epilogue:
+    fp32 p/m/v read + written (24 B/param) + the bf16 weight shadow written
+    (2 B/param) + the two operands dz [B x N] and a [B x K] read once."""
+    return 26 * N * K + es * B * (N + K)
+
+
+def pick_dominant_layer(nat):
+    """Largest parameter count (ties: the first, encoder layer 1)."""
+    best = max(range(len(nat.layers)), key=lambda l: (nat.layers[l]["N"] * nat.layers[l]["K"], -l))
+    return best
+
+
+def _pmc_file(kind, workload):
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", f"*_pmc_{kind}.json")))[::-1]:
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload:
+            return d, os.path.relpath(f, REPO)
+    return None, None
 
 
 def gemm_roofline(model, batch, iters=50):
-    """Average duration of the encoder's first-layer forward GEMM (the largest
-    MFMA kernel of the step) from HIP events on the launch stream."""
+    """Average duration of the encoder's first-layer forward GEMM from HIP
+    events on the launch stream (back-to-back launches between one pair)."""
     import torch
     from icra2021_multimodal_ad_amd import _native
     from icra2021_multimodal_ad_amd._native import call, ptr, stream_ptr
@@ -76,17 +139,12 @@ def gemm_roofline(model, batch, iters=50):
     w = nat.shadow[L["w_off"]:] if nat.shadow is not None else nat.params[L["w_off"]:]
     b = nat.params[L["b_off"]:]
     s = stream_ptr()
-    _native.enable_gemm_workspace(dev)   # split-K workspace, as the executor's GEMMs have
 
     def launch():
         call("mmad_fc_fwd", dt, batch, L["N"], L["K"], Mp, L["Np"], L["Kp"], ptr(xin), ptr(w), ptr(b),
              1, 0.2, None, None, ptr(out), ptr(stats), s)
     for _ in range(5):
         launch()
-    # one event pair on the launch stream around `iters` back-to-back launches
-    # (the queue stays full, so this is the kernel duration plus the GPU's
-    # dispatch gap; an event pair per launch adds ~2 us of event overhead and
-    # disagrees with rocprofv3's kernel-trace average)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(iters):
@@ -97,69 +155,110 @@ def gemm_roofline(model, batch, iters=50):
     flops = 2.0 * batch * L["K"] * L["N"]
     peak = BF16_PEAK_TFLOPS if dt == _native.BF16 else F32_PEAK_TFLOPS
     ach = flops / avg_s / 1e12
+    wl = {"dim": L["K"], "batch": batch, "dtype": nat.dtype_name}
+    pmc, src = _pmc_file("traffic", wl)
     return {"kernel": f"mmad_gemm_kernel fwd (encoder layer 1: {batch}x{L['K']} . {L['N']}x{L['K']}^T,"
                       f" bias+LeakyReLU+BN-stat epilogue)",
             "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(ach / peak, 4), "traffic": _pmc_traffic(L["K"], batch, dt),
-            "avg_us": round(avg_s * 1e6, 2), "flops_per_launch": flops}
+            "frac": round(ach / peak, 4),
+            "traffic": pmc["traffic_bytes_per_launch"] if pmc else None,
+            "traffic_source": src, "avg_us": round(avg_s * 1e6, 2), "flops_per_launch": flops,
+            "timing": f"{iters} back-to-back launches between one HIP event pair"}
 
 
-def _pmc_traffic(dim, batch, dt):
-    """HBM-side bytes per launch of the roofline kernel from the committed
-    rocprofv3 PMC passes (newest profiles/*_pmc_traffic.json: FETCH_SIZE x2 +
-    WRITE_SIZE, gfx950 correction) when they were taken at this workload."""
-    import glob
-    from icra2021_multimodal_ad_amd import _native
-    for f in sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                                           "*_pmc_traffic.json")))[::-1]:
-        try:
-            d = json.load(open(f))
-        except (OSError, ValueError):
-            continue
-        w = d.get("workload", {})
-        if (w.get("dim"), w.get("batch"), w.get("dtype")) == (dim, batch,
-                                                             "bf16" if dt == _native.BF16 else "f32"):
-            return d["traffic_bytes_per_launch"]
-    return None
+def dw_roofline(nat, layer, durations_ms, batch, steps_timed, fused_adam=True):
+    """roofline of the dominant dW GEMM from the in-situ probe durations."""
+    import statistics
+    L = nat.layers[layer]
+    rows = batch                      # k = 1: decoder rows = encoder rows
+    es = 2 if nat.dtype_name == "bf16" else 4
+    if fused_adam:
+        nbytes = dw_adam_bytes(L["N"], L["K"], rows, es)
+        what = "bwd-weight + fused Adam"
+        body = "p/m/v fp32 + bf16 shadow updated in the epilogue"
+    else:
+        nbytes = 4 * L["N"] * L["K"] + es * rows * (L["N"] + L["K"])
+        what = "bwd-weight"
+        body = "fp32 dW written for the all-reduce; Adam runs after the exchange"
+    avg_s = statistics.fmean(durations_ms) / 1e3
+    ach = nbytes / avg_s / 1e9
+    wl = {"dim": nat.enc_widths[0], "batch": batch, "dtype": nat.dtype_name,
+          "model": "vib_ae" if nat.vib else "ae", "layer": layer}
+    pmc, src = _pmc_file("dw", wl)
+    return {"kernel": f"mmad_gemm_kernel {what} (layer {layer}: dW[{L['N']}x{L['K']}] = "
+                      f"dz^T a over {rows} windows; {body})",
+            "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": pmc["traffic_bytes_per_launch"] if pmc else None,
+            "traffic_source": src,
+            "avg_us": round(avg_s * 1e6, 2), "launches_timed": len(durations_ms),
+            "algorithmic_bytes_per_launch": nbytes,
+            "flops_per_launch": 2.0 * rows * L["N"] * L["K"],
+            "timing": f"executor probe: HIP event pair around this launch on its stream, "
+                      f"every one of the {steps_timed} timed steps"}
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--dim", type=int, default=2048)
-    ap.add_argument("--batch", type=int, default=1024, help="windows per GPU per step")
+    ap.add_argument("--config", default="auto", choices=["auto"] + sorted(CONFIGS))
+    ap.add_argument("--model", choices=["ae", "vib_ae"])
+    ap.add_argument("--dim", type=int)
+    ap.add_argument("--batch", type=int, help="windows per GPU per step")
     ap.add_argument("--dtype", default="bf16")
-    ap.add_argument("--model", default="ae", choices=["ae", "vib_ae"],
-                    help="vib_ae: BASELINE config C3/C4 (VIB head, k=1, beta_kl=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    args = ap.parse_args()
+    ap.add_argument("--no-probe", action="store_true", help="skip the in-situ kernel probe")
+    return ap.parse_args(argv)
 
+
+def _spawn_entry(rank, world, port, argv):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run(parse_args(argv))
+
+
+def run(args):
+    import types
     import torch
     import torch.distributed as dist
     from icra2021_multimodal_ad_amd import dist as mdist
+    from icra2021_multimodal_ad_amd import _native
     from icra2021_multimodal_ad_amd.model_builder import get_model
     from icra2021_multimodal_ad_amd.data import synth_windows_device
-    import types
 
+    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     rank, world, local = mdist.init_from_env()
+    cname = args.config if args.config != "auto" else ("c2" if world == 1 else "c4")
+    cfgd = dict(CONFIGS[cname])
+    for k in ("model", "dim", "batch"):
+        if getattr(args, k) is not None:
+            cfgd[k] = getattr(args, k)
+    model_name, dim, batch = cfgd["model"], cfgd["dim"], cfgd["batch"]
+    vib = model_name == "vib_ae"
     torch.cuda.set_device(local)
-    cfg = types.SimpleNamespace(input_size=args.dim, btl_size=100, n_layers=5, gpu_id=local,
-                                dtype=args.dtype, models=args.model, vib_k=1, beta_kl=1.0)
+    cfg = types.SimpleNamespace(input_size=dim, btl_size=100, n_layers=5, gpu_id=local,
+                                dtype=args.dtype, models=model_name, vib_k=1, beta_kl=1.0)
     torch.manual_seed(0)
     model = get_model(cfg)
     mdist.attach_data_parallel(model)
     model._native.sync_shadow(force=True)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     dev = torch.device("cuda", local)
+    nat = model._native
     # a pool of distinct synthetic batches resident in HBM before timing
-    pool = [synth_windows_device(args.batch, args.dim, dev, seed=1000 * rank + i) for i in range(8)]
+    pool = [synth_windows_device(batch, dim, dev, seed=1000 * rank + i) for i in range(8)]
 
     for i in range(args.warmup):
         model.train_step_async(pool[i % len(pool)], opt)
     torch.cuda.synchronize()
+    probe_layer = pick_dominant_layer(nat)
+    lib = _native.load()
+    probing = not args.no_probe and rank == 0
+    if probing:
+        _native.check(lib.mmad_ae_probe(nat._h, 1, probe_layer, args.steps), "mmad_ae_probe")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -171,16 +270,27 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    durs = []
+    if probing:
+        import ctypes
+        buf = (ctypes.c_float * args.steps)()
+        n = lib.mmad_ae_probe_read(nat._h, buf, args.steps)
+        if n < 0:
+            _native.check(n, "mmad_ae_probe_read")
+        durs = list(buf[:n])
+        _native.check(lib.mmad_ae_probe(nat._h, 1, -1, 0), "mmad_ae_probe")
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     loss_v = float(loss.item())
 
-    nat = model._native
     fpw, _ = ae_flops_per_window(nat.enc_widths, nat.dec_widths)
-    windows = args.steps * args.batch * world
+    windows = args.steps * batch * world
     value = windows / el
+    exchange = ("native RCCL per-layer buckets overlapped with backward"
+                if model.dist is not None and model.dist.native else
+                ("torch.distributed flat all-reduce" if world > 1 else "none"))
     res = {
         "metric": "sensor-windows/sec (train fwd+bwd)",
         "value": round(value, 1),
@@ -194,29 +304,70 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (seeded 4-modal window generator, random-init weights)",
-        "config": {"workload": f"{'VIB-AE' if args.model == 'vib_ae' else 'FC-AE'} train step "
-                               f"(fwd+sum-MSE{'+KL' if args.model == 'vib_ae' else ''}+bwd+Adam), "
-                               f"D={args.dim}, btl=100, "
-                               f"n_layers=5, {args.batch} windows/GPU",
-                   "global_batch": args.batch * world, "input_dim": args.dim,
-                   "parallelism": f"dp{world}",
-                   "exchange": ("native RCCL per-layer buckets overlapped with backward"
-                                if model.dist is not None and model.dist.native else
-                                ("torch.distributed flat all-reduce" if world > 1 else "none"))},
+        "config": {"workload": f"{cname} ({cfgd['name']}): "
+                               f"{'VIB-AE (k=1, beta_kl=1)' if vib else 'FC-AE'} train step "
+                               f"(fwd+sum-MSE{'+KL' if vib else ''}+bwd+Adam), D={dim}, btl=100, "
+                               f"n_layers=5, {batch} windows/GPU",
+                   "global_batch": batch * world, "input_dim": dim,
+                   "parallelism": f"dp{world}", "exchange": exchange},
         "model_tflops": round(value * fpw / 1e12, 2),
         "final_loss": loss_v,
     }
+    if world > 1:
+        # same workload without the exchange, same ranks (read scaling against it)
+        mdl_dist = model.dist
+        model.dist = None
+        if mdl_dist is not None and mdl_dist.native:
+            nat.set_comm(None)
+        for i in range(5):
+            model.train_step_async(pool[i % len(pool)], opt)
+        torch.cuda.synchronize()
+        n1 = max(10, args.steps // 2)
+        t1 = time.perf_counter()
+        for i in range(n1):
+            model.train_step_async(pool[i % len(pool)], opt)
+        torch.cuda.synchronize()
+        e1 = time.perf_counter() - t1
+        t = torch.tensor([e1], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        e1 = float(t.item())
+        res["n1_same_workload"] = {"value": round(n1 * batch / e1, 1), "unit": "sensor-windows/sec per GPU",
+                                   "ms_per_step": round(e1 / n1 * 1e3, 4), "steps": n1,
+                                   "how": "same ranks, exchange off, after the timed region (max over ranks)"}
+        model.dist = mdl_dist
     if rank == 0:
-        res["roofline"] = gemm_roofline(model, args.batch)
+        if durs:
+            fused = model.dist is None or not model.dist.native
+            res["roofline"] = dw_roofline(nat, probe_layer, durs, batch, args.steps, fused_adam=fused)
+        res["roofline_encoder_gemm"] = gemm_roofline(model, batch)
         if not args.no_cpu_baseline and world == 1:   # host baseline: rank 0 at N=1 only
-            res["cpu_baseline"] = cpu_baseline(args.dim, args.batch, budget_s=args.cpu_budget)
+            res["cpu_baseline"] = cpu_baseline(dim, batch, vib, budget_s=args.cpu_budget)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()
         if model.dist is not None and model.dist.native:
-            model._native.set_comm(None)
+            nat.set_comm(None)
             model.dist.close()
         dist.destroy_process_group()
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # spawn the ranks here (no GPU has been touched in this process)
+        import socket
+        import torch.multiprocessing as mp
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        mp.start_processes(_spawn_entry, args=(args.gpus, port, sys.argv[1:]), nprocs=args.gpus,
+                           join=True, start_method="spawn")
+        return
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}; "
+              f"using WORLD_SIZE", file=sys.stderr)
+    run(args)
 
 
 if __name__ == "__main__":

@@ -11,6 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MMAD_LIB", os.path.join(HERE, "libmmad.so"))
 
 MMAD_OK = 0
+MMAD_EINVAL, MMAD_EUNSUPPORTED, MMAD_EHIP, MMAD_ERCCL = -1, -2, -3, -4
 F32, BF16 = 0, 1
 ACT = {None: 0, "leakyrelu": 1, "relu": 2, "sigmoid": 3, "tanh": 4}
 
@@ -28,6 +29,7 @@ SIGNATURES = {
     "mmad_tune_set": (_I, [_I, _I]),
     "mmad_gemm_ws_bytes": (ctypes.c_size_t, []),
     "mmad_gemm_set_workspace": (_I, [_P, ctypes.c_size_t]),
+    "mmad_gemm_status": (_I, [_P]),
     "mmad_fc_fwd": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P, _P, _P, _P, _P]),
     "mmad_fc_fwd_mse": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _I, _F, _P, _P, _P]),
     "mmad_fc_fwd_score": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _I, _F, _P, _P, _P, _P,
@@ -65,6 +67,9 @@ SIGNATURES = {
     "mmad_ae_forward": (_I, [_P, _P, _I, _I, _I, _P, _I, _P, _P, _I64, _P]),
     "mmad_ae_score": (_I, [_P, _P, _I, _I, _P, _P, _P, _I64, _P]),
     "mmad_ae_score_stream": (_I, [_P, _P, _I, _I64, _I, _P, _I64, _P, _I64, _I, _P]),
+    "mmad_ae_status": (_I, [_P, _P, _I64, _P]),
+    "mmad_ae_probe": (_I, [_P, _I, _I, _I]),
+    "mmad_ae_probe_read": (_I, [_P, ctypes.POINTER(_F), _I]),
     "mmad_ae_graph_count": (_I, [_P]),
     "mmad_ae_clear_graphs": (_I, [_P]),
     "mmad_comm_unique_id_bytes": (_I, []),
@@ -74,6 +79,10 @@ SIGNATURES = {
     "mmad_comm_destroy": (None, [_P]),
     "mmad_allreduce_bucket": (_I, [_P, _P, _I64, _P]),
     "mmad_ae_set_comm": (_I, [_P, _P]),
+    "mmad_rank_metrics_ws_bytes": (ctypes.c_size_t, [_I64]),
+    "mmad_rank_metrics": (_I, [_I64, _P, _P, _P, _P, ctypes.c_size_t, _P]),
+    "mmad_threshold_metrics_ws_bytes": (ctypes.c_size_t, [_I64]),
+    "mmad_threshold_metrics": (_I, [_I64, _P, _I64, _P, _P, ctypes.c_double, _P, _P, ctypes.c_size_t, _P]),
     "mmad_hsr_weight_count": (_I, []),
     "mmad_hsr_fuse": (_I, [_I, _P, _P, _P, _P, _P, _I, _P, _I, _P]),
 }

@@ -49,13 +49,21 @@ class _AEFunction(torch.autograd.Function):
         model._count_bn_step()
         ctx.model = model
         ctx.B = x.shape[0]
+        ctx.gen = nat.gen
         return xh
 
     @staticmethod
     def backward(ctx, dxh):
         model = ctx.model
         nat = model._native
+        if nat.gen != ctx.gen:
+            # the saved activations live in the model's one workspace: any
+            # native call since this forward (another forward, validate,
+            # score, step) has overwritten them
+            raise RuntimeError("AutoEncoder backward: the model ran another native pass after this "
+                               "forward; call backward() before the next forward/validate/score")
         nat.backward(dxh.contiguous().float(), ctx.B)
+        nat.gen += 1          # the backward consumed (and overwrote) the saved activations
         grads = [g.clone() for g in model._grad_views()]
         return (None, None, *grads)
 
@@ -82,6 +90,7 @@ class AutoEncoder(AbstractModel):
         self._rng_offset = 0
         self.dist = None  # set by icra2021_multimodal_ad_amd.dist.attach_data_parallel
         self._adopt()
+        self._native.version_fn = self._param_version
 
     # ------------------------------------------------------------ plumbing
     def _layers(self):
@@ -137,6 +146,11 @@ class AutoEncoder(AbstractModel):
                 out += [layer.bn.weight, layer.bn.bias]
         return out
 
+    def _param_version(self):
+        """Sum of the version counters the fp32 master can be written through
+        (each nn.Parameter view has its own; the flat buffer has one more)."""
+        return sum(p._version for p in self._param_list()) + self._native.params._version
+
     def _count_bn_step(self):
         self._nbt_pending += 1
 
@@ -172,7 +186,10 @@ class AutoEncoder(AbstractModel):
 
     def load_state_dict(self, state_dict, strict=True, **kwargs):
         self._nbt_pending = 0
-        return super().load_state_dict(state_dict, strict=strict, **kwargs)
+        res = super().load_state_dict(state_dict, strict=strict, **kwargs)
+        # the bf16 weight shadow must follow the restored master at once
+        self._native.sync_shadow(force=True)
+        return res
 
     # ---------------------------------------------------- reference surface
     def encode(self, x):
@@ -285,7 +302,9 @@ class AutoEncoder(AbstractModel):
             x = x.cuda(engine.config.gpu_id)
         x = x.view(x.size(0), -1)
         loss = model.train_step_async(x, engine.optimizer)
-        return (float(loss),)
+        loss = float(loss)
+        model._native.check_status()
+        return (loss,)
 
     @staticmethod
     def validate(engine, mini_batch):
@@ -298,7 +317,9 @@ class AutoEncoder(AbstractModel):
                 x = x.cuda(engine.config.gpu_id)
             x = x.view(x.size(0), -1)
             _, loss = model._native.forward(x, train_bn=False, want_xhat=False, want_loss=True)
-        return (float(loss),)
+        loss = float(loss)
+        model._native.check_status()
+        return (loss,)
 
     @staticmethod
     def attach(trainer, evaluator, config):

@@ -99,7 +99,13 @@ struct mmad_ae {
   };
   std::vector<ScoreGraph> graphs;
   hipStream_t gstream = nullptr;   // capture stream (the caller's may be the null stream)
+  // kernel probe (mmad_ae_probe): timing events around ONE GEMM launch of
+  // the step, on the stream it is launched on (bench roofline, in situ)
+  mutable int probe_id = -1;
+  mutable int probe_n = 0;
+  std::vector<hipEvent_t> probe_ev;   // [2 * capacity]: start, end pairs
   ~mmad_ae() {
+    for (auto e : probe_ev) (void)hipEventDestroy(e);
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.exec);
     if (gstream) (void)hipStreamDestroy(gstream);
     for (auto e : ev_fork) (void)hipEventDestroy(e);
@@ -146,6 +152,17 @@ static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
     return p;
   };
   const size_t es = esz(h->dtype);
+  {
+    // split-K control words first: at a batch-independent offset, so
+    // mmad_ae_status can find them whatever batch the last call used
+    size_t slab = 0, ctl = 0;
+    mmad_gemm_splitk_bytes(0, 0, &slab, &ctl);
+    ctl = (ctl + 255) / 256 * 256;
+    w.sk_ctl_bytes = 2 * ctl;
+    char* c = take((int64_t)(2 * ctl));
+    w.sk_ctl[0] = (unsigned*)c;
+    w.sk_ctl[1] = c ? (unsigned*)(c + ctl) : nullptr;
+  }
   w.B = B;
   w.k = k;
   w.Mpe = mmad_roundup(B, MMAD_PAD);
@@ -167,11 +184,6 @@ static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
   {
     size_t slab = 0, ctl = 0;
     mmad_gemm_splitk_bytes(0, 0, &slab, &ctl);
-    ctl = (ctl + 255) / 256 * 256;
-    w.sk_ctl_bytes = 2 * ctl;
-    char* c = take((int64_t)(2 * ctl));
-    w.sk_ctl[0] = (unsigned*)c;
-    w.sk_ctl[1] = c ? (unsigned*)(c + ctl) : nullptr;
     w.sk_slab[0] = (float*)take((int64_t)slab);
     w.sk_slab[1] = (float*)take((int64_t)slab);
   }
@@ -377,14 +389,26 @@ static int prepare_ws(const mmad_ae* h, int B, int k, void* ws, int64_t ws_bytes
   return MMAD_OK;
 }
 
+// probe ids: PROBE_FWD + layer (forward / MSE / score GEMM of the layer),
+// PROBE_DW + layer (its dW GEMM, with the fused Adam in the fused step)
+enum { PROBE_FWD = 0, PROBE_DW = 64 };
+
 // GEMM dispatch with the split-K workspace of the stream it runs on
 static int ae_gemm(const mmad_ae* h, const AeWS& w, int dt, int epi, const void* A, int lda,
                    const void* B, int ldb, int Mp, int Np, int K, GemmEpi ep, hipStream_t s,
-                   int* cfg = nullptr) {
+                   int* cfg = nullptr, int probe = -1) {
   const int r = (h->side && s == h->side) ? 1 : 0;
   ep.sk_slab = w.sk_slab[r];
   ep.sk_ctl = w.sk_ctl[r];
-  return mmad_gemm_dispatch(dt, epi, A, lda, B, ldb, Mp, Np, K, ep, s, cfg);
+  const bool rec = probe >= 0 && probe == h->probe_id && 2 * h->probe_n < (int)h->probe_ev.size();
+  if (rec) MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n], s));
+  const int rc = mmad_gemm_dispatch(dt, epi, A, lda, B, ldb, Mp, Np, K, ep, s, cfg);
+  if (rc != MMAD_OK) return rc;
+  if (rec) {
+    MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n + 1], s));
+    ++h->probe_n;
+  }
+  return MMAD_OK;
 }
 
 static inline int rows_of(const AeWS& w, const AeLayer& a) { return a.enc ? w.B : w.B * w.k; }
@@ -440,12 +464,14 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
       ep.gscale = 2.0f / (float)k;
       ep.lossp = w.lossp;
       int cfg = 0;
-      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_MSE, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st, &cfg));
+      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_MSE, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st, &cfg,
+                     PROBE_FWD + l));
       h->mse_tiles = mmad_gemm_ntiles(cfg, Mp, a.Np);
     } else if (a.bn && train) {
       GemmEpi ep = fwd_epi(h, w, a, s, M, s.out, folded);
       ep.part = s.stats;
-      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
+      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st, nullptr,
+                     PROBE_FWD + l));
       if (l + 1 < nL) {
         // statistics -> (scale, shift) -> folded into layer l+1's weights/bias
         const AeLayer& c = h->L[l + 1];
@@ -466,10 +492,12 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
       GemmEpi ep = fwd_epi(h, w, a, s, M, s.y, folded);
       ep.bn_scale = s.scale;
       ep.bn_shift = s.shift;
-      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
+      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st, nullptr,
+                     PROBE_FWD + l));
     } else {
       GemmEpi ep = fwd_epi(h, w, a, s, M, s.out, folded);
-      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st));
+      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st, nullptr,
+                     PROBE_FWD + l));
     }
     if (h->vib && l == h->n_enc - 1) {
       const AeLayer& d0 = h->L[h->n_enc];
@@ -503,6 +531,7 @@ struct PendingDW {
   const void *dz, *in;
   int lda, ldb, M, N, K;
   GemmEpi ep;
+  int layer;
 };
 
 static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const AdamHyper* adam,
@@ -549,7 +578,8 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       // fork: dz_l is complete on the main stream; dW_l overlaps the chain below
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
       MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
-      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side));
+      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
+                     nullptr, PROBE_DW + l));
       if (dp) MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l], side));
     }
     if (l > 0) {
@@ -635,19 +665,22 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       const bool on_main = l < h->dw_main;
       if (on_main) {
         dwe.tile_force = mmad_tile_adam_main_override() + 1;
-        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st));
+        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st,
+                       nullptr, PROBE_DW + l));
       } else if (ping) {
         MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
-        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side));
+        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
+                       nullptr, PROBE_DW + l));
       } else if (!rec) {
-        pending.push_back(PendingDW{dz, in, a.Np, a.Kp, a.Np, a.Kp, Mp, dwe});
+        pending.push_back(PendingDW{dz, in, a.Np, a.Kp, a.Np, a.Kp, Mp, dwe, l});
       } else {
         MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_data[l], 0));
         for (const PendingDW& q : pending)
           RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, q.dz, q.lda, q.in, q.ldb, q.M, q.N, q.K, q.ep,
-                         side));
+                         side, nullptr, PROBE_DW + q.layer));
         pending.clear();
-        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side));
+        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
+                       nullptr, PROBE_DW + l));
       }
     }
   }
@@ -954,6 +987,47 @@ int mmad_ae_score_stream(mmad_ae* h, const float* x, int ld_x, int64_t N, int ba
   }
   h->graphs.push_back({x, ld_x, N, batch, layer_sq, ld_sq, ws, weights(h, h->L[0]), exec});
   return MMAD_OK;
+}
+
+int mmad_ae_status(mmad_ae* h, void* ws, int64_t ws_bytes, void* stream) {
+  MMAD_CHECK_ARG(h, "ae_status: null handle");
+  // no split-K GEMM can have run unless the override enabled it
+  if (mmad_splitk_override() <= 1 || !ws) return MMAD_OK;
+  AeWS w;
+  carve(h, 1, 1, (char*)ws, w);
+  MMAD_CHECK_ARG(ws_bytes >= w.bytes, "ae_status: workspace too small");
+  for (int r = 0; r < 2; ++r)
+    RET_IF(mmad_gemm_read_status(w.sk_ctl[r], (hipStream_t)stream, "ae_status"));
+  return MMAD_OK;
+}
+
+int mmad_ae_probe(mmad_ae* h, int kind, int layer, int capacity) {
+  MMAD_CHECK_ARG(h, "ae_probe: null handle");
+  MMAD_CHECK_ARG(kind == 0 || kind == 1, "ae_probe: kind must be 0 (forward GEMM) or 1 (dW GEMM)");
+  MMAD_CHECK_ARG(capacity >= 0 && capacity <= 4096, "ae_probe: capacity out of range");
+  MMAD_CHECK_ARG(layer < 0 || layer < (int)h->L.size(), "ae_probe: bad layer %d", layer);
+  for (auto e : h->probe_ev) (void)hipEventDestroy(e);
+  h->probe_ev.clear();
+  h->probe_n = 0;
+  h->probe_id = -1;
+  if (layer < 0 || capacity == 0) return MMAD_OK;
+  h->probe_ev.resize(2 * (size_t)capacity, nullptr);
+  for (auto& e : h->probe_ev) MMAD_HIP_CHECK(hipEventCreate(&e));
+  h->probe_id = (kind == 0 ? PROBE_FWD : PROBE_DW) + layer;
+  return MMAD_OK;
+}
+
+int mmad_ae_probe_read(mmad_ae* h, float* ms, int max_n) {
+  if (!h || !ms || max_n < 0) {
+    mmad_set_error("ae_probe_read: bad arguments");
+    return MMAD_EINVAL;
+  }
+  const int n = std::min(h->probe_n, max_n);
+  for (int i = 0; i < n; ++i) {
+    MMAD_HIP_CHECK(hipEventSynchronize(h->probe_ev[2 * i + 1]));
+    MMAD_HIP_CHECK(hipEventElapsedTime(&ms[i], h->probe_ev[2 * i], h->probe_ev[2 * i + 1]));
+  }
+  return n;
 }
 
 int mmad_ae_graph_count(const mmad_ae* h) { return h ? (int)h->graphs.size() : -1; }

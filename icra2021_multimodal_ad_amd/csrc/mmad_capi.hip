@@ -138,6 +138,13 @@ int mmad_gemm_set_workspace(void* ws, size_t bytes) {
   return MMAD_OK;
 }
 
+int mmad_gemm_status(void* stream) {
+  if (!g_sk_ws) return MMAD_OK;
+  size_t slab = 0, ctl = 0;
+  mmad_gemm_splitk_bytes(0, 0, &slab, &ctl);
+  return mmad_gemm_read_status((unsigned*)(g_sk_ws + slab), (hipStream_t)stream, "gemm_status");
+}
+
 static int layer_gemm(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,
                       int Np, int K, GemmEpi ep, void* stream) {
   if (g_sk_ws) {

@@ -2,6 +2,11 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+// split-K control block: per-launch arrival counters + flags use at most
+// 1920 words; this word records a combine that timed out (sticky until read
+// by mmad_gemm_status / mmad_ae_status)
+#define MMAD_SK_ERR_WORD 2047
+
 enum GemmEpiKind {
   GEMM_EPI_FWD = 0,         // y = BNaffine(act(acc + bias)); optional Welford partials
   GEMM_EPI_MSE = 1,         // dz = gscale*(acc + bias - target); partials (sum dz, sum d^2)
@@ -74,7 +79,8 @@ struct GemmEpi {
   int splitk;
   int tiles_n, group_m;
   int tile_force;        // caller's tile choice + 1 (0 = none; ignored if it does not fit)
-  int dbg;               // diagnostics (tools/gemm_sweep): 1 skip main loop, 2 skip epilogue
+  int dbg;               // diagnostics (tools/gemm_sweep): 1 skip main loop, 2 skip epilogue,
+                         // 4 force the split-K combine's timeout path (tests)
 };
 
 int mmad_group_override();
@@ -101,6 +107,9 @@ int mmad_gemm_tiles(int Mp, int Np);
 int mmad_gemm_splitk(int Mp, int Np, int K, int dtype);
 // split-K workspace sufficient for every launch (shape-independent bound)
 void mmad_gemm_splitk_bytes(int Mp, int Np, size_t* slab_bytes, size_t* ctl_bytes);
+// read (and clear) the timeout word of a split-K control block after syncing
+// `s`: MMAD_OK, or MMAD_EHIP with the error string set
+int mmad_gemm_read_status(unsigned* ctl, hipStream_t s, const char* who);
 
 // cfg_used (nullable) receives the tile configuration launched
 int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,

@@ -450,17 +450,34 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
       return;
     }
     if (tid == 0) {
+      // a slice that never publishes (it cannot happen with every block of
+      // the grid resident or queued, but a bounded spin must not combine a
+      // stale slab): flag the launch as failed and skip the epilogue; the
+      // host reads the word with mmad_gemm_status / mmad_ae_status.
+      // dbg bit 4 forces the timeout path (tests).
+      unsigned timed_out = 0u;
       for (int s2 = 0; s2 < S; ++s2) {
         if (s2 == sk) continue;
-        for (unsigned spins = 0; spins < (1u << 24); ++spins) {
-          if (__hip_atomic_load(flg + s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
-          __builtin_amdgcn_s_sleep(1);
+        bool ok = false;
+        if (!(ep.dbg & 4)) {
+          for (unsigned spins = 0; spins < (1u << 24); ++spins) {
+            if (__hip_atomic_load(flg + s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+              ok = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
         }
+        if (!ok) timed_out = 1u;
         __hip_atomic_store(flg + s2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (timed_out)
+        __hip_atomic_store(ep.sk_ctl + MMAD_SK_ERR_WORD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      shw[1] = timed_out;
     }
     __syncthreads();
+    if (shw[1]) return;
     asm volatile("" ::: "memory");           // every slab load below is sc1
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(slab_t, 0, S * BM * BN * 4, 0x00020000);
@@ -984,6 +1001,24 @@ void mmad_gemm_splitk_bytes(int Mp, int Np, size_t* slab_bytes, size_t* ctl_byte
   (void)Np;
   if (slab_bytes) *slab_bytes = (size_t)320 * 128 * 128 * 4;
   if (ctl_bytes) *ctl_bytes = (size_t)2048 * 4;
+}
+
+int mmad_gemm_read_status(unsigned* ctl, hipStream_t s, const char* who) {
+  if (!ctl) return MMAD_OK;
+  unsigned word = 0;
+  MMAD_HIP_CHECK(hipMemcpyAsync(&word, ctl + MMAD_SK_ERR_WORD, sizeof(word), hipMemcpyDeviceToHost, s));
+  MMAD_HIP_CHECK(hipStreamSynchronize(s));
+  if (word == 0) return MMAD_OK;
+  // a slice that gave up may still have raised its flag after the combine
+  // cleared it: every launch of the failed one has finished now (stream
+  // synchronised), so re-zero the whole control block for the next launch
+  size_t slab = 0, ctl_bytes = 0;
+  mmad_gemm_splitk_bytes(0, 0, &slab, &ctl_bytes);
+  MMAD_HIP_CHECK(hipMemsetAsync(ctl, 0, ctl_bytes, s));
+  MMAD_HIP_CHECK(hipStreamSynchronize(s));
+  mmad_set_error("%s: a split-K GEMM combine timed out waiting for a slice; its output tiles were "
+                 "not written (results invalid)", who);
+  return MMAD_EHIP;
 }
 
 int mmad_gemm_plan(int Mp, int Np, int K, int epi, int dtype) {

@@ -31,15 +31,16 @@ def _relu_normal(rng, mean, sd, shape):
     return np.maximum(rng.normal(mean, sd, shape), 0.0)
 
 
-def synth_windows(n, d, seed=0, anomaly=None, rng=None):
+def synth_windows(n, d, seed=0, anomaly=None, rng=None, strength=1.0):
     """n windows of width d (float32, [n, d]).  ``anomaly`` is a bool mask of
-    length n (True = anomalous window) or None."""
+    length n (True = anomalous window) or None; ``strength`` scales the
+    anomaly (F/T shift 0.6*strength, RGB gain 1 + 0.5*strength)."""
     rng = rng or np.random.Generator(np.random.PCG64(seed))
     x = np.zeros((n, d), np.float64)
     ft = rng.uniform(0.0, 1.0, (n, 1))
     if anomaly is not None:
         anomaly = np.asarray(anomaly, bool)
-        ft = ft + 0.6 * anomaly[:, None]
+        ft = ft + (0.6 * strength) * anomaly[:, None]
     if d == 64:
         x[:] = ft
         return x.astype(np.float32)
@@ -50,7 +51,7 @@ def synth_windows(n, d, seed=0, anomaly=None, rng=None):
         return x.astype(np.float32)
     rgb = _relu_normal(rng, 0.0, 0.075, (n, 1024))
     if anomaly is not None:
-        rgb = rgb * np.where(anomaly[:, None], 1.5, 1.0)
+        rgb = rgb * np.where(anomaly[:, None], 1.0 + 0.5 * strength, 1.0)
     x[:, 0:1024] = rgb
     x[:, 1024:1536] = _relu_normal(rng, 0.01, 0.08, (n, 512))
     x[:, 1536:1600] = ft

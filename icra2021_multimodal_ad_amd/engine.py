@@ -57,6 +57,14 @@ class NativeAE:
         self._alloc(device)
         self._ws = None
         self._synced_version = None
+        # version of the fp32 master as the plugin surface sees it: the
+        # reference-shaped nn.Parameters are views with their OWN version
+        # counters (load_state_dict / a torch optimizer bump those, not
+        # params._version), so the owner installs a callable summing them
+        self.version_fn = None
+        # bumped by every native call that rewrites the workspace; a
+        # differentiable forward records it and its backward checks it
+        self.gen = 0
         self.adam_step_count = 0
 
     # ------------------------------------------------------------------ memory
@@ -157,15 +165,33 @@ class NativeAE:
         if self.device.type != "cuda":
             raise _native.NativeUnavailable("model buffers are on the CPU; call .cuda() first")
 
+    def master_version(self):
+        return self.version_fn() if self.version_fn is not None else self.params._version
+
     def sync_shadow(self, force=False):
         """Refresh the bf16 weight shadow if the fp32 master was written by
         anything other than the native Adam (load_state_dict, torch optim)."""
-        if self.shadow is None:
+        if self.shadow is None or self.device.type != "cuda":
             return
-        v = self.params._version
+        v = self.master_version()
         if force or v != self._synced_version:
             call("mmad_ae_sync_shadow", self._h, stream_ptr())
             self._synced_version = v
+
+    def _mark_synced(self):
+        """The native Adam just wrote the master AND the shadow."""
+        if self.shadow is not None:
+            self._synced_version = self.master_version()
+
+    def check_status(self):
+        """Raise NativeError if a split-K GEMM combine of the calls since the
+        last check timed out (a no-op unless split-K is enabled)."""
+        if self._ws is None or self.device.type != "cuda":
+            return
+        base = self._ws.data_ptr()
+        aligned = (base + 255) // 256 * 256
+        call("mmad_ae_status", self._h, ctypes.c_void_p(aligned), self._ws.numel() - (aligned - base),
+             stream_ptr())
 
     def workspace(self, B, k=1):
         need = int(self._lib.mmad_ae_workspace_bytes(self._h, int(B), int(k)))
@@ -202,6 +228,7 @@ class NativeAE:
         if eps is not None:
             eps = eps.contiguous().float()
             assert eps.numel() == k * B * self.btl
+        self.gen += 1
         call("mmad_ae_train_fwd_bwd", self._h, ptr(x), x.stride(0), B, int(k), ptr(eps),
              int(seed), int(offset), float(beta_kl), ptr(loss_out), ws, nb, stream_ptr())
         return loss_out
@@ -221,11 +248,11 @@ class NativeAE:
             eps = eps.contiguous().float()
             assert eps.numel() == k * B * self.btl
         self.adam_step_count += 1
+        self.gen += 1
         call("mmad_ae_train_step", self._h, ptr(x), x.stride(0), B, int(k), ptr(eps), int(seed),
              int(offset), float(beta_kl), float(lr), float(betas[0]), float(betas[1]),
              float(adam_eps), int(self.adam_step_count), ptr(loss_out), ws, nb, stream_ptr())
-        if self.shadow is not None:
-            self._synced_version = self.params._version
+        self._mark_synced()
         return loss_out
 
     def backward(self, dxh, B):
@@ -240,8 +267,7 @@ class NativeAE:
             step = self.adam_step_count
         call("mmad_ae_adam", self._h, float(lr), float(betas[0]), float(betas[1]), float(eps),
              int(step), stream_ptr())
-        if self.shadow is not None:
-            self._synced_version = self.params._version
+        self._mark_synced()
 
     def forward(self, x, train_bn=False, want_xhat=True, want_loss=False):
         self._require(x)
@@ -251,6 +277,7 @@ class NativeAE:
         ws, nb = self.workspace(B, 1)
         xh = torch.empty((B, self.dec_widths[-1]), device=self.device) if want_xhat else None
         loss = torch.empty(1, device=self.device) if want_loss else None
+        self.gen += 1
         call("mmad_ae_forward", self._h, ptr(x), x.stride(0), B, int(bool(train_bn)), ptr(xh),
              self.dec_widths[-1], ptr(loss), ws, nb, stream_ptr())
         return xh, loss
@@ -267,6 +294,7 @@ class NativeAE:
         diffs = None
         if want_diffs:
             diffs = torch.empty((B, self.diff_width()), device=self.device)
+        self.gen += 1
         call("mmad_ae_score", self._h, ptr(x), x.stride(0), B, ptr(lsq), ptr(diffs), ws, nb,
              stream_ptr())
         return lsq, diffs
@@ -284,6 +312,7 @@ class NativeAE:
         self.sync_shadow()
         B = min(int(batch), N)
         ws, nb = self.workspace(B, 1)
+        self.gen += 1
         call("mmad_ae_score_stream", self._h, ptr(x), x.stride(0), N, B, ptr(out), out.stride(0),
              ws, nb, 1 if graph else 0, stream_ptr())
         return out

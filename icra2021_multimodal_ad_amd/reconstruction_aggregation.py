@@ -31,6 +31,7 @@ def get_diffs(x, model, batch_size=698):
             d = diffs.cpu().numpy()
             for i in range(len(widths)):
                 out[i].append(d[:, cuts[i]:cuts[i + 1]])
+    model._native.check_status()
     return [np.concatenate(o, axis=0) for o in out]
 
 
@@ -86,13 +87,24 @@ class NapScorer:
     run: ONE native GEMM per batch (mmad_nap_score): the concatenated diffs
     times V^T with the centring/standardising folded into a bias and a
     per-column weight, squared-mean reduced in the epilogue -- the rotated
-    diffs are never materialised.
+    diffs are never materialised.  The run is always the exact-fp32 GEMM,
+    whatever the model's dtype: the centring is folded in AFTER the product,
+    and near-zero ``var`` columns (rank-deficient fits)
+    multiply any rounding of (x V) by 1/var, which bf16 operands would turn
+    into noise.
     """
 
-    def __init__(self, model, start_layer_index=0, end_layer_index=None):
+    def __init__(self, model=None, start_layer_index=0, end_layer_index=None, widths=None,
+                 device=None):
+        import torch as _t
+        if model is not None:
+            widths = model._native.diff_widths()
+            device = model._native.device
+        if widths is None:
+            raise ValueError("NapScorer needs a model or the diff widths")
         self.model = model
-        nat = model._native
-        widths = nat.diff_widths()
+        self.device = _t.device(device) if device is not None else \
+            _t.device("cuda", _t.cuda.current_device())
         n = len(widths)
         if end_layer_index is None:
             end_layer_index = n + 1
@@ -101,25 +113,39 @@ class NapScorer:
         if end_layer_index - start_layer_index < 1:
             end_layer_index = start_layer_index + 1
         self.sel = slice(start_layer_index, end_layer_index)
-        cuts = np.cumsum([0] + widths)
+        cuts = np.cumsum([0] + list(widths))
         self.c0, self.c1 = int(cuts[self.sel.start]), int(cuts[min(self.sel.stop, n)])
         self.fit_state = None
 
+    @classmethod
+    def standalone(cls, width, device=None):
+        """A scorer over already-concatenated [N, width] diffs."""
+        return cls(widths=[int(width)], device=device)
+
     def _cat(self, diffs):
         if isinstance(diffs, (list, tuple)):
-            diffs = np.concatenate(diffs[self.sel], axis=1)
+            parts = [torch.as_tensor(d) for d in diffs[self.sel]]
+            return torch.cat([p.to(parts[0].device, torch.float32) for p in parts], dim=1)
         return torch.as_tensor(diffs)
 
     def fit(self, train_diffs=None, fit_state=None):
         """train_diffs: list of per-layer arrays (get_diffs) or [N, W]; or a
         ready fit_state {'mu_r','v','mu_s','var'} (e.g. the reference's)."""
-        dev = self.model._native.device
+        dev = self.device
         if fit_state is None:
             x = self._cat(train_diffs).to(dev, torch.float64)
             mu_r = x.mean(0)
             xc = x - mu_r
-            _, _, vh = torch.linalg.svd(xc, full_matrices=False)
-            v = vh.T
+            n, wdt = xc.shape
+            if n > wdt:
+                # V = right singular vectors of xc = eigenvectors of the Gram
+                # xc^T xc, in descending eigenvalue order (one [W x W]
+                # symmetric eigensolve instead of an [N x W] SVD)
+                _, evec = torch.linalg.eigh(xc.T @ xc)
+                v = evec.flip(1)
+            else:
+                _, _, vh = torch.linalg.svd(xc, full_matrices=False)
+                v = vh.T
             rot = (xc.float() @ v.float()).double()     # Rotater.run is fp32 matmul
             mu_s = rot.mean(0)
             var = ((rot - mu_s) ** 2).sum(0) / max(rot.shape[0] - 1, 1)
@@ -127,13 +153,11 @@ class NapScorer:
         fit_state = {k: torch.as_tensor(np.asarray(v) if not torch.is_tensor(v) else v).to(dev)
                      for k, v in fit_state.items()}
         self.fit_state = fit_state
-        nat = self.model._native
         from ._native import pad
         W, R = fit_state["v"].shape
         Kp, Rp = pad(W), pad(R)
-        tdt = torch.bfloat16 if nat.dt == 1 else torch.float32
-        vt = torch.zeros((Rp, Kp), device=dev, dtype=tdt)
-        vt[:R, :W] = fit_state["v"].T.to(tdt)
+        vt = torch.zeros((Rp, Kp), device=dev, dtype=torch.float32)
+        vt[:R, :W] = fit_state["v"].T.float()
         # (x - mu_r) V - mu_s = x V + bias, bias = -(mu_r V + mu_s)  (float64 fold)
         bias = torch.zeros(Rp, device=dev)
         bias[:R] = (-(fit_state["mu_r"].double() @ fit_state["v"].double())
@@ -146,20 +170,19 @@ class NapScorer:
     def score(self, diffs):
         """diffs: list of per-layer arrays or [N, W] (host or device) -> [N]
         NAP scores (device fp32)."""
-        from ._native import call, ptr, stream_ptr, pad
-        nat = self.model._native
+        from ._native import call, ptr, stream_ptr, pad, F32, require_gpu
         W, R, Kp, Rp, vt, bias, w = self._dev
-        x = self._cat(diffs).to(nat.device, torch.float32).contiguous()
+        x = self._cat(diffs).to(self.device, torch.float32).contiguous()
+        require_gpu(x)
         N = x.shape[0]
         assert x.shape[1] == W, (x.shape, W)
         Mp = pad(N)
-        tdt = torch.bfloat16 if nat.dt == 1 else torch.float32
-        xp = torch.empty((Mp, Kp), device=nat.device, dtype=tdt)
-        dt = nat.dt
+        xp = torch.empty((Mp, Kp), device=self.device, dtype=torch.float32)
+        dt = F32
         s = stream_ptr()
         call("mmad_pack_input", dt, N, W, Mp, Kp, ptr(x), x.stride(0), ptr(xp), s)
-        rowsq = torch.empty((Rp // 128, Mp), device=nat.device)
-        out = torch.empty(N, device=nat.device)
+        rowsq = torch.empty((Rp // 128, Mp), device=self.device)
+        out = torch.empty(N, device=self.device)
         call("mmad_nap_score", dt, N, W, R, Mp, Kp, Rp, ptr(xp), ptr(vt), ptr(bias), ptr(w),
              ptr(rowsq), ptr(out), s)
         return out

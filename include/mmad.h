@@ -48,7 +48,8 @@ int mmad_pad_granule(void);
  * thr, 4 = 64x128, 5 = 128x128/256 thr; a tile that does not divide a shape
  * falls back to the tuned one), knob 1 = XCD tile-group height override (-1
  * auto), knob 2 = per-shape autotune on first dispatch (1, default) or static
- * heuristic (0), knob 3 = diagnostics (tools/gemm_sweep only), knob 4 = split-K
+ * heuristic (0), knob 3 = diagnostics (tools/gemm_sweep; 4 = force the split-K
+ * combine's timeout path, tests only), knob 4 = split-K
  * factor override for GEMMs given split-K workspace (0 = shape rule, 1/2/4),
  * knob 5 = tile of the dW GEMMs with the fused Adam epilogue (default 3 =
  * 64x64; -1 = autotuned like the others), knobs 6 / 7 = tile of the bwd-data /
@@ -72,6 +73,11 @@ int mmad_tune_set(int knob, int value);
  * different streams.  ws = NULL turns it off. */
 size_t mmad_gemm_ws_bytes(void);
 int mmad_gemm_set_workspace(void* ws, size_t bytes);
+/* Synchronises `stream` and reports (then clears) a split-K combine that timed
+ * out in the calling thread's layer-operator workspace since the last check:
+ * MMAD_EHIP and the error string if one did (its output tiles were not
+ * written), MMAD_OK otherwise (also without a workspace). */
+int mmad_gemm_status(void* stream);
 
 /* FCLayer.forward, layers/fc_layer.py:37-48 (nn.Linear -> Activation -> BN).
  * y[Mp][Np] = bn_affine(act(x[Mp][Kp] . w[Np][Kp]^T + bias[Np])).
@@ -319,9 +325,46 @@ int mmad_ae_score(mmad_ae* h, const float* x, int ld_x, int B, float* layer_sq, 
 int mmad_ae_score_stream(mmad_ae* h, const float* x, int ld_x, int64_t N, int batch,
                          float* layer_sq, int64_t ld_sq, void* ws, int64_t ws_bytes, int use_graph,
                          void* stream);
+/* Split-K health of the executor workspace `ws` (as mmad_gemm_status): a
+ * no-op returning MMAD_OK unless split-K is enabled (tuning knob 4 > 1);
+ * otherwise synchronises `stream` and returns MMAD_EHIP if any GEMM combine
+ * of the calls since the last check timed out. */
+int mmad_ae_status(mmad_ae* h, void* ws, int64_t ws_bytes, void* stream);
+
+/* Kernel probe (measurement only; no reference counterpart): from now on the
+ * executor brackets ONE GEMM launch per call with a pair of timing events on
+ * the stream that launch runs on -- kind 0: the forward (or MSE / score) GEMM
+ * of `layer`, kind 1: its dW GEMM (Adam fused in mmad_ae_train_step) -- for
+ * the next `capacity` calls.  layer < 0 or capacity 0 turns it off.
+ * mmad_ae_probe_read synchronises on the recorded events and writes up to
+ * max_n durations (ms) in call order; returns how many (or < 0). */
+int mmad_ae_probe(mmad_ae* h, int kind, int layer, int capacity);
+int mmad_ae_probe_read(mmad_ae* h, float* ms, int max_n);
+
 /* number of cached score graphs (-1 for a null handle); drop them all */
 int mmad_ae_graph_count(const mmad_ae* h);
 int mmad_ae_clear_graphs(mmad_ae* h);
+
+/* ------------------------------------------------------------------------
+ * Anomaly-score metrics on the device (utils/metric.py, sklearn/numpy on the
+ * host in the reference).  Scores fp32, labels uint8 (nonzero = anomaly,
+ * novelty_detection.py:31-34), all device pointers; workspace caller-owned,
+ * 256-byte aligned, sized by the *_ws_bytes queries.  Results fp64, device.
+ * ---------------------------------------------------------------------- */
+/* get_auc_roc :29-44 (roc_curve + auc; ties count one half, NaN with one
+ * class) and get_auc_prc :97-116 (trapezoid over precision_recall_curve's
+ * points): out[4] = auroc, aupr, n_pos, n_neg. */
+size_t mmad_rank_metrics_ws_bytes(int64_t n);
+int mmad_rank_metrics(int64_t n, const float* score, const uint8_t* label, double* out, void* ws,
+                      size_t ws_bytes, void* stream);
+/* get_f1_score :118-130 (threshold = np.quantile(valid, q), linear rule;
+ * prediction test > threshold) and get_confusion_matrix :83-95 (test >=
+ * threshold): out[10] = threshold, f1, p, r, precision, recall, tp, fp, fn,
+ * tn (undefined ratios are NaN, as numpy's 0/0). */
+size_t mmad_threshold_metrics_ws_bytes(int64_t n_valid);
+int mmad_threshold_metrics(int64_t n_valid, const float* valid, int64_t n_test, const float* test,
+                           const uint8_t* label, double q, double* out, void* ws, size_t ws_bytes,
+                           void* stream);
 
 /* HSR_Net multimodal fusion producer (utils/data_loaders.py:152-229; replaces
  * the per-window loop HSR_Net.forward :179-229 that TabularDataset runs at

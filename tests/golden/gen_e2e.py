@@ -1,0 +1,155 @@
+"""End-to-end fixture: the REFERENCE's own training + scoring on the seeded
+synthetic split, for the north-star "AUROC within +-0.002 of reference" check
+(tests/test_gpu_e2e.py).
+
+Runs only in the build container (needs /root/reference); writes
+tests/golden/e2e.npz.  Usage:
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_e2e.py [--seeds 0 1 2]
+
+What runs from the reference, unmodified: ``AutoEncoder.step`` / ``validate``
+(models/auto_encoder.py:57-91) with ``optim.Adam(lr=1e-3)``
+(novelty_detection.py:90), ``get_diffs`` (reconstruction_aggregation.py:6-37)
+and ``utils.metric.get_recon_loss`` / ``get_d_loss`` / ``get_d_norm_loss``
+(BASE / SAP / NAP with sklearn AUROC, AUPR, F1, precision, recall).
+What is emulated: ignite is absent, so NoveltyDetecter.train's loop
+(novelty_detection.py:88-127) is restated: trainer over the train loader,
+evaluator over the valid loader after every epoch, RunningAverage
+(alpha 0.98, reset per epoch, first value as is) on both, deepcopy of the
+state_dict when the evaluator's EMA beats the lowest, best state loaded at the
+end.  Inputs: the build's seeded dataset and loaders
+(icra2021_multimodal_ad_amd.data_loaders, CPU) -- the same splits, the same
+train order every epoch -- and seeded initial weights (init_state_dict).
+Shims: ``collections.Iterable`` (models/abstract_model.py:25).
+"""
+import argparse
+import collections
+import collections.abc
+import contextlib
+import io
+import os
+import sys
+import tempfile
+import time
+import types
+from copy import deepcopy
+
+sys.dont_write_bytecode = True
+collections.Iterable = collections.abc.Iterable
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(1, REF)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from icra2021_multimodal_ad_amd.common_utils import init_state_dict  # noqa: E402
+from icra2021_multimodal_ad_amd.data_loaders import get_loaders  # noqa: E402
+
+torch.set_num_threads(8)
+
+# the e2e configuration (shared with tests/test_gpu_e2e.py through the fixture)
+E2E = dict(input_size=1728, btl_size=100, n_layers=5, batch_size=1000, n_epochs=8,
+           n_normal=10000, n_novelty=1000, anomaly_strength=0.7, data="hsr_objectdrop",
+           target_class=1, unimodal_normal=False, novelty_ratio=0.0, start_layer_index=0,
+           end_layer_index=-1, sensor="All", verbose=0)
+
+
+def config_for(seed):
+    c = types.SimpleNamespace(**E2E)
+    c.gpu_id = -1
+    c.data_seed = 100 + seed
+    c.sampler_seed = 200 + seed
+    c.model_seed = 300 + seed
+    return c
+
+
+def ema_update(v, x, alpha=0.98):
+    return x if v is None else v * alpha + (1 - alpha) * x
+
+
+def run_reference(seed):
+    from model_builder import get_model
+    from models.auto_encoder import AutoEncoder
+    from reconstruction_aggregation import get_diffs
+    from utils import metric
+    cfg = config_for(seed)
+    model = get_model(types.SimpleNamespace(input_size=cfg.input_size, btl_size=cfg.btl_size,
+                                            n_layers=cfg.n_layers, gpu_id=-1))
+    sd0 = init_state_dict(cfg.input_size, cfg.btl_size, cfg.n_layers, seed=cfg.model_seed)
+    model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd0.items()})
+    dset, train_loader, valid_loader, test_loader = get_loaders(cfg, device="cpu")
+    optimizer = torch.optim.Adam(model.parameters(), lr=1e-3)
+    eng = types.SimpleNamespace(model=model, optimizer=optimizer, config=cfg)
+    train_hist, valid_hist = [], []
+    lowest, best, best_epoch = np.inf, None, 0
+    for epoch in range(1, cfg.n_epochs + 1):
+        ema = None
+        for x, y in train_loader:
+            (lv,) = AutoEncoder.step(eng, (x, y))
+            ema = ema_update(ema, lv)
+        train_hist.append(ema)
+        vema = None
+        for x, y in valid_loader:
+            (lv,) = AutoEncoder.validate(eng, (x, y))
+            vema = ema_update(vema, lv)
+        if vema < lowest:
+            lowest, best, best_epoch = vema, deepcopy(model.state_dict()), epoch
+        valid_hist.append(vema)
+    model.load_state_dict(best)
+    model.eval()
+    with torch.no_grad():
+        tr_x, _ = dset.get_transformed_data(train_loader)
+        va_x, _ = dset.get_transformed_data(valid_loader)
+        te_x, te_y = dset.get_transformed_data(test_loader)
+        te_y = np.where(np.isin(np.asarray(te_y), [cfg.target_class]), True, False)
+        tr = get_diffs(tr_x, model, batch_size=cfg.batch_size)
+        va = get_diffs(va_x, model)
+        te = get_diffs(te_x, model)
+    out = {}
+    end = cfg.n_layers + 1 - cfg.end_layer_index
+    with contextlib.redirect_stdout(io.StringIO()), tempfile.TemporaryDirectory() as td:
+        r_base = metric.get_recon_loss(va[0], te[0], te_y, f1_quantiles=[.90])
+        r_sap = metric.get_d_loss(tr, va, te, te_y, gpu_id=-1, start_layer_index=cfg.start_layer_index,
+                                  end_layer_index=end, norm_type=2, f1_quantiles=[.90])
+        cfg.train_diffs = os.path.join(td, "train_diffs.pt")
+        r_nap = metric.get_d_norm_loss(tr, va, te, te_y, cfg, gpu_id=-1,
+                                       start_layer_index=cfg.start_layer_index, end_layer_index=end,
+                                       norm_type=2, f1_quantiles=[.90])
+    for name, r in (("base", r_base), ("sap", r_sap), ("nap", r_nap)):
+        score, auroc, aupr, f1, prec, rec = r
+        out[f"{name}/score"] = np.asarray(score, np.float32)
+        out[f"{name}/auroc"] = np.float64(auroc)
+        out[f"{name}/aupr"] = np.float64(aupr)
+        out[f"{name}/f1"] = np.float64(f1)
+        out[f"{name}/precision"] = np.float64(prec)
+        out[f"{name}/recall"] = np.float64(rec)
+    out["test_label"] = te_y
+    out["train_history"] = np.asarray(train_hist, np.float64)
+    out["valid_history"] = np.asarray(valid_hist, np.float64)
+    out["best_epoch"] = np.int64(best_epoch)
+    out["n_train"] = np.int64(len(tr_x))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seeds", type=int, nargs="+", default=[0, 1, 2])
+    a = ap.parse_args()
+    res = {"meta/" + k: np.asarray(v) for k, v in E2E.items()}
+    res["meta/torch"] = np.array(torch.__version__)
+    res["meta/seeds"] = np.asarray(a.seeds, np.int64)
+    for s in a.seeds:
+        t0 = time.time()
+        o = run_reference(s)
+        res.update({f"s{s}/{k}": v for k, v in o.items()})
+        print(f"seed {s}: {time.time() - t0:.0f} s  best epoch {int(o['best_epoch'])}  "
+              f"AUROC base {float(o['base/auroc']):.4f} sap {float(o['sap/auroc']):.4f} "
+              f"nap {float(o['nap/auroc']):.4f}", flush=True)
+    np.savez_compressed(os.path.join(HERE, "e2e.npz"), **res)
+
+
+if __name__ == "__main__":
+    main()

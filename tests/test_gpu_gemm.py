@@ -160,3 +160,39 @@ def test_shadow_pair_matches_single_shadow(monkeypatch):
         res[pair] = (losses, nat.params.clone())
     assert res["1"][0] == res["0"][0]
     assert torch.equal(res["1"][1], res["0"][1])
+
+
+def test_splitk_timeout_is_reported_not_combined(ws):
+    """A split-K combine that gives up waiting for a slice (forced here with
+    the diagnostics knob) must not write a result built from stale slabs: the
+    output tiles stay untouched and mmad_gemm_status reports MMAD_EHIP once."""
+    lib = _native.load()
+    M, N, K = 1024, 1658, 2048
+    Mp, Np, Kp = pad(M), pad(N), pad(K)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(Mp, Kp, device=dev).bfloat16()
+    w = (torch.randn(Np, Kp, device=dev) * 0.05).bfloat16()
+    b = torch.zeros(Np, device=dev)
+    y = torch.full((Mp, Np), float("nan"), device=dev, dtype=torch.bfloat16)
+    s = stream_ptr()
+    assert lib.mmad_gemm_status(s) == 0
+    lib.mmad_tune_set(4, 2)
+    lib.mmad_tune_set(3, 4)
+    try:
+        call("mmad_fc_fwd", BF16, M, N, K, Mp, Np, Kp, ptr(x), ptr(w), ptr(b), 0, 0.0, None, None,
+             ptr(y), None, s)
+        rc = lib.mmad_gemm_status(s)
+    finally:
+        lib.mmad_tune_set(3, 0)
+        lib.mmad_tune_set(4, 0)
+    assert rc == _native.MMAD_EHIP
+    assert b"timed out" in lib.mmad_last_error_string()
+    assert torch.isnan(y.float()).all()          # no tile was combined from the slabs
+    assert lib.mmad_gemm_status(s) == 0          # reported once, then cleared
+    assert _ctl_zero(ws)
+    # and the next (normal) launch is correct again
+    call("mmad_fc_fwd", BF16, M, N, K, Mp, Np, Kp, ptr(x), ptr(w), ptr(b), 0, 0.0, None, None,
+         ptr(y), None, s)
+    ref = x[:M, :K].double() @ w[:N, :K].double().t()
+    err = (y[:M, :N].double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-2

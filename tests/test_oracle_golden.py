@@ -159,3 +159,34 @@ def test_auroc_matches_sklearn():
     lab = rng.random(500) < 0.3
     fpr, tpr, _ = metrics.roc_curve(lab, s)
     assert abs(O.auroc(s, lab) - metrics.auc(fpr, tpr)) < 1e-12
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_torch_cpu_restatement_matches_reference(golden, name):
+    """oracle/torch_ref.py (bench.py's cpu_baseline: stock torch modules in the
+    reference's order) reproduces the reference's loss trajectory and step-1
+    gradients on the golden inputs."""
+    import torch
+    from oracle import torch_ref
+    from icra2021_multimodal_ad_amd.common_utils import ae_widths
+    g = golden(name)
+    d, btl, nl = int(g["meta_d"]), int(g["meta_btl"]), int(g["meta_n_layers"])
+    enc, dec = ae_widths(d, btl, nl)
+    m = torch_ref.build({k: torch.from_numpy(np.asarray(v)) for k, v in _sd(g, "init/").items()},
+                        enc, dec)
+    x0 = torch.from_numpy(g["x/0"])
+    m.train()
+    loss = m.recon_loss(m(x0), x0)
+    loss.backward()
+    assert abs(loss.item() - g["step1/loss"]) <= 1e-5 * g["step1/loss"]
+    for k, p in m.named_parameters():
+        assert _rel(p.grad.numpy(), g["step1/grad/" + k]) < 1e-4, k
+    m = torch_ref.build({k: torch.from_numpy(np.asarray(v)) for k, v in _sd(g, "init/").items()},
+                        enc, dec)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    steps = int(g["meta_steps"])
+    for s in range(steps):
+        lv = torch_ref.train_step(m, opt, torch.from_numpy(g[f"x/{s}"]))
+        assert abs(lv - g[f"loss/{s}"]) <= (1e-5 if s == 0 else 5e-3) * g[f"loss/{s}"], s
+    sd = m.state_dict()
+    assert list(sd.keys()) == [k[len("init/"):] for k in g.files if k.startswith("init/")]
