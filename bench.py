@@ -14,12 +14,16 @@ Workloads (``--config``; ``auto`` = c2 on one GPU, c4 on several):
 RANK/WORLD_SIZE/LOCAL_RANK.  W untimed steps, then K timed steps between
 barrier + synchronize pairs, the max over ranks; rank 0 prints ONE JSON line:
 
+* the timed steps each replay ONE captured hipGraph of the whole step
+  (mmad_ae_train_step_graph; ``train_step`` says which schedule ran).
 * ``roofline``: the kernel that dominates the step -- the dW GEMM with the
   fused Adam epilogue of the largest layer, HBM-bound (26 B of Adam state per
-  parameter + its two bf16 operands).  Its duration is measured IN the timed
-  region by the executor's probe (mmad_ae_probe: a HIP event pair around that
-  one launch, on the stream it runs on); ``traffic`` = PMC HBM bytes per launch
-  from the newest matching profiles/*_pmc_dw.json.
+  parameter + its two bf16 operands).  Its duration comes from the executor's
+  probe (mmad_ae_probe: a HIP event pair around that one launch, on the stream
+  it runs on) over eager steps of the same state right after the timed region
+  (a graph replay has no per-kernel events); the rocprofv3 kernel trace of the
+  graph-mode run under profiles/ gives the in-graph average;  ``traffic`` =
+  PMC HBM bytes per launch from the newest matching profiles/*_pmc_dw.json.
 * ``roofline_encoder_gemm``: the encoder's first forward GEMM (the north-star
   MFMA target), launched back to back between one event pair.
 * ``cpu_baseline`` (rank 0, N=1): the torch-CPU fp32 restatement of the
@@ -194,8 +198,8 @@ def dw_roofline(nat, layer, durations_ms, batch, steps_timed, fused_adam=True):
             "avg_us": round(avg_s * 1e6, 2), "launches_timed": len(durations_ms),
             "algorithmic_bytes_per_launch": nbytes,
             "flops_per_launch": 2.0 * rows * L["N"] * L["K"],
-            "timing": f"executor probe: HIP event pair around this launch on its stream, "
-                      f"every one of the {steps_timed} timed steps"}
+            "timing": f"executor probe: HIP event pair around this launch on its stream, in "
+                      f"{steps_timed} eager steps right after the timed region"}
 
 
 def parse_args(argv=None):
@@ -256,29 +260,18 @@ def run(args):
     torch.cuda.synchronize()
     probe_layer = pick_dominant_layer(nat)
     lib = _native.load()
-    probing = not args.no_probe and rank == 0
-    if probing:
-        _native.check(lib.mmad_ae_probe(nat._h, 1, probe_layer, args.steps), "mmad_ae_probe")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = model.train_step_async(pool[i % len(pool)], opt)
+    t_host = time.perf_counter() - t0           # enqueue time (no sync inside the loop)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    durs = []
-    if probing:
-        import ctypes
-        buf = (ctypes.c_float * args.steps)()
-        n = lib.mmad_ae_probe_read(nat._h, buf, args.steps)
-        if n < 0:
-            _native.check(n, "mmad_ae_probe_read")
-        durs = list(buf[:n])
-        _native.check(lib.mmad_ae_probe(nat._h, 1, -1, 0), "mmad_ae_probe")
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -311,6 +304,7 @@ def run(args):
                    "global_batch": batch * world, "input_dim": dim,
                    "parallelism": f"dp{world}", "exchange": exchange},
         "model_tflops": round(value * fpw / 1e12, 2),
+        "host_enqueue_ms_per_step": round(t_host / args.steps * 1e3, 4),
         "final_loss": loss_v,
     }
     if world > 1:
@@ -335,10 +329,34 @@ def run(args):
                                    "ms_per_step": round(e1 / n1 * 1e3, 4), "steps": n1,
                                    "how": "same ranks, exchange off, after the timed region (max over ranks)"}
         model.dist = mdl_dist
+    durs, n_probe = [], 0
+    if not args.no_probe and rank == 0:
+        # the timed steps replay one captured hipGraph each, so the dominant
+        # kernel is timed by the executor's probe on EAGER steps of the same
+        # state and inputs right after the timed region (HIP event pair around
+        # that one launch, on the stream it is launched on)
+        import ctypes
+        n_probe = max(20, args.steps // 4)
+        graph_mode = nat.use_graph
+        nat.use_graph = False
+        _native.check(lib.mmad_ae_probe(nat._h, 1, probe_layer, n_probe), "mmad_ae_probe")
+        for i in range(n_probe):
+            model.train_step_async(pool[i % len(pool)], opt)
+        torch.cuda.synchronize()
+        buf = (ctypes.c_float * n_probe)()
+        n = lib.mmad_ae_probe_read(nat._h, buf, n_probe)
+        if n < 0:
+            _native.check(n, "mmad_ae_probe_read")
+        durs = list(buf[:n])
+        _native.check(lib.mmad_ae_probe(nat._h, 1, -1, 0), "mmad_ae_probe")
+        nat.use_graph = graph_mode
+    res["train_step"] = ("one captured hipGraph replay per step (mmad_ae_train_step_graph)"
+                         if nat.use_graph and (model.dist is None or not model.dist.native)
+                         else "eager executor step (mmad_ae_train_step)")
     if rank == 0:
         if durs:
             fused = model.dist is None or not model.dist.native
-            res["roofline"] = dw_roofline(nat, probe_layer, durs, batch, args.steps, fused_adam=fused)
+            res["roofline"] = dw_roofline(nat, probe_layer, durs, batch, n_probe, fused_adam=fused)
         res["roofline_encoder_gemm"] = gemm_roofline(model, batch)
         if not args.no_cpu_baseline and world == 1:   # host baseline: rank 0 at N=1 only
             res["cpu_baseline"] = cpu_baseline(dim, batch, vib, budget_s=args.cpu_budget)

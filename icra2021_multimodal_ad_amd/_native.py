@@ -40,6 +40,7 @@ SIGNATURES = {
     "mmad_nap_score": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
     "mmad_fc_bwd_data": (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "mmad_fc_bwd_weight": (_I, [_I, _I, _I, _I, _P, _P, _P, _P]),
+    "mmad_fc_bwd_weight_adam": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _P]),
     "mmad_bn_act_bwd_ws": (ctypes.c_size_t, [_I, _I]),
     "mmad_bn_act_bwd": (_I, [_I, _I, _F, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                              _P]),
@@ -62,6 +63,9 @@ SIGNATURES = {
     "mmad_ae_train_fwd_bwd": (_I, [_P, _P, _I, _I, _I, _P, _U64, _U64, _F, _P, _P, _I64, _P]),
     "mmad_ae_train_step": (_I, [_P, _P, _I, _I, _I, _P, _U64, _U64, _F, _F, _F, _F, _F, _I, _P,
                                 _P, _I64, _P]),
+    "mmad_ae_train_step_graph": (_I, [_P, _P, _I, _I, _I, _P, _U64, _U64, _F, _F, _F, _F, _F, _I, _P,
+                                      _P, _I64, _P]),
+    "mmad_ae_train_graph_count": (_I, [_P]),
     "mmad_ae_backward": (_I, [_P, _P, _I, _I, _P, _I64, _P]),
     "mmad_ae_adam": (_I, [_P, _F, _F, _F, _F, _I, _P]),
     "mmad_ae_forward": (_I, [_P, _P, _I, _I, _I, _P, _I, _P, _P, _I64, _P]),

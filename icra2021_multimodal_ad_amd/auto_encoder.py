@@ -115,6 +115,7 @@ class AutoEncoder(AbstractModel):
 
     def _rebind(self):
         nat = self._native
+        self.__dict__.pop("_plist_cache", None)
         for l, layer in enumerate(self._layers()):
             layer.mmad_dtype = self.mmad_dtype
             w, b, g, be = nat.param_views(nat.params, l)
@@ -149,7 +150,11 @@ class AutoEncoder(AbstractModel):
     def _param_version(self):
         """Sum of the version counters the fp32 master can be written through
         (each nn.Parameter view has its own; the flat buffer has one more)."""
-        return sum(p._version for p in self._param_list()) + self._native.params._version
+        plist = self.__dict__.get("_plist_cache")
+        if plist is None:
+            plist = self._param_list()
+            self.__dict__["_plist_cache"] = plist
+        return sum(p._version for p in plist) + self._native.params._version
 
     def _count_bn_step(self):
         self._nbt_pending += 1
@@ -223,7 +228,8 @@ class AutoEncoder(AbstractModel):
     def train_step_async(self, x, optimizer=None, eps=None):
         """One AutoEncoder.step worth of work (train mode, fwd + sum-MSE +
         bwd [+ grad all-reduce] + Adam) with the loss left on the device."""
-        self.train()
+        if not self.training:
+            self.train()
         nat = self._native
         seed = 0x9E3779B97F4A7C15 & ((1 << 63) - 1)
         if self.dist is None or self.dist.native:
@@ -278,8 +284,8 @@ class AutoEncoder(AbstractModel):
         """Expose the native m/v as the torch optimizer's state (views)."""
         nat = self._native
         if getattr(optimizer, "_mmad_mirrored", None) is self:
-            for st in optimizer.state.values():
-                st["step"].fill_(float(nat.adam_step_count))
+            # every parameter's state shares one step tensor
+            optimizer._mmad_step.fill_(float(nat.adam_step_count))
             return
         ms, vs = [], []
         for l, layer in enumerate(self._layers()):
@@ -287,9 +293,10 @@ class AutoEncoder(AbstractModel):
             w2, b2, g2, be2 = nat.param_views(nat.exp_avg_sq, l)
             ms += [w, b] + ([g, be] if layer.bn is not None else [])
             vs += [w2, b2] + ([g2, be2] if layer.bn is not None else [])
+        step = torch.tensor(float(nat.adam_step_count))
         for p, m, v in zip(self._param_list(), ms, vs):
-            optimizer.state[p] = {"step": torch.tensor(float(nat.adam_step_count)),
-                                  "exp_avg": m, "exp_avg_sq": v}
+            optimizer.state[p] = {"step": step, "exp_avg": m, "exp_avg_sq": v}
+        optimizer._mmad_step = step
         optimizer._mmad_mirrored = self
 
     @staticmethod

@@ -104,7 +104,32 @@ struct mmad_ae {
   mutable int probe_id = -1;
   mutable int probe_n = 0;
   std::vector<hipEvent_t> probe_ev;   // [2 * capacity]: start, end pairs
+  // hipGraph-captured fused train steps (mmad_ae_train_step_graph): one per
+  // call signature, replayed after a host->device copy of the per-call values
+  // (a ring of pinned host slots, each reused only once its copy has run)
+  struct TrainGraph {
+    int B, k, ld_x, xvec, has_eps, dw_main, ev_every, keep_grads;
+    const void* ws;
+    float beta_kl, b1, b2, aeps;
+    hipGraphExec_t exec;
+  };
+  std::vector<TrainGraph> tgraphs;
+  static constexpr int kDynSlots = 64;
+  MmadDyn* dyn_host = nullptr;
+  hipEvent_t dyn_ev[kDynSlots] = {};
+  bool dyn_used[kDynSlots] = {};
+  int dyn_next = 0;
+  bool capturing = false;
+  bool graph_broken = false;
+  void clear_train_graphs() {
+    for (auto& g : tgraphs) (void)hipGraphExecDestroy(g.exec);
+    tgraphs.clear();
+  }
   ~mmad_ae() {
+    clear_train_graphs();
+    for (auto e : dyn_ev)
+      if (e) (void)hipEventDestroy(e);
+    if (dyn_host) (void)hipHostFree(dyn_host);
     for (auto e : probe_ev) (void)hipEventDestroy(e);
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.exec);
     if (gstream) (void)hipStreamDestroy(gstream);
@@ -121,7 +146,8 @@ struct mmad_ae {
 
 struct LayerWS {
   void *out, *y, *dy, *dz;
-  float *stats, *mean, *rstd, *scale, *shift, *bnpart, *dbpart, *rowsq;
+  float *stats, *mean, *rstd, *scale, *shift, *dbpart, *rowsq;
+  double* bnpart;   // fp64 BN-backward column partials [Mp/64][2][Np]
   // consumer of a train-mode BN producer: W*scale (GEMM dtype) and the
   // per-64-column partials of sum_k shift[k] W[n][k]
   void* wf;
@@ -129,6 +155,8 @@ struct LayerWS {
 };
 struct AeWS {
   int B, k, Mpe, Mpd;
+  MmadDyn* dyn_dev = nullptr;    // device slot for the per-call values (graph-captured step)
+  const MmadDyn* dyn = nullptr;  // set: kernels read x / loss / noise / Adam terms from dyn_dev
   void *xin, *zbuf, *dzin;
   float *eps, *klpart, *misc, *lossp;
   int64_t kl_parts;
@@ -181,6 +209,8 @@ static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
     w.klpart = (float*)take(w.kl_parts * 4);
   }
   w.misc = (float*)take(1024 * 4);
+  w.dyn_dev = (MmadDyn*)take(sizeof(MmadDyn));
+  w.dyn = nullptr;
   {
     size_t slab = 0, ctl = 0;
     mmad_gemm_splitk_bytes(0, 0, &slab, &ctl);
@@ -206,7 +236,7 @@ static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
     s.rstd = (float*)take(a.Np * 4);
     s.scale = (float*)take(a.Np * 4);
     s.shift = (float*)take(a.Np * 4);
-    s.bnpart = (float*)take((int64_t)(Mp / 64) * 2 * a.Np * 4);
+    s.bnpart = (double*)take((int64_t)(Mp / 64) * 2 * a.Np * 8);
     s.dbpart = (float*)take((int64_t)(Mp / 128) * a.Np * 4);
     s.rowsq = (float*)take((int64_t)(a.Np / 128) * Mp * 4);
     const bool folded = i > 0 && h->L[i - 1].bn;
@@ -302,6 +332,7 @@ int mmad_ae_bind(mmad_ae* h, float* params, float* grads, float* adam_m, float* 
                  void* shadow, float* running) {
   MMAD_CHECK_ARG(h && params, "ae_bind: null params");
   MMAD_CHECK_ARG(h->dtype != MMAD_BF16 || shadow, "ae_bind: bf16 needs a shadow buffer");
+  h->clear_train_graphs();   // captured steps bake the buffer addresses in
   h->params = params;
   h->grads = grads;
   h->m = adam_m;
@@ -400,7 +431,8 @@ static int ae_gemm(const mmad_ae* h, const AeWS& w, int dt, int epi, const void*
   const int r = (h->side && s == h->side) ? 1 : 0;
   ep.sk_slab = w.sk_slab[r];
   ep.sk_ctl = w.sk_ctl[r];
-  const bool rec = probe >= 0 && probe == h->probe_id && 2 * h->probe_n < (int)h->probe_ev.size();
+  const bool rec = probe >= 0 && probe == h->probe_id && !h->capturing &&
+                   2 * h->probe_n < (int)h->probe_ev.size();
   if (rec) MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n], s));
   const int rc = mmad_gemm_dispatch(dt, epi, A, lda, B, ldb, Mp, Np, K, ep, s, cfg);
   if (rc != MMAD_OK) return rc;
@@ -445,7 +477,7 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
   const int nL = (int)h->L.size();
   const int B = w.B, k = w.k;
   const bool train = mode != 1;
-  RET_IF(mmad_pack_input(dt, B, h->L[0].K, w.Mpe, h->L[0].Kp, x, ld_x, w.xin, st));
+  RET_IF(mmad_pack_input_dyn(dt, B, h->L[0].K, w.Mpe, h->L[0].Kp, x, ld_x, w.xin, w.dyn, st));
   for (int l = 0; l < nL; ++l) {
     const AeLayer& a = h->L[l];
     LayerWS& s = w.l[l];
@@ -463,6 +495,7 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
       ep.tmod = B;
       ep.gscale = 2.0f / (float)k;
       ep.lossp = w.lossp;
+      ep.dyn = w.dyn;
       int cfg = 0;
       RET_IF(ae_gemm(h, w, dt, GEMM_EPI_MSE, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st, &cfg,
                      PROBE_FWD + l));
@@ -501,9 +534,9 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
     }
     if (h->vib && l == h->n_enc - 1) {
       const AeLayer& d0 = h->L[h->n_enc];
-      RET_IF(mmad_vib_reparam_fwd(dt, B, h->btl, k, s.out, a.Np, eps, w.eps, seed, offset,
-                                  mode == 1 ? 1 : 0, w.zbuf, d0.Kp,
-                                  mode == 0 ? w.klpart : nullptr, st));
+      RET_IF(mmad_vib_reparam_fwd_dyn(dt, B, h->btl, k, s.out, a.Np, eps, w.eps, seed, offset,
+                                      mode == 1 ? 1 : 0, w.zbuf, d0.Kp,
+                                      mode == 0 ? w.klpart : nullptr, mode == 0 ? w.dyn : nullptr, st));
     }
   }
   return MMAD_OK;
@@ -647,6 +680,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       dwe.ad_eps = adam->eps;
       dwe.ad_step = adam->step_size;
       dwe.ad_bc2 = adam->bc2_sqrt;
+      dwe.dyn = w.dyn;
       dwe.sm_p = h->params + a.b_off;
       dwe.sm_g = h->grads + a.b_off;
       dwe.sm_m = h->m + a.b_off;
@@ -730,6 +764,7 @@ static int finish_reductions(mmad_ae* h, AeWS& w, bool biases, bool from_mse, fl
     }
   }
   if (n == 0) return MMAD_OK;
+  jobs.dyn = loss_out ? w.dyn : nullptr;
   return mmad_reduce_jobs(jobs, n, max_np, st);
 }
 
@@ -787,6 +822,92 @@ int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const
   if (h->shadow_alt) std::swap(h->shadow, h->shadow_alt);
   return MMAD_OK;
 }
+
+int mmad_ae_train_step_graph(mmad_ae* h, const float* x, int ld_x, int B, int k, const float* eps,
+                             uint64_t seed, uint64_t offset, float beta_kl, float lr, float beta1,
+                             float beta2, float adam_eps, int step, float* loss_out, void* ws,
+                             int64_t ws_bytes, void* stream) {
+  MMAD_CHECK_ARG(h && h->params && h->grads && h->running && h->m && h->v,
+                 "ae_train_step_graph: unbound handle");
+  MMAD_CHECK_ARG(x && ld_x >= h->L[0].K && loss_out, "ae_train_step_graph: bad input");
+  MMAD_CHECK_ARG(step >= 1, "ae_train_step_graph: step must be >= 1");
+  if (h->comm || h->shadow_alt || h->graph_broken)   // eager schedule for these
+    return mmad_ae_train_step(h, x, ld_x, B, k, eps, seed, offset, beta_kl, lr, beta1, beta2,
+                              adam_eps, step, loss_out, ws, ws_bytes, stream);
+  AeWS w;
+  hipStream_t st = (hipStream_t)stream;
+  RET_IF(prepare_ws(h, B, k, ws, ws_bytes, w, st));
+  const AdamHyper ah = adam_hyper(lr, beta1, beta2, adam_eps, step);
+  // this call's values -> pinned slot -> the workspace's device slot
+  if (!h->dyn_host) {
+    MMAD_HIP_CHECK(hipHostMalloc((void**)&h->dyn_host, sizeof(MmadDyn) * mmad_ae::kDynSlots,
+                                 hipHostMallocDefault));
+    for (auto& e : h->dyn_ev) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, kEvFlags));
+  }
+  const int slot = h->dyn_next;
+  h->dyn_next = (slot + 1) % mmad_ae::kDynSlots;
+  if (h->dyn_used[slot]) MMAD_HIP_CHECK(hipEventSynchronize(h->dyn_ev[slot]));
+  MmadDyn& d = h->dyn_host[slot];
+  d.x = x;
+  d.loss = loss_out;
+  d.eps = eps;
+  d.seed = seed;
+  d.offset = offset;
+  d.ad_step = ah.step_size;
+  d.ad_bc2 = ah.bc2_sqrt;
+  MMAD_HIP_CHECK(hipMemcpyAsync(w.dyn_dev, &d, sizeof(MmadDyn), hipMemcpyHostToDevice, st));
+  MMAD_HIP_CHECK(hipEventRecord(h->dyn_ev[slot], st));
+  h->dyn_used[slot] = true;
+  const int xvec = ((uintptr_t)x % 16 == 0 && ld_x % 4 == 0) ? 1 : 0;
+  for (auto& g : h->tgraphs) {
+    if (g.B == B && g.k == k && g.ld_x == ld_x && g.xvec == xvec && g.has_eps == (eps != nullptr) &&
+        g.ws == ws && g.dw_main == h->dw_main && g.ev_every == h->ev_every &&
+        g.keep_grads == h->keep_grads && g.beta_kl == beta_kl && g.b1 == beta1 && g.b2 == beta2 &&
+        g.aeps == adam_eps) {
+      MMAD_HIP_CHECK(hipGraphLaunch(g.exec, st));
+      return MMAD_OK;
+    }
+  }
+  // first call of this signature: run it eagerly (reading the same device
+  // slot; this also settles every GEMM tile choice, which cannot be timed
+  // under capture), then capture the identical launch sequence
+  w.dyn = w.dyn_dev;
+  RET_IF(run_forward(h, w, x, ld_x, 0, eps, seed, offset, st));
+  RET_IF(run_backward(h, w, true, beta_kl, &ah, st));
+  RET_IF(finish_reductions(h, w, false, true, beta_kl, loss_out, st));
+  if (!h->gstream) MMAD_HIP_CHECK(hipStreamCreateWithFlags(&h->gstream, hipStreamNonBlocking));
+  hipGraph_t graph = nullptr;
+  if (hipStreamBeginCapture(h->gstream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    h->graph_broken = true;
+    (void)hipGetLastError();
+    return MMAD_OK;
+  }
+  h->capturing = true;
+  int rc = run_forward(h, w, x, ld_x, 0, eps, seed, offset, h->gstream);
+  if (rc == MMAD_OK) rc = run_backward(h, w, true, beta_kl, &ah, h->gstream);
+  if (rc == MMAD_OK) rc = finish_reductions(h, w, false, true, beta_kl, loss_out, h->gstream);
+  h->capturing = false;
+  const hipError_t ec = hipStreamEndCapture(h->gstream, &graph);
+  hipGraphExec_t exec = nullptr;
+  hipError_t ei = hipErrorUnknown;
+  if (rc == MMAD_OK && ec == hipSuccess && graph) ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  if (graph) (void)hipGraphDestroy(graph);
+  if (rc != MMAD_OK || ec != hipSuccess || ei != hipSuccess) {
+    // this step already ran eagerly; later calls stay eager
+    h->graph_broken = true;
+    (void)hipGetLastError();
+    return MMAD_OK;
+  }
+  if (h->tgraphs.size() >= 16) {
+    (void)hipGraphExecDestroy(h->tgraphs.front().exec);
+    h->tgraphs.erase(h->tgraphs.begin());
+  }
+  h->tgraphs.push_back({B, k, ld_x, xvec, eps != nullptr, h->dw_main, h->ev_every, h->keep_grads, ws,
+                        beta_kl, beta1, beta2, adam_eps, exec});
+  return MMAD_OK;
+}
+
+int mmad_ae_train_graph_count(const mmad_ae* h) { return h ? (int)h->tgraphs.size() : -1; }
 
 int mmad_ae_set_comm(mmad_ae* h, mmad_comm* c) {
   MMAD_CHECK_ARG(h, "ae_set_comm: null handle");

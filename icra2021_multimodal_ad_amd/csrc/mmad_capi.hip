@@ -236,3 +236,18 @@ int mmad_fc_bwd_weight(int dtype, int Mp, int Np, int Kp, const void* dz, const 
   // dW[Np][Kp] = dz^T . x, contraction over the batch; both read MN-major
   return layer_gemm(dtype, GEMM_EPI_BWD_WEIGHT, dz, Np, x, Kp, Np, Kp, Mp, ep, stream);
 }
+
+int mmad_fc_bwd_weight_adam(int dtype, int Mp, int Np, int Kp, const void* dz, const void* x,
+                            float* p, float* m, float* v, void* shadow, float* dw, float beta1,
+                            float beta2, float eps, float step_size, float bc2_sqrt, void* stream) {
+  RET_IF(check_dtype(dtype));
+  RET_IF(check_dims("fc_bwd_weight_adam", Mp, Np, Kp, Mp, Np, Kp));
+  MMAD_CHECK_ARG(dz && x && p && m && v, "fc_bwd_weight_adam: null operand");
+  MMAD_CHECK_ARG(!shadow || dtype == MMAD_BF16, "fc_bwd_weight_adam: the shadow is bf16");
+  GemmEpi ep{};
+  ep.M = Np; ep.N = Kp; ep.out = dw; ep.ldo = Kp;
+  ep.ad_p = p; ep.ad_m = m; ep.ad_v = v; ep.ad_shadow = shadow;
+  ep.ad_b1 = beta1; ep.ad_b2 = beta2; ep.ad_eps = eps; ep.ad_step = step_size; ep.ad_bc2 = bc2_sqrt;
+  ep.dw_nostore = dw ? 0 : 1;
+  return layer_gemm(dtype, GEMM_EPI_BWD_WEIGHT, dz, Np, x, Kp, Np, Kp, Mp, ep, stream);
+}

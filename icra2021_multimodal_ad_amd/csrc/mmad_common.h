@@ -23,6 +23,19 @@ typedef unsigned int uint4v __attribute__((ext_vector_type(4)));
 
 static inline int mmad_roundup(int x, int g) { return (x + g - 1) / g * g; }
 
+// Per-call values of a train step that a captured hipGraph reads from device
+// memory instead of kernel arguments (the executor copies a fresh block in
+// before each replay): the input windows, the loss destination, the VIB noise
+// source and the Adam bias-correction terms of this step.
+struct MmadDyn {
+  const float* x;        // input windows [B][ld_x] (also the MSE target)
+  float* loss;           // loss destination (device fp32 [1])
+  const float* eps;      // injected VIB noise [k][B][btl] or null (Philox)
+  unsigned long long seed, offset;
+  float ad_step, ad_bc2; // Adam lr/(1-b1^t), sqrt(1-b2^t)
+  float pad[2];
+};
+
 // ---- error reporting (thread-local, no exceptions across the ABI) -------
 void mmad_set_error(const char* fmt, ...);
 #define MMAD_CHECK_ARG(cond, ...)                                      \

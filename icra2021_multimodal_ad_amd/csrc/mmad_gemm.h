@@ -50,7 +50,7 @@ struct GemmEpi {
   const void* bn_a;      // pre-BN activation, same shape/ld as out (nullable)
   const float* bn_mean;
   const float* bn_rstd;
-  float* bn_part;        // [Mp/64][2][ldo]: (sum dy, sum dy*xhat)
+  double* bn_part;       // [Mp/64][2][ldo]: (sum dy, sum dy*xhat), fp64
   // MSE: one loss partial (sum d^2) per output tile, [mmad_gemm_ntiles(plan)]
   float* lossp;
   // BWD_WEIGHT: torch.optim.Adam step fused into the epilogue (nullable p).
@@ -79,6 +79,9 @@ struct GemmEpi {
   int splitk;
   int tiles_n, group_m;
   int tile_force;        // caller's tile choice + 1 (0 = none; ignored if it does not fit)
+  // graph-captured step (nullable): MSE target = dyn->x, Adam step terms
+  // from dyn (see MmadDyn)
+  const MmadDyn* dyn;
   int dbg;               // diagnostics (tools/gemm_sweep): 1 skip main loop, 2 skip epilogue,
                          // 4 force the split-K combine's timeout path (tests)
 };

@@ -268,7 +268,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   constexpr int QB = 8;                                // prefetched bias partials per lane
   constexpr int QG = 32;                               // prefetched dW row-sum partials
   constexpr int OSTRIDE = BN * (int)sizeof(TO) + 16;
-  constexpr int OBYTES = BM * OSTRIDE + (EPI == GEMM_EPI_BWD_DATA ? BM * BN / 2 : 0);
+  constexpr int OBYTES = BM * OSTRIDE + (EPI == GEMM_EPI_BWD_DATA ? BM * BN / 2 : 0);   // + fp64 [BM/16][BN]
   constexpr int LDS_BYTES = (NS * SLOT > OBYTES) ? NS * SLOT : OBYTES;
   static_assert((NS - 1) * NL <= 63, "vmcnt range");
   static_assert(LDS_BYTES <= 163840, "LDS budget");
@@ -537,6 +537,16 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
     return;
   }
   // ===================== epilogue, register phase ==========================
+  // per-call values of a graph-captured step come from device memory
+  const float* tgt = ep.target;
+  float ad_step = ep.ad_step, ad_bc2 = ep.ad_bc2;
+  if (ep.dyn) {
+    if constexpr (EPI == GEMM_EPI_MSE) tgt = ep.dyn->x;
+    if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
+      ad_step = ep.dyn->ad_step;
+      ad_bc2 = ep.dyn->ad_bc2;
+    }
+  }
   float db_own = 0.f;                        // db[m0 + tid] (tid < BM, need_db)
   if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
     if (need_db && tid < BM) {
@@ -596,7 +606,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
           s1[i >> 1] += v;
         } else if (EPI == GEMM_EPI_MSE) {
           float d = 0.f;
-          if (valid) d = v + bias - ep.target[(size_t)(row % ep.tmod) * ep.ldt + col];
+          if (valid) d = v + bias - tgt[(size_t)(row % ep.tmod) * ep.ldt + col];
           v = ep.gscale * d;
           s1[i >> 1] += v;
           s2[i >> 1] += d * d;
@@ -712,7 +722,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
         if (!ep.dw_nostore) *(uint4v*)(out + off[u]) = v;
         adam4(P[u], Mm[u], Vv[u], __builtin_bit_cast(floatx4, v), ep.ad_b1, ep.ad_b2, ep.ad_eps,
-              ep.ad_step, ep.ad_bc2);
+              ad_step, ad_bc2);
         *(floatx4*)(ep.ad_p + off[u]) = P[u];
         *(floatx4*)(ep.ad_m + off[u]) = Mm[u];
         *(floatx4*)(ep.ad_v + off[u]) = Vv[u];
@@ -784,7 +794,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         float g = ep.gb_src ? (n < ep.sm_bN ? db_own : 0.f) : ep.sm_g[n];
         if (ep.gb_src) ep.sm_g[n] = g;
         float pp = ep.sm_p[n], mm = ep.sm_m[n], vv = ep.sm_v[n];
-        adam_elem(pp, mm, vv, g, ep.ad_b1, ep.ad_b2, ep.ad_eps, ep.ad_step, ep.ad_bc2);
+        adam_elem(pp, mm, vv, g, ep.ad_b1, ep.ad_b2, ep.ad_eps, ad_step, ad_bc2);
         ep.sm_p[n] = pp;
         ep.sm_m[n] = mm;
         ep.sm_v[n] = vv;
@@ -795,7 +805,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         const floatx4 gg = *(const floatx4*)(ep.sm_g + i4);
         floatx4 pp = *(floatx4*)(ep.sm_p + i4), mm = *(floatx4*)(ep.sm_m + i4);
         floatx4 vv = *(floatx4*)(ep.sm_v + i4);
-        adam4(pp, mm, vv, gg, ep.ad_b1, ep.ad_b2, ep.ad_eps, ep.ad_step, ep.ad_bc2);
+        adam4(pp, mm, vv, gg, ep.ad_b1, ep.ad_b2, ep.ad_eps, ad_step, ad_bc2);
         *(floatx4*)(ep.sm_p + i4) = pp;
         *(floatx4*)(ep.sm_m + i4) = mm;
         *(floatx4*)(ep.sm_v + i4) = vv;
@@ -805,39 +815,52 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   if constexpr (EPI == GEMM_EPI_BWD_DATA) {
     if (ep.bn_part) {
       // sum over rows of dy and dy*xhat, xhat = (a - mean)*rstd, per 64-row
-      // chunk, in one canonical order for every tile configuration: 16-row
-      // pieces summed row by row, then ((p0 + p1) + p2) + p3 per chunk
+      // chunk, in fp64 (torch's CPU BatchNorm backward reduces in double) and
+      // in one canonical order for every tile configuration: 16-row pieces
+      // summed row by row, then ((p0 + p1) + p2) + p3 per chunk.  Pieces
+      // pc = grp, grp + NG, ... of this thread stay in registers; the two sums
+      // go through one [PIECES][BN] fp64 LDS scratch in turn.
       constexpr int NG = NT / BN;      // thread groups per column
       constexpr int PIECES = BM / 16;  // 16-row pieces of the tile
+      constexpr int PPT = (PIECES + NG - 1) / NG;   // pieces per thread
       const int cc = tid % BN, grp = tid / BN;
       const int col = n0 + cc;
-      const float mu = ep.bn_mean[col], rs = ep.bn_rstd[col];
+      const double mu = ep.bn_mean[col], rs = ep.bn_rstd[col];
       const TO* an = (const TO*)ep.bn_a;
-      float* scr = (float*)(smem + BM * OSTRIDE);    // [2][PIECES][BN]
-      for (int pc = grp; pc < PIECES; pc += NG) {
-        float s1 = 0.f, s2 = 0.f;
+      double* scr = (double*)(smem + BM * OSTRIDE);    // [PIECES][BN]
+      double ps1[PPT], ps2[PPT];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int rl = pc * 16 + r;
-          const float dy = to_f32<TO>(*(const TO*)(smem + rl * OSTRIDE + cc * (int)sizeof(TO)));
-          const float av = to_f32<TO>(an[(size_t)(m0 + rl) * ep.ldo + col]);
-          s1 += dy;
-          s2 += dy * (av - mu) * rs;
+      for (int u = 0; u < PPT; ++u) {
+        const int pc = grp + u * NG;
+        double s1 = 0.0, s2 = 0.0;
+        if (pc < PIECES) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rl = pc * 16 + r;
+            const double dy = to_f32<TO>(*(const TO*)(smem + rl * OSTRIDE + cc * (int)sizeof(TO)));
+            const double av = to_f32<TO>(an[(size_t)(m0 + rl) * ep.ldo + col]);
+            s1 += dy;
+            s2 += dy * ((av - mu) * rs);
+          }
         }
-        scr[pc * BN + cc] = s1;
-        scr[(PIECES + pc) * BN + cc] = s2;
+        ps1[u] = s1;
+        ps2[u] = s2;
       }
-      __syncthreads();
-      for (int c4 = grp; c4 < BM / 64; c4 += NG) {
-        float s1 = scr[(4 * c4) * BN + cc], s2 = scr[(PIECES + 4 * c4) * BN + cc];
 #pragma unroll
-        for (int q = 1; q < 4; ++q) {
-          s1 += scr[(4 * c4 + q) * BN + cc];
-          s2 += scr[(PIECES + 4 * c4 + q) * BN + cc];
+      for (int which = 0; which < 2; ++which) {
+#pragma unroll
+        for (int u = 0; u < PPT; ++u) {
+          const int pc = grp + u * NG;
+          if (pc < PIECES) scr[pc * BN + cc] = which ? ps2[u] : ps1[u];
         }
-        float* pp = ep.bn_part + (size_t)((m0 + c4 * 64) / 64) * 2 * ep.ldo;
-        pp[col] = s1;
-        pp[ep.ldo + col] = s2;
+        __syncthreads();
+        for (int c4 = grp; c4 < BM / 64; c4 += NG) {
+          double t = scr[(4 * c4) * BN + cc];
+#pragma unroll
+          for (int q = 1; q < 4; ++q) t += scr[(4 * c4 + q) * BN + cc];
+          ep.bn_part[(size_t)((m0 + c4 * 64) / 64) * 2 * ep.ldo + which * ep.ldo + col] = t;
+        }
+        __syncthreads();
       }
     }
   }

@@ -2,6 +2,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "mmad_common.h"
+
 int mmad_matrix_colsum_partials(int dtype, int M, int Mp, int Np, const void* x, float* part,
                                 void* stream);
 int mmad_sum2d(int rows, int cols, const float* x, int64_t ld, float scale, float* out,
@@ -10,6 +12,13 @@ int mmad_sse_partials(int dtype, int M, int N, int Np, const void* y, const floa
                       float* part, int nparts, void* stream);
 int mmad_to_bf16(int64_t n, const float* x, void* y, void* stream);
 int64_t mmad_vib_kl_parts(int B, int k, int ld_z);
+// as the C-ABI forms, with the per-call values read from `dyn` (nullable)
+int mmad_pack_input_dyn(int dtype, int M, int K, int Mp, int Kp, const float* x, int ld_x,
+                        void* out, const MmadDyn* dyn, void* stream);
+int mmad_vib_reparam_fwd_dyn(int dtype, int B, int btl, int k, const void* enc_out, int ld_enc,
+                             const float* eps, float* eps_out, uint64_t seed, uint64_t offset,
+                             int deterministic, void* z, int ld_z, float* kl_partial,
+                             const MmadDyn* dyn, void* stream);
 
 #define MMAD_MAX_REDUCE_JOBS 24
 struct MmadReduceJob {
@@ -22,7 +31,10 @@ struct MmadReduceJob {
   int n2;
   float scale2;
 };
-struct MmadReduceJobs { MmadReduceJob j[MMAD_MAX_REDUCE_JOBS]; };
+struct MmadReduceJobs {
+  MmadReduceJob j[MMAD_MAX_REDUCE_JOBS];
+  const MmadDyn* dyn;   // non-null: scalar jobs write dyn->loss (graph-captured step)
+};
 int mmad_reduce_jobs(const MmadReduceJobs& jobs, int n_jobs, int max_np, void* stream);
 
 // One Adam segment.  If bsrc != null the first bNp elements take their
@@ -50,6 +62,6 @@ int mmad_bn_finalize_fold(int dtype, int M, int N, int Mp, int Np, const float* 
                           void* wout, float* cpart, void* stream);
 int mmad_bn_act_bwd_apply(int dtype, int act, float slope, int M, int N, int Mp, int Np,
                           const void* dy, const void* a, const float* save_mean,
-                          const float* save_rstd, const float* gamma, const float* part,
+                          const float* save_rstd, const float* gamma, const double* part,
                           int nparts, void* dz, float* dgamma, float* dbeta, float* db_partials,
                           void* stream);

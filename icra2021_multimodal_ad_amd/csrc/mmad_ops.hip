@@ -21,7 +21,7 @@ __global__ void bn_eval_affine_k(int N, int Np, const float* gamma, const float*
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= Np) return;
   if (j < N) {
-    float s = gamma[j] * rsqrtf(rv[j] + eps);
+    float s = gamma[j] * (float)(1.0 / sqrt((double)rv[j] + (double)eps));
     scale[j] = s;
     shift[j] = beta[j] - rm[j] * s;
   } else {
@@ -30,21 +30,22 @@ __global__ void bn_eval_affine_k(int N, int Np, const float* gamma, const float*
   }
 }
 
-// Merge the GEMM-epilogue Welford partials of 64 columns -> (mean, var) in LDS.
+// Merge the GEMM-epilogue Welford partials of 64 columns -> (mean, var) in LDS
+// (the merge in fp64, as torch's CPU BatchNorm accumulates its statistics).
 __device__ void merge_welford(int M, int nparts, const float* stats, int Np, int n0, float* s_mean,
                               float* s_var) {
-  __shared__ float pm[4][SLAB_COLS], pq[4][SLAB_COLS], pn[4][SLAB_COLS];
+  __shared__ double pm[4][SLAB_COLS], pq[4][SLAB_COLS], pn[4][SLAB_COLS];
   const int tid = threadIdx.x, c = tid & 63, grp = tid >> 6;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
   for (int i = grp; i < nparts; i += 4) {
     int cnt = M - i * MMAD_PART_ROWS;
     cnt = cnt < 0 ? 0 : (cnt > MMAD_PART_ROWS ? MMAD_PART_ROWS : cnt);
     if (cnt == 0) continue;
-    const float mb = stats[(size_t)i * 2 * Np + n0 + c];
-    const float qb = stats[((size_t)i * 2 + 1) * Np + n0 + c];
-    const float nb = (float)cnt;
-    const float nn = n + nb;
-    const float d = mb - mean;
+    const double mb = stats[(size_t)i * 2 * Np + n0 + c];
+    const double qb = stats[((size_t)i * 2 + 1) * Np + n0 + c];
+    const double nb = (double)cnt;
+    const double nn = n + nb;
+    const double d = mb - mean;
     mean += d * (nb / nn);
     m2 += qb + d * d * (n * nb / nn);
     n = nn;
@@ -54,18 +55,18 @@ __device__ void merge_welford(int M, int nparts, const float* stats, int Np, int
   pn[grp][c] = n;
   __syncthreads();
   if (tid < SLAB_COLS) {
-    float n1 = 0.f, mu = 0.f, q = 0.f;
+    double n1 = 0.0, mu = 0.0, q = 0.0;
     for (int g = 0; g < 4; ++g) {
-      const float nb = pn[g][tid];
-      if (nb == 0.f) continue;
-      const float nn = n1 + nb;
-      const float d = pm[g][tid] - mu;
+      const double nb = pn[g][tid];
+      if (nb == 0.0) continue;
+      const double nn = n1 + nb;
+      const double d = pm[g][tid] - mu;
       mu += d * (nb / nn);
       q += pq[g][tid] + d * d * (n1 * nb / nn);
       n1 = nn;
     }
-    s_mean[tid] = mu;
-    s_var[tid] = n1 > 0.f ? q / n1 : 0.f;  // biased variance (normalisation)
+    s_mean[tid] = (float)mu;
+    s_var[tid] = n1 > 0.0 ? (float)(q / n1) : 0.f;  // biased variance (normalisation)
   }
   __syncthreads();
 }
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(256) void bn_train_apply_k(int M, int N, int Np, co
     const int col = n0 + tid;
     float sc = 0.f, sh = 0.f;
     if (col < N) {
-      const float rstd = rsqrtf(s_var[tid] + eps);
+      const float rstd = (float)(1.0 / sqrt((double)s_var[tid] + (double)eps));
       sc = gamma[col] * rstd;
       sh = beta[col] - s_mean[tid] * sc;
       if (blockIdx.y == 0) {
@@ -130,7 +131,7 @@ __global__ __launch_bounds__(64) void bn_finalize_k(int M, int N, int Np, const 
                                                     float* scale, float* shift) {
   constexpr int U = 16;
   const int col = blockIdx.x * 64 + threadIdx.x;
-  float n = 0.f, mean = 0.f, m2 = 0.f;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
   for (int i0 = 0; i0 < nparts; i0 += U) {
     float mb[U], qb[U];
 #pragma unroll
@@ -145,15 +146,15 @@ __global__ __launch_bounds__(64) void bn_finalize_k(int M, int N, int Np, const 
       int cnt = M - i * MMAD_PART_ROWS;
       cnt = cnt < 0 ? 0 : (cnt > MMAD_PART_ROWS ? MMAD_PART_ROWS : cnt);
       if (i >= nparts || cnt == 0) continue;
-      const float nb = (float)cnt, nn = n + nb, d = mb[u] - mean;
+      const double nb = (double)cnt, nn = n + nb, d = (double)mb[u] - mean;
       mean += d * (nb / nn);
-      m2 += qb[u] + d * d * (n * nb / nn);
+      m2 += (double)qb[u] + d * d * (n * nb / nn);
       n = nn;
     }
   }
-  const float var = n > 0.f ? m2 / n : 0.f;
+  const float var = n > 0.0 ? (float)(m2 / n) : 0.f;
   if (col < N) {
-    const float rstd = rsqrtf(var + eps);
+    const float rstd = (float)(1.0 / sqrt((double)var + (double)eps));
     const float sc = gamma[col] * rstd;
     save_mean[col] = mean;
     save_rstd[col] = rstd;
@@ -185,7 +186,8 @@ __global__ __launch_bounds__(256) void bn_fold_k(int M, int N, int Np, const flo
                                                  TW* __restrict__ wout, float* __restrict__ cpart,
                                                  int cp_stride) {
   constexpr int U = 8;
-  __shared__ float pm[4][64], pq[4][64], pn[4][64], s_sc[64], s_sh[64];
+  __shared__ double pm[4][64], pq[4][64], pn[4][64];
+  __shared__ float s_sc[64], s_sh[64];
   const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64 * FOLD_RPT, tid = threadIdx.x;
   // W tile loads first (independent of the statistics): rows r + 64 i, 16 columns
   const int r = tid >> 2, cq = (tid & 3) * 16;
@@ -197,7 +199,7 @@ __global__ __launch_bounds__(256) void bn_fold_k(int M, int N, int Np, const flo
       wv[i][u] = *(const floatx4*)(W + (size_t)(n0 + r + 64 * i) * Np + k0 + cq + 4 * u);
   {
     const int c = tid & 63, grp = tid >> 6;
-    float n = 0.f, mean = 0.f, m2 = 0.f;
+    double n = 0.0, mean = 0.0, m2 = 0.0;
     for (int i0 = grp; i0 < nparts; i0 += 4 * U) {
       float mb[U], qb[U];
 #pragma unroll
@@ -212,9 +214,9 @@ __global__ __launch_bounds__(256) void bn_fold_k(int M, int N, int Np, const flo
         int cnt = M - i * MMAD_PART_ROWS;
         cnt = cnt < 0 ? 0 : (cnt > MMAD_PART_ROWS ? MMAD_PART_ROWS : cnt);
         if (i >= nparts || cnt == 0) continue;
-        const float nb = (float)cnt, nn = n + nb, d = mb[u] - mean;
+        const double nb = (double)cnt, nn = n + nb, d = (double)mb[u] - mean;
         mean += d * (nb / nn);
-        m2 += qb[u] + d * d * (n * nb / nn);
+        m2 += (double)qb[u] + d * d * (n * nb / nn);
         n = nn;
       }
     }
@@ -224,21 +226,22 @@ __global__ __launch_bounds__(256) void bn_fold_k(int M, int N, int Np, const flo
   }
   __syncthreads();
   if (tid < 64) {
-    float n1 = 0.f, mu = 0.f, q = 0.f;
+    double n1 = 0.0, mud = 0.0, q = 0.0;
 #pragma unroll
     for (int gq = 0; gq < 4; ++gq) {
-      const float nb = pn[gq][tid];
-      if (nb == 0.f) continue;
-      const float nn = n1 + nb, d = pm[gq][tid] - mu;
-      mu += d * (nb / nn);
+      const double nb = pn[gq][tid];
+      if (nb == 0.0) continue;
+      const double nn = n1 + nb, d = pm[gq][tid] - mud;
+      mud += d * (nb / nn);
       q += pq[gq][tid] + d * d * (n1 * nb / nn);
       n1 = nn;
     }
-    const float var = n1 > 0.f ? q / n1 : 0.f;
+    const float mu = (float)mud;
+    const float var = n1 > 0.0 ? (float)(q / n1) : 0.f;
     const int col = k0 + tid;
     float sc = 0.f, sh = 0.f;
     if (col < N) {
-      const float rstd = rsqrtf(var + eps);
+      const float rstd = (float)(1.0 / sqrt((double)var + (double)eps));
       sc = gamma[col] * rstd;
       sh = beta[col] - mu * sc;
       if (blockIdx.y == 0) {
@@ -293,18 +296,18 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(int M, int Np, const T* _
                                                        const T* __restrict__ a,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ rstd,
-                                                       float* __restrict__ part) {
+                                                       double* __restrict__ part) {
   constexpr int V = Vec<T>::N;
   constexpr int CPR = SLAB_COLS / V;
   constexpr int RG = 256 / CPR;  // row groups
-  __shared__ float s1[RG][SLAB_COLS], s2[RG][SLAB_COLS];
+  __shared__ double s1[RG][SLAB_COLS], s2[RG][SLAB_COLS];
   const int n0 = blockIdx.x * SLAB_COLS, r0 = blockIdx.y * SLAB_ROWS, tid = threadIdx.x;
   const int ch = tid % CPR, rg = tid / CPR;
-  float acc1[V], acc2[V], mu[V], rs[V];
+  double acc1[V], acc2[V], mu[V], rs[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) {
-    acc1[k] = 0.f;
-    acc2[k] = 0.f;
+    acc1[k] = 0.0;
+    acc2[k] = 0.0;
     mu[k] = mean[n0 + ch * V + k];
     rs[k] = rstd[n0 + ch * V + k];
   }
@@ -318,9 +321,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(int M, int Np, const T* _
     const T* pa = (const T*)&ra;
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      const float d = to_f32<T>(pd[k]);
+      const double d = to_f32<T>(pd[k]);
       acc1[k] += d;
-      acc2[k] += d * (to_f32<T>(pa[k]) - mu[k]) * rs[k];
+      acc2[k] += d * (((double)to_f32<T>(pa[k]) - mu[k]) * rs[k]);
     }
   }
 #pragma unroll
@@ -330,7 +333,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(int M, int Np, const T* _
   }
   __syncthreads();
   if (tid < SLAB_COLS) {
-    float t1 = 0.f, t2 = 0.f;
+    double t1 = 0.0, t2 = 0.0;
     for (int g = 0; g < RG; ++g) { t1 += s1[g][tid]; t2 += s2[g][tid]; }
     part[((size_t)blockIdx.y * 2) * Np + n0 + tid] = t1;
     part[((size_t)blockIdx.y * 2 + 1) * Np + n0 + tid] = t2;
@@ -348,7 +351,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
                                                       const float* __restrict__ mean,
                                                       const float* __restrict__ rstd,
                                                       const float* __restrict__ gamma,
-                                                      const float* __restrict__ part,
+                                                      const double* __restrict__ part,
                                                       T* __restrict__ dz, float* __restrict__ dgamma,
                                                       float* __restrict__ dbeta, float* __restrict__ dbpart) {
   constexpr int V = Vec<T>::N;
@@ -356,8 +359,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
   constexpr int RG = 256 / CPR;           // row groups
   constexpr int RPT = SLAB_ROWS / RG;     // rows per thread
   constexpr int PU = 8;                   // partial chunks per group loaded at once
-  __shared__ float s_red[RG][SLAB_COLS];
-  __shared__ float s_p1[4][SLAB_COLS], s_p2[4][SLAB_COLS];
+  __shared__ double s_red[RG][SLAB_COLS];
+  __shared__ double s_p1[4][SLAB_COLS], s_p2[4][SLAB_COLS];
   const int n0 = blockIdx.x * SLAB_COLS, r0 = blockIdx.y * SLAB_ROWS, tid = threadIdx.x;
   const int ch = tid % CPR, rg = tid / CPR;
   // (1) this thread's dy / a rows
@@ -380,9 +383,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
   // (3) partial sums: 4 groups of 64 columns, group g sums chunks g, g+4, ...
   {
     const int c = tid & 63, grp = tid >> 6;
-    float t1 = 0.f, t2 = 0.f;
+    double t1 = 0.0, t2 = 0.0;
     for (int i0 = grp; i0 < nparts; i0 += 4 * PU) {
-      float p1[PU], p2[PU];
+      double p1[PU], p2[PU];
 #pragma unroll
       for (int u = 0; u < PU; ++u) {
         const int i = i0 + 4 * u < nparts ? i0 + 4 * u : grp;
@@ -398,24 +401,27 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
   }
   __syncthreads();
   if (tid < SLAB_COLS) {
-    float t1 = ((s_p1[0][tid] + s_p1[1][tid]) + s_p1[2][tid]) + s_p1[3][tid];
-    float t2 = ((s_p2[0][tid] + s_p2[1][tid]) + s_p2[2][tid]) + s_p2[3][tid];
+    double t1 = ((s_p1[0][tid] + s_p1[1][tid]) + s_p1[2][tid]) + s_p1[3][tid];
+    double t2 = ((s_p2[0][tid] + s_p2[1][tid]) + s_p2[2][tid]) + s_p2[3][tid];
     const int col = n0 + tid;
-    if (col >= N) { t1 = 0.f; t2 = 0.f; }
+    if (col >= N) { t1 = 0.0; t2 = 0.0; }
     s_p1[0][tid] = t1;
     s_p2[0][tid] = t2;
-    if (blockIdx.y == 0) { dbeta[col] = t1; dgamma[col] = t2; }
+    if (blockIdx.y == 0) { dbeta[col] = (float)t1; dgamma[col] = (float)t2; }
   }
   __syncthreads();
-  const float invM = 1.f / (float)M;
-  float cf[V], dbv[V], dgv[V], accb[V];
+  // da = gamma rstd / M (M dy - sum dy - xhat sum dy xhat): the bracket nearly
+  // cancels, so it is evaluated in fp64 (as the reference's CPU BatchNorm
+  // backward does its reductions); dz and its column sums follow in fp64 too
+  const double invM = 1.0 / (double)M;
+  double cf[V], dbv[V], dgv[V], accb[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) {
     const int col = n0 + ch * V + k;
-    cf[k] = col < N ? gm[k] * rs[k] * invM : 0.f;
+    cf[k] = col < N ? (double)gm[k] * (double)rs[k] * invM : 0.0;
     dbv[k] = s_p1[0][ch * V + k];
     dgv[k] = s_p2[0][ch * V + k];
-    accb[k] = 0.f;
+    accb[k] = 0.0;
   }
 #pragma unroll
   for (int i = 0; i < RPT; ++i) {
@@ -427,13 +433,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       const float av = to_f32<T>(pa[k]);
-      const float xh = (av - mu[k]) * rs[k];
-      float da = cf[k] * ((float)M * to_f32<T>(pd[k]) - dbv[k] - xh * dgv[k]);
-      float d = da * act_grad_from_out(av, act, slope);
+      const double xh = ((double)av - (double)mu[k]) * (double)rs[k];
+      const double da = cf[k] * ((double)M * (double)to_f32<T>(pd[k]) - dbv[k] - xh * dgv[k]);
+      float d = (float)(da * (double)act_grad_from_out(av, act, slope));
       d = row < M ? d : 0.f;
       const T dt = from_f32<T>(d);
       po[k] = dt;
-      accb[k] += to_f32<T>(dt);
+      accb[k] += (double)to_f32<T>(dt);
     }
     *(uint4v*)(dz + (size_t)row * Np + n0 + ch * V) = ro;
   }
@@ -441,9 +447,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
   for (int k = 0; k < V; ++k) s_red[rg][ch * V + k] = accb[k];
   __syncthreads();
   if (tid < SLAB_COLS) {
-    float t = 0.f;
+    double t = 0.0;
     for (int g = 0; g < RG; ++g) t += s_red[g][tid];
-    dbpart[(size_t)blockIdx.y * Np + n0 + tid] = t;
+    dbpart[(size_t)blockIdx.y * Np + n0 + tid] = (float)t;
   }
 }
 
@@ -509,8 +515,9 @@ __global__ __launch_bounds__(1024) void sum2d_k(int rows, int cols, const float*
 
 template <typename T>
 __global__ void pack_input_k(int M, int K, int Mp, int Kp, const float* __restrict__ x, int ldx,
-                             int vec, T* __restrict__ out) {
+                             int vec, T* __restrict__ out, const MmadDyn* __restrict__ dyn) {
   constexpr int V = Vec<T>::N;
+  if (dyn) x = dyn->x;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int cpr = Kp / V;
   if (idx >= (int64_t)Mp * cpr) return;
@@ -616,7 +623,7 @@ __global__ __launch_bounds__(256) void reduce_jobs_k(MmadReduceJobs jobs) {
     t = wave_sum(t);
     if ((tid & 63) == 0) red[tid >> 6] = t;
     __syncthreads();
-    if (tid == 0) jb.dst[0] = red[0] + red[1] + red[2] + red[3];
+    if (tid == 0) (jobs.dyn ? jobs.dyn->loss : jb.dst)[0] = red[0] + red[1] + red[2] + red[3];
     return;
   }
   const int j = blockIdx.x * 256 + tid;
@@ -696,10 +703,16 @@ __global__ __launch_bounds__(256) void vib_fwd_k(int B, int btl, int k, const T*
                                                  int ld_enc, const float* __restrict__ eps,
                                                  float* __restrict__ eps_out, uint64_t seed,
                                                  uint64_t offset, int det, T* __restrict__ z,
-                                                 int ld_z, int Mpz, float* kl_part) {
+                                                 int ld_z, int Mpz, float* kl_part,
+                                                 const MmadDyn* __restrict__ dyn) {
   // one thread per element of the packed z buffer [Mpz][ld_z]; rows < B also
   // contribute the KL term of their (mu, logvar) pair.
   __shared__ float red[4];
+  if (dyn) {
+    eps = dyn->eps;
+    seed = dyn->seed;
+    offset = dyn->offset;
+  }
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t total = (int64_t)Mpz * ld_z;
   float kl = 0.f;
@@ -852,7 +865,7 @@ int mmad_adam2(const MmadAdamSeg& s0, const MmadAdamSeg& s1, float beta1, float 
 
 int mmad_bn_act_bwd_apply(int dtype, int act, float slope, int M, int N, int Mp, int Np,
                           const void* dy, const void* a, const float* save_mean,
-                          const float* save_rstd, const float* gamma, const float* part,
+                          const float* save_rstd, const float* gamma, const double* part,
                           int nparts, void* dz, float* dgamma, float* dbeta, float* db_partials,
                           void* stream) {
   dim3 grd(Np / SLAB_COLS, Mp / SLAB_ROWS);
@@ -869,7 +882,7 @@ int mmad_bn_act_bwd_apply(int dtype, int act, float slope, int M, int N, int Mp,
   return MMAD_OK;
 }
 
-size_t mmad_bn_act_bwd_ws(int Mp, int Np) { return (size_t)(Mp / SLAB_ROWS) * 2 * Np * sizeof(float); }
+size_t mmad_bn_act_bwd_ws(int Mp, int Np) { return (size_t)(Mp / SLAB_ROWS) * 2 * Np * sizeof(double); }
 
 int mmad_bn_act_bwd(int dtype, int act, float slope, int M, int N, int Mp, int Np, const void* dy,
                     const void* a, const float* save_mean, const float* save_rstd,
@@ -879,7 +892,7 @@ int mmad_bn_act_bwd(int dtype, int act, float slope, int M, int N, int Mp, int N
                  "bn_act_bwd: bad sizes");
   dim3 grd(Np / SLAB_COLS, Mp / SLAB_ROWS);
   hipStream_t s = (hipStream_t)stream;
-  float* part = (float*)ws;
+  double* part = (double*)ws;
   const int nparts = Mp / SLAB_ROWS;
   if (dtype == MMAD_BF16) {
     bn_bwd_reduce_k<bf16><<<grd, 256, 0, s>>>(M, Np, (const bf16*)dy, (const bf16*)a, save_mean,
@@ -933,20 +946,27 @@ int mmad_sum(int64_t n, const float* x, float scale, float* out, int accumulate,
   return mmad_sum2d(1, (int)n, x, n, scale, out, accumulate, stream);
 }
 
-int mmad_pack_input(int dtype, int M, int K, int Mp, int Kp, const float* x, int ld_x, void* out,
-                    void* stream) {
+int mmad_pack_input_dyn(int dtype, int M, int K, int Mp, int Kp, const float* x, int ld_x,
+                        void* out, const MmadDyn* dyn, void* stream) {
   MMAD_CHECK_ARG(M <= Mp && K <= Kp && Kp % 8 == 0 && ld_x >= K, "pack_input: bad sizes");
   hipStream_t s = (hipStream_t)stream;
+  // with dyn the source is read at run time: x is the current call's value
+  // (same alignment class is required of every later replay, see mmad_ae)
   const int vec = ((uintptr_t)x % 16 == 0 && ld_x % 4 == 0) ? 1 : 0;
   if (dtype == MMAD_BF16) {
     const int64_t n = (int64_t)Mp * (Kp / 8);
-    pack_input_k<bf16><<<nblk(n, 256), 256, 0, s>>>(M, K, Mp, Kp, x, ld_x, vec, (bf16*)out);
+    pack_input_k<bf16><<<nblk(n, 256), 256, 0, s>>>(M, K, Mp, Kp, x, ld_x, vec, (bf16*)out, dyn);
   } else {
     const int64_t n = (int64_t)Mp * (Kp / 4);
-    pack_input_k<float><<<nblk(n, 256), 256, 0, s>>>(M, K, Mp, Kp, x, ld_x, vec, (float*)out);
+    pack_input_k<float><<<nblk(n, 256), 256, 0, s>>>(M, K, Mp, Kp, x, ld_x, vec, (float*)out, dyn);
   }
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
+}
+
+int mmad_pack_input(int dtype, int M, int K, int Mp, int Kp, const float* x, int ld_x, void* out,
+                    void* stream) {
+  return mmad_pack_input_dyn(dtype, M, K, Mp, Kp, x, ld_x, out, nullptr, stream);
 }
 
 int mmad_unpack_output(int dtype, int M, int N, int Np, const void* y, float* out, int ld_out,
@@ -997,6 +1017,14 @@ int mmad_to_bf16(int64_t n, const float* x, void* y, void* stream) {
 int mmad_vib_reparam_fwd(int dtype, int B, int btl, int k, const void* enc_out, int ld_enc,
                          const float* eps, float* eps_out, uint64_t seed, uint64_t offset,
                          int deterministic, void* z, int ld_z, float* kl_partial, void* stream) {
+  return mmad_vib_reparam_fwd_dyn(dtype, B, btl, k, enc_out, ld_enc, eps, eps_out, seed, offset,
+                                  deterministic, z, ld_z, kl_partial, nullptr, stream);
+}
+
+int mmad_vib_reparam_fwd_dyn(int dtype, int B, int btl, int k, const void* enc_out, int ld_enc,
+                             const float* eps, float* eps_out, uint64_t seed, uint64_t offset,
+                             int deterministic, void* z, int ld_z, float* kl_partial,
+                             const MmadDyn* dyn, void* stream) {
   MMAD_CHECK_ARG(B >= 1 && btl >= 1 && k >= 1 && ld_enc >= 2 * btl && ld_z >= btl,
                  "vib_reparam_fwd: bad sizes");
   const int Mpz = mmad_roundup(k * B, MMAD_PAD);
@@ -1005,11 +1033,11 @@ int mmad_vib_reparam_fwd(int dtype, int B, int btl, int k, const void* enc_out, 
   if (dtype == MMAD_BF16)
     vib_fwd_k<bf16><<<nblk(n, 256), 256, 0, s>>>(B, btl, k, (const bf16*)enc_out, ld_enc, eps,
                                                  eps_out, seed, offset, deterministic, (bf16*)z,
-                                                 ld_z, Mpz, kl_partial);
+                                                 ld_z, Mpz, kl_partial, dyn);
   else
     vib_fwd_k<float><<<nblk(n, 256), 256, 0, s>>>(B, btl, k, (const float*)enc_out, ld_enc, eps,
                                                   eps_out, seed, offset, deterministic, (float*)z,
-                                                  ld_z, Mpz, kl_partial);
+                                                  ld_z, Mpz, kl_partial, dyn);
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
 }

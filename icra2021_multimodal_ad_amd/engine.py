@@ -66,6 +66,7 @@ class NativeAE:
         # differentiable forward records it and its backward checks it
         self.gen = 0
         self.adam_step_count = 0
+        self.use_graph = os.environ.get("MMAD_TRAIN_GRAPH", "1") != "0"
 
     # ------------------------------------------------------------------ memory
     def _alloc(self, device, src=None):
@@ -249,7 +250,11 @@ class NativeAE:
             assert eps.numel() == k * B * self.btl
         self.adam_step_count += 1
         self.gen += 1
-        call("mmad_ae_train_step", self._h, ptr(x), x.stride(0), B, int(k), ptr(eps), int(seed),
+        # one replayed hipGraph per step (mmad_ae_train_step_graph) unless
+        # MMAD_TRAIN_GRAPH=0; the executor falls back to the eager schedule
+        # where capture does not apply (data parallel, shadow pair)
+        fn = "mmad_ae_train_step_graph" if self.use_graph else "mmad_ae_train_step"
+        call(fn, self._h, ptr(x), x.stride(0), B, int(k), ptr(eps), int(seed),
              int(offset), float(beta_kl), float(lr), float(betas[0]), float(betas[1]),
              float(adam_eps), int(self.adam_step_count), ptr(loss_out), ws, nb, stream_ptr())
         self._mark_synced()

@@ -30,7 +30,7 @@ from .reconstruction_aggregation import (NapScorer, base_from_layer_sq, sap_from
 
 def _layer_sq(model, x, batch_size):
     return score_windows(x.to(model._native.device).float().contiguous(), model,
-                         batch_size=batch_size)
+                         batch_size=batch_size, graph=False)
 
 
 def _device_diffs(model, x, batch_size):
@@ -92,6 +92,8 @@ class NoveltyDetecter:
             test_y = np.where(np.isin(test_y, [cfg.target_class]), False, True)
         else:
             test_y = np.where(np.isin(test_y, [cfg.target_class]), True, False)
+        self.model = model
+        self.last_inputs = (train_x, valid_x, test_x, test_y)
         sc = self.scores(model, train_x, valid_x, test_x)
         row = {}
         res = {}

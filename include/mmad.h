@@ -140,6 +140,16 @@ int mmad_fc_bwd_data(int dtype, int M, int N, int K, int Mp, int Np, int Kp, con
 int mmad_fc_bwd_weight(int dtype, int Mp, int Np, int Kp, const void* dz, const void* x,
                        float* dw, void* stream);
 
+/* dW as mmad_fc_bwd_weight with torch.optim.Adam's step (as mmad_adam) fused
+ * into the GEMM epilogue (loss.backward() + optimizer.step() for one
+ * nn.Linear weight, models/auto_encoder.py:73-75): p/m/v fp32 [Np][Kp] are
+ * updated in place, shadow (nullable, bf16 [Np][Kp]) receives bf16(p), dw
+ * (nullable) the gradient itself.  Padding rows/columns of p/m/v must be zero
+ * (they stay zero: their gradient is zero). */
+int mmad_fc_bwd_weight_adam(int dtype, int Mp, int Np, int Kp, const void* dz, const void* x,
+                            float* p, float* m, float* v, void* shadow, float* dw, float beta1,
+                            float beta2, float eps, float step_size, float bc2_sqrt, void* stream);
+
 /* Backward of BN(train) o Activation (layers/fc_layer.py:38-45):
  * dbeta = sum dy, dgamma = sum dy*xhat, da = gamma*rstd/M*(M dy - dbeta - xhat dgamma),
  * dz = da * act'(a).  Writes dz (dtype), dgamma/dbeta (fp32 [Np]) and db
@@ -259,6 +269,21 @@ int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const
                        uint64_t seed, uint64_t offset, float beta_kl, float lr, float beta1,
                        float beta2, float adam_eps, int step, float* loss_out, void* ws,
                        int64_t ws_bytes, void* stream);
+
+/* mmad_ae_train_step replayed as ONE captured hipGraph (the whole step's
+ * ~45 kernels, side-stream dW/Adam overlap included) after a 64-byte
+ * host->device copy of this call's values (x, loss_out, eps, seed/offset, the
+ * Adam bias-correction terms of `step`): same arguments, same results bit for
+ * bit.  The first call of a signature (B, k, ld_x, x alignment, eps given or
+ * not, ws, beta_kl, Adam betas/eps) runs eagerly and captures; rebinding the
+ * buffers drops the captures.  With a communicator or a shadow pair attached,
+ * or if capture is unavailable, it runs the eager step instead. */
+int mmad_ae_train_step_graph(mmad_ae* h, const float* x, int ld_x, int B, int k, const float* eps,
+                             uint64_t seed, uint64_t offset, float beta_kl, float lr, float beta1,
+                             float beta2, float adam_eps, int step, float* loss_out, void* ws,
+                             int64_t ws_bytes, void* stream);
+/* number of captured train-step graphs (-1 for a null handle) */
+int mmad_ae_train_graph_count(const mmad_ae* h);
 
 /* loss.backward() after mmad_ae_forward(train_bn=1) on the same workspace
  * (autograd path of AutoEncoder.forward): dxhat fp32 [B][ld] = dL/dx_hat;

@@ -134,6 +134,43 @@ def run_reference(seed):
     return out
 
 
+def run_oracle(seed):
+    """The same training + scoring with the CPU oracle (oracle/ae_oracle.py, an
+    independent fp32 restatement pinned to the reference's goldens): how far
+    ANY independent fp32 implementation lands from the reference after
+    n_epochs of Adam (summation-order noise amplified by training)."""
+    from oracle import ae_oracle as O
+    from oracle.model_io import model_from_state_dict
+    cfg = config_for(seed)
+    m = model_from_state_dict(init_state_dict(cfg.input_size, cfg.btl_size, cfg.n_layers,
+                                              seed=cfg.model_seed))
+    dset, train_loader, valid_loader, test_loader = get_loaders(cfg, device="cpu")
+    st, train_hist, lowest, best = {}, [], np.inf, None
+    for epoch in range(1, cfg.n_epochs + 1):
+        ema = None
+        for x, _ in train_loader:
+            ema = ema_update(ema, O.train_step(x.numpy(), m, st))
+        train_hist.append(ema)
+        vema = None
+        for x, _ in valid_loader:
+            xh, _ = O.ae_forward(x.numpy(), m, train=False)
+            vema = ema_update(vema, O.mse_sum(xh, x.numpy()))
+        if vema < lowest:
+            lowest, best = vema, deepcopy(m)
+    tr_x, _ = dset.get_transformed_data(train_loader)
+    va_x, _ = dset.get_transformed_data(valid_loader)
+    te_x, te_y = dset.get_transformed_data(test_loader)
+    lab = np.isin(np.asarray(te_y), [cfg.target_class])
+    tr = O.get_diffs(tr_x.numpy(), best, batch_size=cfg.batch_size)
+    te = O.get_diffs(te_x.numpy(), best)
+    out = {"oracle/train_history": np.asarray(train_hist, np.float64),
+           "oracle/base/auroc": np.float64(O.auroc(O.base_score(te), lab)),
+           "oracle/sap/auroc": np.float64(O.auroc(O.sap_score(te), lab))}
+    fit = O.nap_fit(np.concatenate(tr, axis=1))
+    out["oracle/nap/auroc"] = np.float64(O.auroc(O.nap_score(np.concatenate(te, axis=1), fit), lab))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seeds", type=int, nargs="+", default=[0, 1, 2])
@@ -144,10 +181,12 @@ def main():
     for s in a.seeds:
         t0 = time.time()
         o = run_reference(s)
+        o.update(run_oracle(s))
         res.update({f"s{s}/{k}": v for k, v in o.items()})
         print(f"seed {s}: {time.time() - t0:.0f} s  best epoch {int(o['best_epoch'])}  "
               f"AUROC base {float(o['base/auroc']):.4f} sap {float(o['sap/auroc']):.4f} "
-              f"nap {float(o['nap/auroc']):.4f}", flush=True)
+              f"nap {float(o['nap/auroc']):.4f}; oracle base {float(o['oracle/base/auroc']):.4f} "
+              f"sap {float(o['oracle/sap/auroc']):.4f} nap {float(o['oracle/nap/auroc']):.4f}", flush=True)
     np.savez_compressed(os.path.join(HERE, "e2e.npz"), **res)
 
 

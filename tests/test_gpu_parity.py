@@ -493,3 +493,28 @@ def test_differentiable_forward_guards_its_saved_activations(golden):
         l3 = m.get_loss_value(x, x)
         l3.backward(retain_graph=True)
         l3.backward()                               # a second backward reuses consumed state
+
+
+@pytest.mark.parametrize("dtype,models", [("f32", "ae"), ("bf16", "ae"), ("bf16", "vib_ae")])
+def test_graph_step_equals_eager_step(dtype, models, monkeypatch):
+    """mmad_ae_train_step_graph (whole step captured once, replayed with the
+    per-call values copied in) == the eager mmad_ae_train_step, bit for bit,
+    over steps with changing inputs, Adam step counts and VIB noise offsets."""
+    from icra2021_multimodal_ad_amd import _native
+    d, btl, nl = 700, 40, 5
+    enc_out = 2 * btl if models == "vib_ae" else None
+    sd = init_state_dict(d, btl, nl, seed=71, enc_out=enc_out)
+    xs = [torch.from_numpy(synth_windows(384, d, seed=80 + i)).cuda() for i in range(4)]
+    res = {}
+    for graph in (False, True):
+        m, _ = _model(d, btl, nl, sd, dtype=dtype, models=models)
+        m._native.use_graph = graph
+        losses = [float(m.train_step_async(xs[i % 4])) for i in range(7)]
+        nat = m._native
+        res[graph] = (losses, nat.params.clone(), nat.exp_avg.clone(), nat.exp_avg_sq.clone(),
+                      nat.running.clone())
+        if graph:
+            assert nat._lib.mmad_ae_train_graph_count(nat._h) == 1
+    for a, b in zip(res[False][1:], res[True][1:]):
+        assert torch.equal(a, b)
+    assert res[False][0] == res[True][0]
