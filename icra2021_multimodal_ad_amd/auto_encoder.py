@@ -118,6 +118,7 @@ class AutoEncoder(AbstractModel):
         self.__dict__.pop("_plist_cache", None)
         for l, layer in enumerate(self._layers()):
             layer.mmad_dtype = self.mmad_dtype
+            layer._flat = (nat, l)          # standalone layer calls use the padded buffers
             w, b, g, be = nat.param_views(nat.params, l)
             gw, gb, gg, gbe = nat.param_views(nat.grads, l)
             layer.layer.weight.data = w
@@ -210,10 +211,17 @@ class AutoEncoder(AbstractModel):
         """models/auto_encoder.py:46-50 (x_hat = dec(enc(x))) as one fused
         native pass; differentiable in train mode."""
         x2 = x.reshape(x.size(0), -1)
-        if self.training and torch.is_grad_enabled() and not self.vib:
+        if self.training and torch.is_grad_enabled():
             params = self._param_list()
             if any(p.requires_grad for p in params):
-                return _AEFunction.apply(x2, self, *params).view(x.size(0), -1)
+                if not self.vib:
+                    return _AEFunction.apply(x2, self, *params).view(x.size(0), -1)
+                # VIB-AE: layer by layer through the differentiable FCLayer /
+                # reparameterisation ops; the reconstruction of the k samples
+                # is averaged (k = 1: dec(z))
+                out = self.encoder(x2, distribution="normal", k=self.k)
+                xh = self.decoder(out["z"])
+                return xh.mean(dim=0).view(x.size(0), -1)
         xh, _ = self._native.forward(x2, train_bn=self.training)
         if self.training:
             self._count_bn_step()

@@ -83,6 +83,13 @@ struct mmad_ae {
     const char* e = getenv("MMAD_KEEP_GRADS");
     return e ? atoi(e) : 0;
   }();
+  // train-mode BN: fold the batch statistics into the consumer's weights
+  // (bn_fold_k; the bf16 throughput path) or normalise the activations into y
+  // (bn_train_apply_k; the exact-fp32 parity path: folding contracts the raw,
+  // un-centred activations and cancels the mean back out, which costs the
+  // fp32 path ~10x the reference's rounding error on BN-producer layers).
+  // Set at create from the dtype; MMAD_BN_FOLD=0/1 overrides.
+  int fold = 1;
   // fused step: record the "bwd-data of l done" event only every ev_every-th
   // side-stream layer (each record costs a bubble on the main stream); the dW
   // GEMMs of the layers in between wait for the next recorded one
@@ -270,6 +277,10 @@ int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, i
   h->slope = slope;
   h->bn_eps = bn_eps;
   h->bn_mom = bn_momentum;
+  {
+    const char* e = getenv("MMAD_BN_FOLD");
+    h->fold = e ? (atoi(e) != 0) : (dtype == MMAD_BF16);
+  }
   for (int side = 0; side < 2; ++side) {
     const int n = side == 0 ? n_enc : n_dec;
     const int* wd = side == 0 ? enc_widths : dec_widths;
@@ -399,7 +410,7 @@ static const void* input_of(const mmad_ae* h, const AeWS& w, int l, bool train,
   const AeLayer& p = h->L[l - 1];
   const LayerWS& ps = w.l[l - 1];
   if (!p.bn) return ps.out;
-  if (!train) return ps.y;
+  if (!train || !h->fold) return ps.y;
   *scale = ps.scale;
   *shift = ps.shift;
   return ps.out;
@@ -505,7 +516,13 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
       ep.part = s.stats;
       RET_IF(ae_gemm(h, w, dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st, nullptr,
                      PROBE_FWD + l));
-      if (l + 1 < nL) {
+      if (!h->fold) {
+        // exact-fp32 path: normalise into y (the consumer GEMM and its dW read
+        // y as the reference's layers do: no fold, no fix-up cancellation)
+        RET_IF(mmad_bn_train_apply(dt, M, a.N, Mp, a.Np, s.out, s.stats, h->params + a.g_off,
+                                   h->params + a.be_off, running_mean(h, a), running_var(h, a),
+                                   h->bn_mom, h->bn_eps, s.mean, s.rstd, s.y, st));
+      } else if (l + 1 < nL) {
         // statistics -> (scale, shift) -> folded into layer l+1's weights/bias
         const AeLayer& c = h->L[l + 1];
         LayerWS& cs = w.l[l + 1];

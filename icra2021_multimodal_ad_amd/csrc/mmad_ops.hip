@@ -453,6 +453,50 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
   }
 }
 
+// Activation backward without BatchNorm (an FCLayer with bn=False):
+// dz = dy * act'(a) from the activation OUTPUT a, plus the per-slab column
+// sums of dz (the bias gradient) -> db partials [Mp/128][Np]
+template <typename T>
+__global__ __launch_bounds__(256) void act_bwd_k(int act, float slope, int M, int Np,
+                                                 const T* __restrict__ dy, const T* __restrict__ a,
+                                                 T* __restrict__ dz, float* __restrict__ dbpart) {
+  constexpr int V = Vec<T>::N;
+  constexpr int CPR = SLAB_COLS / V;
+  constexpr int RG = 256 / CPR;
+  __shared__ double s_red[RG][SLAB_COLS];
+  const int n0 = blockIdx.x * SLAB_COLS, r0 = blockIdx.y * SLAB_ROWS, tid = threadIdx.x;
+  const int ch = tid % CPR, rg = tid / CPR;
+  double acc[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) acc[k] = 0.0;
+  for (int rl = rg; rl < SLAB_ROWS; rl += RG) {
+    const int row = r0 + rl;
+    const size_t off = (size_t)row * Np + n0 + ch * V;
+    const uint4v rd = *(const uint4v*)(dy + off);
+    const uint4v ra = *(const uint4v*)(a + off);
+    const T* pd = (const T*)&rd;
+    const T* pa = (const T*)&ra;
+    uint4v ro;
+    T* po = (T*)&ro;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float d = to_f32<T>(pd[k]) * act_grad_from_out(to_f32<T>(pa[k]), act, slope);
+      d = row < M ? d : 0.f;
+      po[k] = from_f32<T>(d);
+      acc[k] += (double)to_f32<T>(po[k]);
+    }
+    *(uint4v*)(dz + off) = ro;
+  }
+#pragma unroll
+  for (int k = 0; k < V; ++k) s_red[rg][ch * V + k] = acc[k];
+  __syncthreads();
+  if (tid < SLAB_COLS) {
+    double t = 0.0;
+    for (int g = 0; g < RG; ++g) t += s_red[g][tid];
+    dbpart[(size_t)blockIdx.y * Np + n0 + tid] = (float)t;
+  }
+}
+
 // column sums of a packed matrix -> partials [Mp/128][Np]
 template <typename T>
 __global__ __launch_bounds__(256) void matrix_colsum_k(int M, int Np, const T* __restrict__ x,
@@ -1064,5 +1108,21 @@ int mmad_vib_reparam_bwd(int dtype, int B, int btl, int k, const void* enc_out, 
                                                   (float*)d_enc_out, ld_denc, Mpe);
   MMAD_LAUNCH_CHECK();
   if (colsum) return mmad_matrix_colsum_partials(dtype, B, Mpe, ld_denc, d_enc_out, colsum, stream);
+  return MMAD_OK;
+}
+
+int mmad_act_bwd(int dtype, int act, float slope, int M, int Mp, int Np, const void* dy,
+                 const void* a, void* dz, float* db_partials, void* stream) {
+  MMAD_CHECK_ARG(Mp % 128 == 0 && Np % 128 == 0 && M >= 0 && M <= Mp && dy && a && dz && db_partials,
+                 "act_bwd: bad arguments");
+  dim3 grd(Np / SLAB_COLS, Mp / SLAB_ROWS);
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == MMAD_BF16)
+    act_bwd_k<bf16><<<grd, 256, 0, s>>>(act, slope, M, Np, (const bf16*)dy, (const bf16*)a, (bf16*)dz,
+                                        db_partials);
+  else
+    act_bwd_k<float><<<grd, 256, 0, s>>>(act, slope, M, Np, (const float*)dy, (const float*)a,
+                                         (float*)dz, db_partials);
+  MMAD_LAUNCH_CHECK();
   return MMAD_OK;
 }

@@ -66,7 +66,7 @@ class NativeAE:
         # differentiable forward records it and its backward checks it
         self.gen = 0
         self.adam_step_count = 0
-        self.use_graph = os.environ.get("MMAD_TRAIN_GRAPH", "1") != "0"
+        self.use_graph = os.environ.get("MMAD_TRAIN_GRAPH", "0") == "1"
 
     # ------------------------------------------------------------------ memory
     def _alloc(self, device, src=None):
@@ -250,9 +250,10 @@ class NativeAE:
             assert eps.numel() == k * B * self.btl
         self.adam_step_count += 1
         self.gen += 1
-        # one replayed hipGraph per step (mmad_ae_train_step_graph) unless
-        # MMAD_TRAIN_GRAPH=0; the executor falls back to the eager schedule
-        # where capture does not apply (data parallel, shadow pair)
+        # eager multi-stream schedule by default.  MMAD_TRAIN_GRAPH=1 replays
+        # one captured hipGraph per step instead (mmad_ae_train_step_graph);
+        # measured slower on ROCm 7 (profiles/r02e_host.log: host 377 vs 325
+        # us/step, GPU 675 vs 524 us/step at C2), so it stays opt-in
         fn = "mmad_ae_train_step_graph" if self.use_graph else "mmad_ae_train_step"
         call(fn, self._h, ptr(x), x.stride(0), B, int(k), ptr(eps), int(seed),
              int(offset), float(beta_kl), float(lr), float(betas[0]), float(betas[1]),

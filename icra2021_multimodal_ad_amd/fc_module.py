@@ -97,7 +97,13 @@ class Loss(nn.Module):
 
 
 class FCLayer(nn.Module):
-    """layers/fc_layer.py:23-48: y = BN(act(x W^T + b)) [-> dropout]."""
+    """layers/fc_layer.py:23-48: y = BN(act(x W^T + b)) [-> dropout].
+
+    forward runs the fused HIP layer (mmad_fc_fwd [+ mmad_bn_train_apply]) and
+    is differentiable: backward is mmad_bn_act_bwd / mmad_act_bwd +
+    mmad_fc_bwd_weight + mmad_fc_bwd_data.  Inside an AutoEncoder the packed
+    operands are the executor's own padded buffers (no copy); a standalone
+    layer packs W/b once per parameter version."""
 
     def __init__(self, input_size, output_size=1, bias=True, act="relu", bn=False, dropout_p=0):
         super().__init__()
@@ -106,6 +112,8 @@ class FCLayer(nn.Module):
         self.dropout = nn.Dropout(dropout_p) if dropout_p else None
         self.act = Activation(act) if act else None
         self.mmad_dtype = "f32"
+        self._flat = None        # (NativeAE, layer index) when owned by an AutoEncoder
+        self._pack = None        # standalone: (key, w_packed, b_packed, g_packed, be_packed)
 
     @property
     def act_name(self):
@@ -117,14 +125,54 @@ class FCLayer(nn.Module):
             raise NotImplementedError("FCLayer HIP path supports bias=True, element-wise "
                                       "activations and no dropout (the AE configuration)")
         shape = x.shape
-        y = fc_layer_forward(self, x.reshape(-1, shape[-1]), self.training)
+        x2 = x.reshape(-1, shape[-1])
+        params = [self.layer.weight, self.layer.bias]
+        if self.bn is not None:
+            params += [self.bn.weight, self.bn.bias]
+        if torch.is_grad_enabled() and (x2.requires_grad or any(p.requires_grad for p in params)):
+            y = _FCLayerFn.apply(x2, self, self.training, *params)
+        else:
+            y = fc_layer_forward(self, x2, self.training)[0]
         return y.reshape(*shape[:-1], y.shape[-1])
+
+    # packed operands -------------------------------------------------------
+    def packed(self, dev, dt):
+        """(w [Np][Kp] dtype, bias [Np], gamma [Np] | None, beta [Np] | None) fp32
+        padded device buffers holding the current parameter values."""
+        if self._flat is not None:
+            nat, l = self._flat
+            L = nat.layers[l]
+            nat.sync_shadow()
+            wsrc = nat.shadow if dt == _native.BF16 else nat.params
+            w = wsrc[L["w_off"]: L["w_off"] + L["Np"] * L["Kp"]]
+            b = nat.params[L["b_off"]: L["b_off"] + L["Np"]]
+            g = nat.params[L["g_off"]: L["g_off"] + L["Np"]] if L["bn"] else None
+            be = nat.params[L["be_off"]: L["be_off"] + L["Np"]] if L["bn"] else None
+            return w, b, g, be
+        lin, bn = self.layer, self.bn
+        src = [lin.weight, lin.bias] + ([bn.weight, bn.bias] if bn is not None else [])
+        key = (dt, str(dev)) + tuple((p._version, p.data_ptr()) for p in src)
+        if self._pack is None or self._pack[0] != key:
+            N, K = lin.out_features, lin.in_features
+            Np, Kp = pad(N), pad(K)
+            tdt = torch.bfloat16 if dt == _native.BF16 else torch.float32
+            with torch.no_grad():
+                w = torch.zeros((Np, Kp), device=dev, dtype=tdt)
+                w[:N, :K] = lin.weight.detach()
+                vecs = []
+                for p in src[1:]:
+                    v = torch.zeros(Np, device=dev)
+                    v[:N] = p.detach()
+                    vecs.append(v)
+            self._pack = (key, w, vecs[0], vecs[1] if bn is not None else None,
+                          vecs[2] if bn is not None else None)
+        return self._pack[1:]
 
 
 def fc_layer_forward(layer, x2, training):
     """Run one FCLayer through ``mmad_fc_fwd`` (+ ``mmad_bn_train_apply`` in
-    train mode, which also updates the running statistics in place).  Packs
-    operands into the 128-padded layouts the kernels require."""
+    train mode, which also updates the running statistics in place).  Returns
+    (y [M, N] fp32, saved) with saved = what the backward needs."""
     _native.require_gpu(x2)
     lin, bn = layer.layer, layer.bn
     dev = x2.device
@@ -133,70 +181,143 @@ def fc_layer_forward(layer, x2, training):
     M, K = x2.shape
     N = lin.out_features
     Mp, Kp, Np = pad(M), pad(K), pad(N)
-    x2 = x2.float().contiguous()
+    x2 = x2.detach().float().contiguous()
     s = stream_ptr()
     xin = torch.empty((Mp, Kp), device=dev, dtype=tdt)
     call("mmad_pack_input", dt, M, K, Mp, Kp, ptr(x2), K, ptr(xin), s)
-    w = torch.zeros((Np, Kp), device=dev, dtype=tdt)
-    w[:N, :K] = lin.weight.detach()
-    b = torch.zeros(Np, device=dev)
-    b[:N] = lin.bias.detach()
+    w, b, g, be = layer.packed(dev, dt)
     out = torch.empty((Mp, Np), device=dev, dtype=tdt)
     act = _native.ACT[layer.act_name]
+    saved = dict(dt=dt, M=M, N=N, K=K, Mp=Mp, Np=Np, Kp=Kp, xin=xin, w=w, g=g, act=act,
+                 bn_train=False, bn_eval=False)
     if bn is None:
         call("mmad_fc_fwd", dt, M, N, K, Mp, Np, Kp, ptr(xin), ptr(w), ptr(b), act,
              LEAKY_SLOPE, None, None, ptr(out), None, s)
+        saved["a"] = out
+    elif training:
+        stats = torch.empty((Mp // 32, 2, Np), device=dev)
+        a = torch.empty((Mp, Np), device=dev, dtype=tdt)
+        call("mmad_fc_fwd", dt, M, N, K, Mp, Np, Kp, ptr(xin), ptr(w), ptr(b), act,
+             LEAKY_SLOPE, None, None, ptr(a), ptr(stats), s)
+        sm = torch.empty(Np, device=dev)
+        sr = torch.empty(Np, device=dev)
+        # running statistics are updated in place (valid columns only)
+        call("mmad_bn_train_apply", dt, M, N, Mp, Np, ptr(a), ptr(stats), ptr(g), ptr(be),
+             ptr(bn.running_mean), ptr(bn.running_var), float(bn.momentum), float(bn.eps), ptr(sm),
+             ptr(sr), ptr(out), s)
+        with torch.no_grad():
+            bn.num_batches_tracked.add_(1)
+        saved.update(a=a, sm=sm, sr=sr, bn_train=True)
     else:
-        g = torch.zeros(Np, device=dev)
-        be = torch.zeros(Np, device=dev)
-        g[:N] = bn.weight.detach()
-        be[:N] = bn.bias.detach()
+        sc = torch.empty(Np, device=dev)
+        sh = torch.empty(Np, device=dev)
         rm = torch.zeros(Np, device=dev)
         rv = torch.ones(Np, device=dev)
         rm[:N] = bn.running_mean
         rv[:N] = bn.running_var
-        if training:
-            stats = torch.empty((Mp // 32, 2, Np), device=dev)
-            a = torch.empty((Mp, Np), device=dev, dtype=tdt)
-            call("mmad_fc_fwd", dt, M, N, K, Mp, Np, Kp, ptr(xin), ptr(w), ptr(b), act,
-                 LEAKY_SLOPE, None, None, ptr(a), ptr(stats), s)
-            sm = torch.empty(Np, device=dev)
-            sr = torch.empty(Np, device=dev)
-            call("mmad_bn_train_apply", dt, M, N, Mp, Np, ptr(a), ptr(stats), ptr(g), ptr(be),
-                 ptr(rm), ptr(rv), float(bn.momentum), float(bn.eps), ptr(sm), ptr(sr), ptr(out), s)
-            with torch.no_grad():
-                bn.running_mean.copy_(rm[:N])
-                bn.running_var.copy_(rv[:N])
-                bn.num_batches_tracked.add_(1)
-        else:
-            sc = torch.empty(Np, device=dev)
-            sh = torch.empty(Np, device=dev)
-            call("mmad_bn_eval_affine", N, Np, ptr(g), ptr(be), ptr(rm), ptr(rv), float(bn.eps),
-                 ptr(sc), ptr(sh), s)
-            call("mmad_fc_fwd", dt, M, N, K, Mp, Np, Kp, ptr(xin), ptr(w), ptr(b), act,
-                 LEAKY_SLOPE, ptr(sc), ptr(sh), ptr(out), None, s)
+        call("mmad_bn_eval_affine", N, Np, ptr(g), ptr(be), ptr(rm), ptr(rv), float(bn.eps),
+             ptr(sc), ptr(sh), s)
+        call("mmad_fc_fwd", dt, M, N, K, Mp, Np, Kp, ptr(xin), ptr(w), ptr(b), act,
+             LEAKY_SLOPE, ptr(sc), ptr(sh), ptr(out), None, s)
+        saved["bn_eval"] = True
     y = torch.empty((M, N), device=dev)
     call("mmad_unpack_output", dt, M, N, Np, ptr(out), ptr(y), N, s)
-    return y
+    return y, saved
+
+
+class _FCLayerFn(torch.autograd.Function):
+    """Autograd of FCLayer (layers/fc_layer.py:37-48) on the native kernels."""
+
+    @staticmethod
+    def forward(ctx, x2, layer, training, *params):
+        y, saved = fc_layer_forward(layer, x2, training)
+        ctx.saved = saved
+        ctx.n_params = len(params)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        sv = ctx.saved
+        if sv["bn_eval"]:
+            raise NotImplementedError("FCLayer backward through eval-mode BatchNorm is not supported "
+                                      "on the HIP path (train() the layer to differentiate it)")
+        dt, M, N, K, Mp, Np, Kp = sv["dt"], sv["M"], sv["N"], sv["K"], sv["Mp"], sv["Np"], sv["Kp"]
+        dev = dy.device
+        tdt = torch.bfloat16 if dt == _native.BF16 else torch.float32
+        s = stream_ptr()
+        dy = dy.detach().float().contiguous()
+        dyp = torch.empty((Mp, Np), device=dev, dtype=tdt)
+        call("mmad_pack_input", dt, M, N, Mp, Np, ptr(dy), N, ptr(dyp), s)
+        dz = torch.empty((Mp, Np), device=dev, dtype=tdt)
+        dbpart = torch.empty((Mp // 128, Np), device=dev)
+        dgamma = dbeta = None
+        if sv["bn_train"]:
+            dgamma = torch.empty(Np, device=dev)
+            dbeta = torch.empty(Np, device=dev)
+            ws = torch.empty(int(_native.load().mmad_bn_act_bwd_ws(Mp, Np)), dtype=torch.uint8, device=dev)
+            call("mmad_bn_act_bwd", dt, sv["act"], LEAKY_SLOPE, M, N, Mp, Np, ptr(dyp), ptr(sv["a"]),
+                 ptr(sv["sm"]), ptr(sv["sr"]), ptr(sv["g"]), ptr(dz), ptr(dgamma), ptr(dbeta),
+                 ptr(dbpart), ptr(ws), s)
+        else:
+            call("mmad_act_bwd", dt, sv["act"], LEAKY_SLOPE, M, Mp, Np, ptr(dyp), ptr(sv["a"]), ptr(dz),
+                 ptr(dbpart), s)
+        db = torch.empty(Np, device=dev)
+        call("mmad_colsum", Mp // 128, N, Np, ptr(dbpart), Np, 1.0, ptr(db), s)
+        dw = torch.empty((Np, Kp), device=dev)
+        call("mmad_fc_bwd_weight", dt, Mp, Np, Kp, ptr(dz), ptr(sv["xin"]), ptr(dw), s)
+        dxp = torch.empty((Mp, Kp), device=dev, dtype=tdt)
+        call("mmad_fc_bwd_data", dt, M, N, K, Mp, Np, Kp, ptr(dz), ptr(sv["w"]), ptr(dxp), None, s)
+        dx = torch.empty((M, K), device=dev)
+        call("mmad_unpack_output", dt, M, K, Kp, ptr(dxp), ptr(dx), K, s)
+        grads = [dw[:N, :K], db[:N]]
+        if ctx.n_params == 4:
+            grads += [dgamma[:N], dbeta[:N]]
+        return (dx, None, None, *grads)
+
+
+class _ReparamFn(torch.autograd.Function):
+    """decorators/variational_info_bottleneck.py:22-26,37 with its autograd:
+    dmu = sum_k dz, dlogvar = 1/2 sigma sum_k dz eps (mmad_vib_reparam_bwd)."""
+
+    @staticmethod
+    def forward(ctx, mu, logvar, k, det, eps, seed):
+        _native.require_gpu(mu)
+        B, btl = mu.shape
+        dev = mu.device
+        enc = torch.cat([mu.detach(), logvar.detach()], dim=-1).float().contiguous()
+        Mpz, Kpz = pad(k * B), pad(btl)
+        z = torch.empty((Mpz, Kpz), device=dev)
+        eps_used = torch.empty((k, B, btl), device=dev)
+        if eps is not None:
+            eps = eps.float().contiguous()
+        call("mmad_vib_reparam_fwd", _native.F32, B, btl, k, ptr(enc), 2 * btl, ptr(eps),
+             ptr(eps_used) if not det else None, int(seed), 0, int(det), ptr(z), Kpz, None, stream_ptr())
+        if det:
+            eps_used.zero_()              # z = mu: no noise term in the gradient
+        ctx.save_for_backward(enc, eps_used)
+        ctx.k, ctx.B, ctx.btl = k, B, btl
+        return z[:k * B, :btl].reshape(k, B, btl)
+
+    @staticmethod
+    def backward(ctx, dz):
+        enc, eps_used = ctx.saved_tensors
+        k, B, btl = ctx.k, ctx.B, ctx.btl
+        dz = dz.detach().float().contiguous().reshape(k * B, btl)
+        denc = torch.empty((pad(B), 2 * btl), device=dz.device)
+        call("mmad_vib_reparam_bwd", _native.F32, B, btl, k, ptr(enc), 2 * btl, ptr(eps_used), ptr(dz),
+             btl, 0.0, ptr(denc), 2 * btl, None, stream_ptr())
+        return denc[:B, :btl], denc[:B, btl:], None, None, None, None
 
 
 def reparameterize(mu, logvar, k, stochastic_inference, eps=None, seed=None):
     """decorators/variational_info_bottleneck.py:22-26,37 on the GPU through
-    ``mmad_vib_reparam_fwd``: z[k,B,btl] = eps*exp(0.5*logvar) + mu, or
-    mu expanded when grad is disabled and stochastic_inference is False."""
-    _native.require_gpu(mu)
-    B, btl = mu.shape
+    ``mmad_vib_reparam_fwd`` (differentiable via ``mmad_vib_reparam_bwd``):
+    z[k,B,btl] = eps*exp(0.5*logvar) + mu, or mu expanded when grad is
+    disabled and stochastic_inference is False."""
     det = not (torch.is_grad_enabled() or stochastic_inference)
-    enc = torch.cat([mu, logvar], dim=-1).float().contiguous()
-    Mpz, Kpz = pad(k * B), pad(btl)
-    z = torch.empty((Mpz, Kpz), device=mu.device)
-    if eps is not None:
-        eps = eps.float().contiguous()
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-    call("mmad_vib_reparam_fwd", _native.F32, B, btl, k, ptr(enc), 2 * btl, ptr(eps), None,
-         int(seed), 0, int(det), ptr(z), Kpz, None, stream_ptr())
-    return z[:k * B, :btl].reshape(k, B, btl)
+    return _ReparamFn.apply(mu, logvar, int(k), det, eps, seed)
 
 
 def variational_info_bottleneck(forward_fn):

@@ -160,6 +160,13 @@ int mmad_bn_act_bwd(int dtype, int act, float slope, int M, int N, int Mp, int N
                     const float* gamma, void* dz, float* dgamma, float* dbeta, float* db_partials,
                     void* ws, void* stream);
 
+/* Backward of Activation alone (an FCLayer without BN, layers/fc_layer.py:38):
+ * dz = dy * act'(a) from the activation output a (packed [Mp][Np], dtype;
+ * rows >= M -> 0) and db partials fp32 [Mp/128][Np] (column sums of dz, the
+ * bias gradient; reduce with mmad_colsum). */
+int mmad_act_bwd(int dtype, int act, float slope, int M, int Mp, int Np, const void* dy,
+                 const void* a, void* dz, float* db_partials, void* stream);
+
 /* out[j] = scale * sum_{i<n_parts} partials[i*part_stride + j], j < N (Np padded -> 0). */
 int mmad_colsum(int n_parts, int N, int Np, const float* partials, int part_stride, float scale,
                 float* out, void* stream);

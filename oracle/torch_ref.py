@@ -78,11 +78,14 @@ class TorchRefVIBAE(TorchRefAE):
         super().__init__(enc_widths, dec_widths)
         self.k, self.beta_kl = k, beta_kl
 
-    def vib_loss(self, x):
+    def vib_loss(self, x, eps=None):
+        """eps: optional injected noise [k, B, btl] (tests); drawn otherwise."""
         out = self.encoder(x)
         mu, logvar = out.split(out.size(-1) // 2, dim=-1)
         sigma = (0.5 * logvar).exp()
-        z = torch.randn((self.k,) + mu.shape) * sigma + mu
+        if eps is None:
+            eps = torch.randn((self.k,) + mu.shape)
+        z = eps * sigma + mu
         xh = self.decoder(z)
         recon = ((xh - x[None]) ** 2).sum() / self.k
         kl = -0.5 * (1 + logvar - mu * mu - logvar.exp()).sum()
@@ -105,4 +108,4 @@ def train_step(model, optimizer, x):
         loss = model.recon_loss(model(x), x)
     loss.backward(retain_graph=True)
     optimizer.step()
-    return float(loss)
+    return float(loss.detach())
