@@ -152,7 +152,7 @@ def test_eval_forward_validate_and_scores(golden, name):
     m, cfg = _model(d, btl, nl, _sd(g, f"after{steps - 1}/"))
     m.eval()
     with torch.no_grad():
-        xh = m(torch.from_numpy(g["x/0"]).cuda()).cpu().numpy()
+        xh = m(torch.from_numpy(g["x/0"]).cuda()).detach().cpu().numpy()
     assert _rel(xh, g["eval/x_hat"]) < 1e-4
     eng = types.SimpleNamespace(model=m, optimizer=None, config=cfg)
     (vl,) = m.validate(eng, (torch.from_numpy(g["x/0"]), None))
@@ -190,11 +190,11 @@ def test_fc_layer_standalone_matches_oracle(golden):
         layer.bn.running_var.copy_(torch.from_numpy(om["enc"][0]["bn"]["rv"]))
     x = g["x/1"]
     layer.eval()
-    y = layer(torch.from_numpy(x).cuda()).cpu().numpy()
+    y = layer(torch.from_numpy(x).cuda()).detach().cpu().numpy()
     ye, _ = O.fc_forward(x, om["enc"][0], train=False)
     assert _rel(y, ye) < 1e-5
     layer.train()
-    y = layer(torch.from_numpy(x).cuda()).cpu().numpy()
+    y = layer(torch.from_numpy(x).cuda()).detach().cpu().numpy()
     yt, _ = O.fc_forward(x, om["enc"][0], train=True)
     assert _rel(y, yt) < 1e-4
     assert _rel(layer.bn.running_var.cpu().numpy(), om["enc"][0]["bn"]["rv"]) < 1e-5

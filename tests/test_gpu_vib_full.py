@@ -78,7 +78,7 @@ def _torch_cpu_grads(x, sd, eps):
     m.train()
     loss = m.vib_loss(torch.from_numpy(x), eps=torch.from_numpy(eps))
     loss.backward()
-    return float(loss), {n: p.grad.double().numpy() for n, p in m.named_parameters()}
+    return float(loss.detach()), {n: p.grad.double().numpy() for n, p in m.named_parameters()}
 
 
 @pytest.mark.parametrize("d", [2048, 1728])
