@@ -27,6 +27,7 @@ SIGNATURES = {
     "mmad_abi_version": (_I, []),
     "mmad_pad_granule": (_I, []),
     "mmad_tune_set": (_I, [_I, _I]),
+    "mmad_gemm_splitk_for": (_I, [_I, _I, _I, _I, _I]),
     "mmad_gemm_ws_bytes": (ctypes.c_size_t, []),
     "mmad_gemm_set_workspace": (_I, [_P, ctypes.c_size_t]),
     "mmad_gemm_status": (_I, [_P]),

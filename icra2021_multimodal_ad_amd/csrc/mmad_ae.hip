@@ -67,6 +67,14 @@ struct mmad_ae {
   hipStream_t side = nullptr;
   std::vector<hipEvent_t> ev_fork, ev_data;
   hipEvent_t ev_join = nullptr;
+  // tail stream (MMAD_DW_TAIL=1): the main-stream dW GEMMs of layers
+  // 1 .. dw_main-1 run here instead, concurrently with the end of the chain
+  int dw_tail = [] {
+    const char* e = getenv("MMAD_DW_TAIL");
+    return e ? atoi(e) : 0;
+  }();
+  hipStream_t tail = nullptr;
+  hipEvent_t ev_tail = nullptr;
   int mse_tiles = 0;   // loss partials written by the last MSE GEMM
   // data parallelism: RCCL communicator (not owned), its stream and events
   mmad_comm* comm = nullptr;
@@ -90,6 +98,13 @@ struct mmad_ae {
   // fp32 path ~10x the reference's rounding error on BN-producer layers).
   // Set at create from the dtype; MMAD_BN_FOLD=0/1 overrides.
   int fold = 1;
+  // train-mode BN inside the producing GEMM (bn_mode 2, MMAD_BN_MODE): the
+  // forward GEMM's epilogue finishes the batch statistics and writes y, the
+  // bwd-data GEMM's epilogue writes dz (a per-column-tile barrier between the
+  // blocks of one column, mmad_gemm_mfma.hip) -- no finalize / fold / apply
+  // launches.  Layers whose grid cannot be co-resident fall back to mode 0
+  // (apply kernels).  0 = apply kernels, 1 = fold, 2 = fused.
+  int bn_mode = 0;
   // fused step: record the "bwd-data of l done" event only every ev_every-th
   // side-stream layer (each record costs a bubble on the main stream); the dW
   // GEMMs of the layers in between wait for the next recorded one
@@ -128,6 +143,8 @@ struct mmad_ae {
   int dyn_next = 0;
   bool capturing = false;
   bool graph_broken = false;
+  // workspace whose split-K control block this handle has zeroed
+  const void* ws_zeroed = nullptr;
   void clear_train_graphs() {
     for (auto& g : tgraphs) (void)hipGraphExecDestroy(g.exec);
     tgraphs.clear();
@@ -148,6 +165,8 @@ struct mmad_ae {
     if (ev_cdone) (void)hipEventDestroy(ev_cdone);
     if (cstream) (void)hipStreamDestroy(cstream);
     if (side) (void)hipStreamDestroy(side);
+    if (ev_tail) (void)hipEventDestroy(ev_tail);
+    if (tail) (void)hipStreamDestroy(tail);
   }
 };
 
@@ -159,6 +178,11 @@ struct LayerWS {
   // per-64-column partials of sum_k shift[k] W[n][k]
   void* wf;
   float* cpart;
+  // this call: BN of the layer fused into its forward GEMM / into the
+  // bwd-data GEMM of the next layer (bias gradient partials per 64 rows)
+  bool fwd_fused, bwd_fused;
+  unsigned* sync_f;   // fused-BN barrier counters (MMAD_BN_SYNC_WORDS each)
+  unsigned* sync_b;
 };
 struct AeWS {
   int B, k, Mpe, Mpd;
@@ -171,7 +195,8 @@ struct AeWS {
   // the two control blocks are contiguous (one memset per call)
   float* sk_slab[2];
   unsigned* sk_ctl[2];
-  size_t sk_ctl_bytes;
+  size_t sk_ctl_bytes;   // both split-K control blocks + the fused-BN counters
+  unsigned* bn_err;      // fused-BN barrier timeout word
   std::vector<LayerWS> l;
   int64_t bytes;
 };
@@ -193,10 +218,20 @@ static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
     size_t slab = 0, ctl = 0;
     mmad_gemm_splitk_bytes(0, 0, &slab, &ctl);
     ctl = (ctl + 255) / 256 * 256;
-    w.sk_ctl_bytes = 2 * ctl;
-    char* c = take((int64_t)(2 * ctl));
+    // + fused-BN barrier counters: 2 blocks per layer, then the error word
+    const size_t bn_ctl = ((size_t)(2 * h->L.size() * MMAD_BN_SYNC_WORDS + 64) * 4 + 255) / 256 * 256;
+    w.sk_ctl_bytes = 2 * ctl + bn_ctl;
+    char* c = take((int64_t)w.sk_ctl_bytes);
     w.sk_ctl[0] = (unsigned*)c;
     w.sk_ctl[1] = c ? (unsigned*)(c + ctl) : nullptr;
+    unsigned* bc = c ? (unsigned*)(c + 2 * ctl) : nullptr;
+    w.bn_err = bc ? bc + 2 * h->L.size() * MMAD_BN_SYNC_WORDS : nullptr;
+    w.l.resize(h->L.size());
+    for (size_t i = 0; i < h->L.size(); ++i) {
+      w.l[i].sync_f = bc ? bc + (2 * i) * MMAD_BN_SYNC_WORDS : nullptr;
+      w.l[i].sync_b = bc ? bc + (2 * i + 1) * MMAD_BN_SYNC_WORDS : nullptr;
+      w.l[i].fwd_fused = w.l[i].bwd_fused = false;
+    }
   }
   w.B = B;
   w.k = k;
@@ -228,7 +263,6 @@ static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
     const AeLayer& last = h->L[nL - 1];
     w.lossp = (float*)take((int64_t)(w.Mpd / 64) * (last.Np / 64) * 4);
   }
-  w.l.resize(nL);
   for (int i = 0; i < nL; ++i) {
     const AeLayer& a = h->L[i];
     const int Mp = a.enc ? w.Mpe : w.Mpd;
@@ -244,7 +278,7 @@ static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
     s.scale = (float*)take(a.Np * 4);
     s.shift = (float*)take(a.Np * 4);
     s.bnpart = (double*)take((int64_t)(Mp / 64) * 2 * a.Np * 8);
-    s.dbpart = (float*)take((int64_t)(Mp / 128) * a.Np * 4);
+    s.dbpart = (float*)take((int64_t)(Mp / 64) * a.Np * 4);   // 128-row (apply) or 64-row (fused) parts
     s.rowsq = (float*)take((int64_t)(a.Np / 128) * Mp * 4);
     const bool folded = i > 0 && h->L[i - 1].bn;
     s.wf = folded ? take((int64_t)a.Np * a.Kp * es) : nullptr;
@@ -280,6 +314,12 @@ int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, i
   {
     const char* e = getenv("MMAD_BN_FOLD");
     h->fold = e ? (atoi(e) != 0) : (dtype == MMAD_BF16);
+    h->bn_mode = h->fold ? 1 : 0;
+    const char* m = getenv("MMAD_BN_MODE");
+    if (m && atoi(m) >= 0 && atoi(m) <= 2) {
+      h->bn_mode = atoi(m);
+      h->fold = h->bn_mode == 1;
+    }
   }
   for (int side = 0; side < 2; ++side) {
     const int n = side == 0 ? n_enc : n_dec;
@@ -356,8 +396,22 @@ int mmad_ae_bind(mmad_ae* h, float* params, float* grads, float* adam_m, float* 
     MMAD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     // (MMAD_SIDE_PRIO=1: the highest priority instead, for schedule sweeps)
     const char* sp = getenv("MMAD_SIDE_PRIO");
-    MMAD_HIP_CHECK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking,
-                                               (sp && atoi(sp) == 1) ? greatest : least));
+    const char* sc = getenv("MMAD_SIDE_CUS");
+    const int side_cus = sc ? atoi(sc) : 0;
+    if (side_cus > 0 && side_cus < 256) {
+      // (schedule experiments) the side stream confined to side_cus CUs, the
+      // same number on each XCD whether the mask bits enumerate CUs XCD-major
+      // or round-robin over XCDs: bit i set iff i % 32 < side_cus / 8
+      uint32_t mask[8] = {};
+      const int per = side_cus / 8 > 0 ? side_cus / 8 : 1;
+      for (int i = 0; i < 256; ++i)
+        if (i % 32 < per) mask[i / 32] |= 1u << (i % 32);
+      MMAD_HIP_CHECK(hipExtStreamCreateWithCUMask(&h->side, 8, mask));
+    } else {
+      MMAD_HIP_CHECK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking,
+                                                 (sp && atoi(sp) == 1) ? greatest : least));
+    }
+    if (h->dw_tail) MMAD_HIP_CHECK(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
     const size_t n = h->L.size();
     h->ev_fork.resize(n);
     h->ev_data.resize(n);
@@ -366,6 +420,7 @@ int mmad_ae_bind(mmad_ae* h, float* params, float* grads, float* adam_m, float* 
       MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_data[i], kEvFlags));
     }
     MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_join, kEvFlags));
+    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_tail, kEvFlags));
   }
   return MMAD_OK;
 }
@@ -416,6 +471,13 @@ static const void* input_of(const mmad_ae* h, const AeWS& w, int l, bool train,
   return ps.out;
 }
 
+// can the dispatcher choose a split-K factor > 1 for this handle's GEMMs?
+// (bf16: the dW rule; any dtype: a forced override)
+static bool splitk_possible(int dtype) {
+  const int o = mmad_splitk_override();
+  return o > 1 || (dtype == MMAD_BF16 && o != 1);
+}
+
 static int prepare_ws(const mmad_ae* h, int B, int k, void* ws, int64_t ws_bytes, AeWS& w,
                       hipStream_t st) {
   MMAD_CHECK_ARG(B >= 1 && k >= 1, "bad batch B=%d k=%d", B, k);
@@ -424,10 +486,14 @@ static int prepare_ws(const mmad_ae* h, int B, int k, void* ws, int64_t ws_bytes
   MMAD_CHECK_ARG(ws && ws_bytes >= w.bytes, "workspace too small (%lld < %lld bytes)",
                  (long long)ws_bytes, (long long)w.bytes);
   MMAD_CHECK_ARG(((uintptr_t)ws) % 256 == 0, "workspace must be 256-byte aligned");
-  // split-K arrival counters / flags start every call at zero (each GEMM
-  // leaves them zero again, this heals a poisoned or reused workspace); only
-  // when a split can be chosen at all (the default rule never splits)
-  if (mmad_splitk_override() > 1) MMAD_HIP_CHECK(hipMemsetAsync(w.sk_ctl[0], 0, w.sk_ctl_bytes, st));
+  // split-K arrival counters / flags must be zero before a split GEMM runs;
+  // every split GEMM leaves them zero again, so a workspace is zeroed once
+  // when this handle first sees it (and mmad_ae_status re-zeroes after a
+  // timed-out combine); only when a split can be chosen at all
+  if ((splitk_possible(h->dtype) || h->bn_mode == 2) && ws != h->ws_zeroed) {
+    MMAD_HIP_CHECK(hipMemsetAsync(w.sk_ctl[0], 0, w.sk_ctl_bytes, st));
+    const_cast<mmad_ae*>(h)->ws_zeroed = ws;
+  }
   return MMAD_OK;
 }
 
@@ -442,6 +508,10 @@ static int ae_gemm(const mmad_ae* h, const AeWS& w, int dt, int epi, const void*
   const int r = (h->side && s == h->side) ? 1 : 0;
   ep.sk_slab = w.sk_slab[r];
   ep.sk_ctl = w.sk_ctl[r];
+  if (h->tail && s == h->tail) {   // no split-K workspace of its own: never split
+    ep.sk_slab = nullptr;
+    ep.sk_ctl = nullptr;
+  }
   const bool rec = probe >= 0 && probe == h->probe_id && !h->capturing &&
                    2 * h->probe_n < (int)h->probe_ev.size();
   if (rec) MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n], s));
@@ -514,9 +584,26 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
     } else if (a.bn && train) {
       GemmEpi ep = fwd_epi(h, w, a, s, M, s.out, folded);
       ep.part = s.stats;
+      s.fwd_fused = h->bn_mode == 2 && mmad_gemm_bn_fusable(dt, GEMM_EPI_FWD, Mp, a.Np);
+      if (s.fwd_fused) {
+        // BN finished inside the GEMM: a (for the backward) and y = BN(a)
+        ep.bn_sync = s.sync_f;
+        ep.bn_err = w.bn_err;
+        ep.bn_gamma = h->params + a.g_off;
+        ep.bn_beta = h->params + a.be_off;
+        ep.bn_rmean = running_mean(h, a);
+        ep.bn_rvar = running_var(h, a);
+        ep.bn_mom = h->bn_mom;
+        ep.bn_eps = h->bn_eps;
+        ep.bn_save_mean = s.mean;
+        ep.bn_save_rstd = s.rstd;
+        ep.bn_y = s.y;
+      }
       RET_IF(ae_gemm(h, w, dt, GEMM_EPI_FWD, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st, nullptr,
                      PROBE_FWD + l));
-      if (!h->fold) {
+      if (s.fwd_fused) {
+        // nothing left to launch
+      } else if (!h->fold) {
         // exact-fp32 path: normalise into y (the consumer GEMM and its dW read
         // y as the reference's layers do: no fold, no fix-up cancellation)
         RET_IF(mmad_bn_train_apply(dt, M, a.N, Mp, a.Np, s.out, s.stats, h->params + a.g_off,
@@ -567,6 +654,7 @@ static BiasSrc bias_src(const mmad_ae* h, const AeWS& w, int l, bool from_mse) {
   const int Mp = prows_of(w, a);
   const int nL = (int)h->L.size();
   if (l == nL - 1 && from_mse) return {s.stats, Mp / MMAD_PART_ROWS, 2 * a.Np};
+  if (a.bn && s.bwd_fused) return {s.dbpart, Mp / 64, a.Np};   // fused bwd-data epilogue
   if (l == nL - 1 || a.bn || (h->vib && l == h->n_enc - 1)) return {s.dbpart, Mp / 128, a.Np};
   return {s.stats, Mp / MMAD_PART_ROWS, 2 * a.Np};  // bwd-data epilogue column sums
 }
@@ -590,6 +678,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
   const int nL = (int)h->L.size();
   hipStream_t side = h->side;
   std::vector<PendingDW> pending;   // side-stream dW GEMMs waiting for a recorded event
+  bool used_tail = false;
   for (int l = nL - 1; l >= 0; --l) {
     const AeLayer& a = h->L[l];
     LayerWS& s = w.l[l];
@@ -622,8 +711,10 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     // the DP exchange and by side-stream dW GEMMs (every ev_every-th layer;
     // the lowest side layer always records, flushing the deferred ones)
     const bool side_dw = adam && !dp && !ping && l >= h->dw_main;
-    const bool rec = dp || (side_dw && (h->ev_every <= 1 || l == h->dw_main ||
-                                        (l - h->dw_main) % h->ev_every == 0));
+    const bool tail_dw = adam && !dp && !ping && h->tail && l > 0 && l < h->dw_main;
+    const bool rec = dp || tail_dw ||
+                     (side_dw && (h->ev_every <= 1 || l == h->dw_main ||
+                                  (l - h->dw_main) % h->ev_every == 0));
     if (!adam || dp) {
       // fork: dz_l is complete on the main stream; dW_l overlaps the chain below
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
@@ -654,13 +745,28 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
         ep.bn_mean = ps.mean;
         ep.bn_rstd = ps.rstd;
         ep.bn_part = ps.bnpart;
+        ps.bwd_fused = h->bn_mode == 2 && mmad_gemm_bn_fusable(dt, GEMM_EPI_BWD_DATA, Mp, a.Kp);
+        if (ps.bwd_fused) {
+          // BN + activation backward of layer l-1 inside this GEMM: dz directly
+          ep.out = nullptr;
+          ep.bn_sync = ps.sync_b;
+          ep.bn_err = w.bn_err;
+          ep.bn_gamma = h->params + p.g_off;
+          ep.bn_dz = ps.dz;
+          ep.bn_dgamma = h->grads + p.g_off;
+          ep.bn_dbeta = h->grads + p.be_off;
+          ep.bn_dbpart = ps.dbpart;
+          ep.bn_act = p.act;
+          ep.slope = h->slope;
+        }
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
                                   a.Np, ep, st));
         if (rec) MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
-        RET_IF(mmad_bn_act_bwd_apply(dt, p.act, h->slope, rows_of(w, p), p.N, Mpp, p.Np, ps.dy,
-                                     ps.out, ps.mean, ps.rstd, h->params + p.g_off, ps.bnpart,
-                                     Mpp / 64, ps.dz, h->grads + p.g_off, h->grads + p.be_off,
-                                     ps.dbpart, st));
+        if (!ps.bwd_fused)
+          RET_IF(mmad_bn_act_bwd_apply(dt, p.act, h->slope, rows_of(w, p), p.N, Mpp, p.Np, ps.dy,
+                                       ps.out, ps.mean, ps.rstd, h->params + p.g_off, ps.bnpart,
+                                       Mpp / 64, ps.dz, h->grads + p.g_off, h->grads + p.be_off,
+                                       ps.dbpart, st));
       } else {
         ep.out = ps.dy;
         ep.part = ps.stats;
@@ -714,7 +820,13 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       // the last dW GEMMs of the chain go to the main stream, which is idle
       // by then, instead of queueing behind the side stream's backlog
       const bool on_main = l < h->dw_main;
-      if (on_main) {
+      if (tail_dw) {
+        dwe.tile_force = mmad_tile_adam_main_override() + 1;
+        MMAD_HIP_CHECK(hipStreamWaitEvent(h->tail, h->ev_data[l], 0));
+        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, h->tail,
+                       nullptr, PROBE_DW + l));
+        used_tail = true;
+      } else if (on_main) {
         dwe.tile_force = mmad_tile_adam_main_override() + 1;
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st,
                        nullptr, PROBE_DW + l));
@@ -736,9 +848,13 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     }
   }
   MMAD_CHECK_ARG(pending.empty(), "ae backward: deferred dW GEMMs left unissued");
-  // join the side stream back into the main stream
+  // join the side (and tail) streams back into the main stream
   MMAD_HIP_CHECK(hipEventRecord(h->ev_join, side));
   MMAD_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
+  if (used_tail) {
+    MMAD_HIP_CHECK(hipEventRecord(h->ev_tail, h->tail));
+    MMAD_HIP_CHECK(hipStreamWaitEvent(st, h->ev_tail, 0));
+  }
   return MMAD_OK;
 }
 
@@ -1129,13 +1245,28 @@ int mmad_ae_score_stream(mmad_ae* h, const float* x, int ld_x, int64_t N, int ba
 
 int mmad_ae_status(mmad_ae* h, void* ws, int64_t ws_bytes, void* stream) {
   MMAD_CHECK_ARG(h, "ae_status: null handle");
-  // no split-K GEMM can have run unless the override enabled it
-  if (mmad_splitk_override() <= 1 || !ws) return MMAD_OK;
+  // no split-K GEMM / fused-BN barrier can have run unless the dtype /
+  // override / BN mode allows one
+  if ((!splitk_possible(h->dtype) && h->bn_mode != 2) || !ws) return MMAD_OK;
   AeWS w;
   carve(h, 1, 1, (char*)ws, w);
   MMAD_CHECK_ARG(ws_bytes >= w.bytes, "ae_status: workspace too small");
   for (int r = 0; r < 2; ++r)
     RET_IF(mmad_gemm_read_status(w.sk_ctl[r], (hipStream_t)stream, "ae_status"));
+  if (h->bn_mode == 2 && w.bn_err) {
+    unsigned word = 0;
+    MMAD_HIP_CHECK(hipMemcpyAsync(&word, w.bn_err, sizeof(word), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    MMAD_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    if (word) {
+      // re-zero every control word (a barrier that gave up may have left
+      // counters raised) for the next call
+      MMAD_HIP_CHECK(hipMemsetAsync(w.sk_ctl[0], 0, w.sk_ctl_bytes, (hipStream_t)stream));
+      MMAD_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+      mmad_set_error("ae_status: a fused BatchNorm column barrier timed out; the outputs of that "
+                     "call are invalid");
+      return MMAD_EHIP;
+    }
+  }
   return MMAD_OK;
 }
 

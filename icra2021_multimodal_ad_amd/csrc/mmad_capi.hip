@@ -52,6 +52,16 @@ static int g_splitk = [] {
   return e ? atoi(e) : 0;
 }();
 int mmad_splitk_override() { return g_splitk; }
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+static int g_splitk_dw = env_int("MMAD_GEMM_SPLITK_DW", 0);
+static int g_splitk_dw_blocks = env_int("MMAD_SPLITK_DW_BLOCKS", 512);
+static int g_splitk_dw_min_stages = env_int("MMAD_SPLITK_DW_MIN_STAGES", 8);
+int mmad_splitk_dw_override() { return g_splitk_dw; }
+int mmad_splitk_dw_blocks() { return g_splitk_dw_blocks; }
+int mmad_splitk_dw_min_stages() { return g_splitk_dw_min_stages; }
 // tile for the dW GEMMs with the fused Adam epilogue (the autotuner times
 // them without Adam, which under-weights the epilogue's HBM traffic: it picks
 // 128x128 for the large layers, 208 blocks for 256 CUs).  Default 64x64 (cfg
@@ -94,8 +104,16 @@ int mmad_tune_set(int knob, int value) {
     case 6: g_tile_bwd_data = value; return MMAD_OK;
     case 7: g_tile_fwd = value; return MMAD_OK;
     case 8: g_tile_adam_main = value; return MMAD_OK;
+    case 9: g_splitk_dw = value; return MMAD_OK;
+    case 10: g_splitk_dw_blocks = value; return MMAD_OK;
+    case 11: g_splitk_dw_min_stages = value; return MMAD_OK;
     default: mmad_set_error("tune_set: unknown knob %d", knob); return MMAD_EINVAL;
   }
+}
+
+int mmad_gemm_splitk_for(int Mp, int Np, int K, int dtype, int epi) {
+  if (Mp <= 0 || Np <= 0 || K <= 0 || epi < 0 || epi > 4) return 1;
+  return mmad_gemm_splitk(Mp, Np, K, dtype, epi);
 }
 
 #define RET_IF(x)              \

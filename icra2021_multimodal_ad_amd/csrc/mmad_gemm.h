@@ -82,6 +82,33 @@ struct GemmEpi {
   // graph-captured step (nullable): MSE target = dyn->x, Adam step terms
   // from dyn (see MmadDyn)
   const MmadDyn* dyn;
+  // Train-mode BatchNorm fused into the producing GEMM (bn_sync != null):
+  // the tiles_m blocks of one output column tile publish their column
+  // partials (sc1 stores), meet at a counter barrier (bn_sync[tn] arrivals,
+  // bn_sync[MMAD_BN_EXIT + tn] exits; zero before the launch, left zero) and
+  // each finishes the whole-batch statistics for its columns itself.  Needs
+  // every block of the grid co-resident (mmad_gemm_coresident) and S = 1.
+  //  FWD: part = Welford partials; writes out = a (pre-BN activation) and
+  //       bn_y = BN(a) = a*scale + shift; the tm == 0 blocks write
+  //       bn_save_mean/rstd and update the running statistics (nullable).
+  //  BWD_DATA: bn_part = fp64 (sum dy, sum dy*xhat) per 64 rows; writes
+  //       bn_dz = act'(a) * dBN(dy) (out unused), bn_dbpart = per-64-row
+  //       column sums of dz, and (tm == 0) bn_dgamma / bn_dbeta.
+  unsigned* bn_sync;
+  unsigned* bn_err;      // sticky timeout word (barrier never completed)
+  const float* bn_gamma;
+  const float* bn_beta;
+  float* bn_rmean;
+  float* bn_rvar;
+  float bn_mom, bn_eps;
+  float* bn_save_mean;
+  float* bn_save_rstd;
+  void* bn_y;
+  void* bn_dz;
+  float* bn_dgamma;
+  float* bn_dbeta;
+  float* bn_dbpart;
+  int bn_act;            // BWD_DATA: the BN producer's activation (act' from a)
   int dbg;               // diagnostics (tools/gemm_sweep): 1 skip main loop, 2 skip epilogue,
                          // 4 force the split-K combine's timeout path (tests)
 };
@@ -91,7 +118,10 @@ int mmad_group_override();
 int mmad_tile_override();
 int mmad_autotune_enabled();
 int mmad_dbg_override();
-int mmad_splitk_override();   // 0 = shape rule; 1, 2, 4 = forced split factor
+int mmad_splitk_override();   // 0 = shape rule; 1, 2, 4, 8, 16 = forced split factor
+int mmad_splitk_dw_override();     // the same for the dW GEMMs only (knob 9)
+int mmad_splitk_dw_blocks();       // dW split rule: target 64x64-tile blocks (knob 10)
+int mmad_splitk_dw_min_stages();   // dW split rule: minimum K stages per slice (knob 11)
 int mmad_tile_adam_override();  // >= 0: tile of the Adam-fused dW GEMMs
 int mmad_tile_adam_main_override();  // >= 0: ... of those on the main stream
 int mmad_tile_epi_override(int epi);  // >= 0: tile of this epilogue's GEMMs
@@ -105,14 +135,24 @@ int mmad_gemm_ntiles(int cfg, int Mp, int Np);
 int mmad_gemm_tiles(int Mp, int Np);
 
 // split-K factor the dispatcher uses for a shape when the caller provides
-// split-K workspace (1, 2 or 4; a function of the shape only, so every tile
-// configuration of a shape accumulates in the same order)
-int mmad_gemm_splitk(int Mp, int Np, int K, int dtype);
+// split-K workspace (1, 2, 4, 8 or 16; a function of the shape and epilogue
+// only, so every tile configuration of a shape accumulates in the same order)
+int mmad_gemm_splitk(int Mp, int Np, int K, int dtype, int epi);
 // split-K workspace sufficient for every launch (shape-independent bound)
 void mmad_gemm_splitk_bytes(int Mp, int Np, size_t* slab_bytes, size_t* ctl_bytes);
 // read (and clear) the timeout word of a split-K control block after syncing
 // `s`: MMAD_OK, or MMAD_EHIP with the error string set
 int mmad_gemm_read_status(unsigned* ctl, hipStream_t s, const char* who);
+
+// offset of the exit counters inside a fused-BN barrier block; words per block
+#define MMAD_BN_EXIT 64
+#define MMAD_BN_SYNC_WORDS 128
+// can a GEMM with the fused train-mode BN epilogue (bn_sync) run this shape:
+// is there a fitting tile configuration whose whole grid is co-resident on
+// the current device?  (the per-column-tile barrier needs every block of a
+// column resident; with the whole grid resident, work of other streams can
+// delay it but never block it)
+bool mmad_gemm_bn_fusable(int dtype, int epi, int Mp, int Np);
 
 // cfg_used (nullable) receives the tile configuration launched
 int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,

@@ -239,6 +239,68 @@ __device__ __forceinline__ void block_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// ---- cross-workgroup hand-off of the fused-BN column partials -------------
+// Agent-scope relaxed atomics lower to sc1 global loads / stores (L1
+// bypassed, written through): producers store every partial sc1, wait for
+// their stores, meet at a workgroup barrier, and one lane adds to the column
+// counter; one lane polls it with sc1 loads, the block joins it at a barrier
+// and then reads the partials with sc1 loads only (MI355X_MICROARCH.md,
+// hand-off table row 1: no release / acquire fences needed).
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store((unsigned*)p, __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store((unsigned long long*)p, __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __builtin_bit_cast(float, __hip_atomic_load((unsigned*)p, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Barrier of the `target` blocks sharing one output column tile.  Bounded:
+// a barrier that does not complete within ~2^20 polls (about a second) sets
+// the sticky error word and returns false (the caller skips its outputs; the
+// host reports it through mmad_ae_status) instead of hanging the GPU.
+__device__ __forceinline__ bool col_barrier(unsigned* arrive, unsigned target, unsigned* err,
+                                            int tid, unsigned* shw) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's partial stores landed
+  __syncthreads();                                   // ... and every other wave's
+  if (tid == 0) {
+    __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned ok = 0u;
+    for (unsigned spins = 0; spins < (1u << 20); ++spins) {
+      if (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) {
+        ok = 1u;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (!ok) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    shw[0] = ok;
+  }
+  __syncthreads();
+  return shw[0] != 0u;
+}
+
+// every block of the column has read the partials: the last one out resets
+// both counters for the next launch (stream-ordered after this one)
+__device__ __forceinline__ void col_exit(unsigned* arrive, unsigned* exitc, unsigned target, int tid) {
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(exitc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1u == target) {
+      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(exitc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 }  // namespace
 
 // -------------------------------------------------------------------------
@@ -269,7 +331,9 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   constexpr int QG = 32;                               // prefetched dW row-sum partials
   constexpr int OSTRIDE = BN * (int)sizeof(TO) + 16;
   constexpr int OBYTES = BM * OSTRIDE + (EPI == GEMM_EPI_BWD_DATA ? BM * BN / 2 : 0);   // + fp64 [BM/16][BN]
-  constexpr int LDS_BYTES = (NS * SLOT > OBYTES) ? NS * SLOT : OBYTES;
+  // fused train-mode BN: per-column merge results (2 x fp64 [BN]) + a flag word
+  constexpr int XBYTES = (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_BWD_DATA) ? 2 * BN * 8 + 64 : 0;
+  constexpr int LDS_BYTES = (NS * SLOT > OBYTES + XBYTES) ? NS * SLOT : OBYTES + XBYTES;
   static_assert((NS - 1) * NL <= 63, "vmcnt range");
   static_assert(LDS_BYTES <= 163840, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
@@ -499,26 +563,34 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] += ob[i][j];
     } else {
-      // ((p0 + p1) + p2) + p3 in split order, one slab per round trip (slot
-      // sk was never written: loaded anyway, then replaced by acc)
+      // ((p0 + p1) + p2) + ... in split order, G slabs per round trip (slot
+      // sk was never written: loaded anyway, then replaced by acc).  G = 2
+      // for the 8-wave / 64x64-wave-tile configurations (register budget).
+      constexpr int G = TM * TN <= 8 ? 4 : 2;
       floatx4 r[TM][TN];
-      for (int t = 0; t < S; ++t) {
-        floatx4 lb[TM][TN];
+      for (int t0 = 0; t0 < S; t0 += G) {
+        floatx4 lb[G][TM][TN];
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int u = 0; u < G; ++u)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            lb[i][j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                       rs, t * BM * BN * 4 + ((frag0 + i * TN + j) * 64 + lane) * 16, 0, 16));
-            asm volatile("" : "+v"(lb[i][j]));   // materialise: no branch around the load
-          }
+          for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+            for (int j = 0; j < TN; ++j) {
+              lb[u][i][j] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                            rs, (t0 + u) * BM * BN * 4 + ((frag0 + i * TN + j) * 64 + lane) * 16, 0, 16));
+              asm volatile("" : "+v"(lb[u][i][j]));   // materialise: no branch around the load
+            }
 #pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const floatx4 e = t == sk ? acc[i][j] : lb[i][j];
-            r[i][j] = t == 0 ? e : r[i][j] + e;
-          }
+        for (int u = 0; u < G; ++u) {
+          const int t = t0 + u;
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              const floatx4 e = t == sk ? acc[i][j] : lb[u][i][j];
+              r[i][j] = t == 0 ? e : r[i][j] + e;
+            }
+        }
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -642,7 +714,15 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
             }
           q += __shfl_xor(q, 16);
           q += __shfl_xor(q, 32);
-          if (g == 0) { part[col] = mean; part[ep.ldpart + col] = q; }
+          if (g == 0) {
+            if (ep.bn_sync) {   // handed to the other blocks of this column: sc1
+              st_sc1(part + col, mean);
+              st_sc1(part + ep.ldpart + col, q);
+            } else {
+              part[col] = mean;
+              part[ep.ldpart + col] = q;
+            }
+          }
         } else if (EPI == GEMM_EPI_MSE) {
           float a2 = s2[p];
           a2 += __shfl_xor(a2, 16);
@@ -754,7 +834,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
       const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
       const int row = m0 + rl;
       const int col = n0 + ch * OEPC;
-      if (EPI != GEMM_EPI_SCORE || out) *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
+      if (out) *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
       if constexpr (EPI == GEMM_EPI_SCORE) {
         const uint4v rv = rvs[it];
         const TO* pv = (const TO*)&v;
@@ -782,6 +862,90 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         for (int o = 1; o < CPR128; o <<= 1) sq += __shfl_xor(sq, o);
         if (ch % CPR128 == 0) ep.rowsq[(size_t)(col / 128) * ep.ldrow + row] = sq;
       }
+    }
+  }
+  if constexpr (EPI == GEMM_EPI_FWD) {
+    if (ep.bn_sync) {
+      // ---- fused BatchNorm(train) of this layer (layers/fc_layer.py:37-48,
+      // Linear -> act -> BN): whole-batch mean / variance merged from every
+      // block's Welford partials (one sequential chunk order: every block of
+      // the column computes the same bits), then y = a*scale + shift from the
+      // fp32 activations still in registers
+      const unsigned tiles_m = (unsigned)(ntl / ep.tiles_n);
+      unsigned* shw = (unsigned*)(smem + OBYTES + 2 * BN * 8);
+      if (!col_barrier(ep.bn_sync + tn, tiles_m, ep.bn_err, tid, shw)) return;
+      float* s_sc = (float*)(smem + OBYTES);
+      float* s_sh = s_sc + BN;
+      if (tid < BN) {
+        const int c = n0 + tid;
+        const int nparts = (int)tiles_m * BM / MMAD_PART_ROWS;
+        constexpr int U = 16;
+        double n = 0.0, mean = 0.0, m2 = 0.0;
+        for (int i0 = 0; i0 < nparts; i0 += U) {
+          float mb[U], qb[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int i = i0 + u < nparts ? i0 + u : nparts - 1;
+            mb[u] = ld_sc1(ep.part + (size_t)i * 2 * ep.ldpart + c);
+            qb[u] = ld_sc1(ep.part + ((size_t)i * 2 + 1) * ep.ldpart + c);
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int i = i0 + u;
+            int cnt = ep.M - i * MMAD_PART_ROWS;
+            cnt = cnt < 0 ? 0 : (cnt > MMAD_PART_ROWS ? MMAD_PART_ROWS : cnt);
+            if (i >= nparts || cnt == 0) continue;
+            const double nb = (double)cnt, nn = n + nb, d = (double)mb[u] - mean;
+            mean += d * (nb / nn);
+            m2 += (double)qb[u] + d * d * (n * nb / nn);
+            n = nn;
+          }
+        }
+        const float var = n > 0.0 ? (float)(m2 / n) : 0.f;
+        const float mu = (float)mean;
+        float sc = 0.f, sh = 0.f;
+        if (c < ep.N) {
+          const float rstd = (float)(1.0 / sqrt((double)var + (double)ep.bn_eps));
+          sc = ep.bn_gamma[c] * rstd;
+          sh = ep.bn_beta[c] - mu * sc;
+          if (tm == 0) {
+            ep.bn_save_mean[c] = mu;
+            ep.bn_save_rstd[c] = rstd;
+            if (ep.bn_rmean) {
+              const float unb = ep.M > 1 ? var * (float)ep.M / (float)(ep.M - 1) : var;
+              ep.bn_rmean[c] = (1.f - ep.bn_mom) * ep.bn_rmean[c] + ep.bn_mom * mu;
+              ep.bn_rvar[c] = (1.f - ep.bn_mom) * ep.bn_rvar[c] + ep.bn_mom * unb;
+            }
+          }
+        } else if (tm == 0) {
+          ep.bn_save_mean[c] = 0.f;
+          ep.bn_save_rstd[c] = 0.f;
+        }
+        s_sc[tid] = sc;
+        s_sh[tid] = sh;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int rl = wm * 16 * TM + i * 16 + 4 * g + r;
+            const int cl = wn * 16 * TN + j * 16 + c;
+            const float yv = m0 + rl < ep.M ? acc[i][j][r] * s_sc[cl] + s_sh[cl] : 0.f;
+            *(TO*)(smem + rl * OSTRIDE + cl * (int)sizeof(TO)) = from_f32<TO>(yv);
+          }
+      __syncthreads();
+      TO* yo = (TO*)ep.bn_y;
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) {
+        const int idx = it * NT + tid;
+        const int rl = idx / CPR, ch = idx % CPR;
+        const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
+        *(uint4v*)(yo + (size_t)(m0 + rl) * ep.ldo + n0 + ch * OEPC) = v;
+      }
+      col_exit(ep.bn_sync + tn, ep.bn_sync + MMAD_BN_EXIT + tn, tiles_m, tid);
     }
   }
   if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
@@ -858,9 +1022,98 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
           double t = scr[(4 * c4) * BN + cc];
 #pragma unroll
           for (int q = 1; q < 4; ++q) t += scr[(4 * c4 + q) * BN + cc];
-          ep.bn_part[(size_t)((m0 + c4 * 64) / 64) * 2 * ep.ldo + which * ep.ldo + col] = t;
+          double* dst = ep.bn_part + (size_t)((m0 + c4 * 64) / 64) * 2 * ep.ldo + which * ep.ldo + col;
+          if (ep.bn_sync) st_sc1(dst, t);   // handed to the other blocks of this column
+          else *dst = t;
         }
         __syncthreads();
+      }
+      if (ep.bn_sync) {
+        // ---- fused BatchNorm(train) + activation backward of the producer:
+        // whole-batch sums from every block's partials, then
+        // dz = act'(a) * gamma*rstd/M * (M dy - sum dy - xhat sum dy*xhat)
+        // (fp64 bracket, as bn_bwd_apply_k) in place in the staged tile
+        const unsigned tiles_m = (unsigned)(ntl / ep.tiles_n);
+        unsigned* shw = (unsigned*)(smem + OBYTES + 2 * BN * 8);
+        if (!col_barrier(ep.bn_sync + tn, tiles_m, ep.bn_err, tid, shw)) return;
+        double* s_t1 = (double*)(smem + OBYTES);
+        double* s_t2 = s_t1 + BN;
+        if (tid < BN) {
+          const int c = n0 + tid;
+          const int nch = (int)tiles_m * BM / 64;
+          constexpr int U = 16;
+          double t1 = 0.0, t2 = 0.0;
+          for (int i0 = 0; i0 < nch; i0 += U) {
+            double p1[U], p2[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const int i = i0 + u < nch ? i0 + u : nch - 1;
+              p1[u] = ld_sc1(ep.bn_part + (size_t)i * 2 * ep.ldo + c);
+              p2[u] = ld_sc1(ep.bn_part + ((size_t)i * 2 + 1) * ep.ldo + c);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+              if (i0 + u < nch) { t1 += p1[u]; t2 += p2[u]; }
+          }
+          if (c >= ep.N) { t1 = 0.0; t2 = 0.0; }
+          if (tm == 0) {
+            ep.bn_dbeta[c] = (float)t1;
+            ep.bn_dgamma[c] = (float)t2;
+          }
+          s_t1[tid] = t1;
+          s_t2[tid] = t2;
+        }
+        __syncthreads();
+        const double t1 = s_t1[cc], t2 = s_t2[cc];
+        const double cf = col < ep.N ? (double)ep.bn_gamma[col] * rs / (double)ep.M : 0.0;
+        const double Md = (double)ep.M;
+        double pz[PPT];
+#pragma unroll
+        for (int u = 0; u < PPT; ++u) {
+          const int pc = grp + u * NG;
+          double sz = 0.0;
+          if (pc < PIECES) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int rl = pc * 16 + r;
+              TO* slot = (TO*)(smem + rl * OSTRIDE + cc * (int)sizeof(TO));
+              const double dy = to_f32<TO>(*slot);
+              const float av = to_f32<TO>(an[(size_t)(m0 + rl) * ep.ldo + col]);
+              const double xh = ((double)av - mu) * rs;
+              const double da = cf * (Md * dy - t1 - xh * t2);
+              float d = (float)(da * (double)act_grad_from_out(av, ep.bn_act, ep.slope));
+              d = m0 + rl < ep.M ? d : 0.f;
+              const TO dt = from_f32<TO>(d);
+              *slot = dt;
+              sz += (double)to_f32<TO>(dt);
+            }
+          }
+          pz[u] = sz;
+        }
+        // per-64-row column sums of dz (the producer's bias gradient), the
+        // same piece order as bn_part
+#pragma unroll
+        for (int u = 0; u < PPT; ++u) {
+          const int pc = grp + u * NG;
+          if (pc < PIECES) scr[pc * BN + cc] = pz[u];
+        }
+        __syncthreads();
+        for (int c4 = grp; c4 < BM / 64; c4 += NG) {
+          double t = scr[(4 * c4) * BN + cc];
+#pragma unroll
+          for (int q = 1; q < 4; ++q) t += scr[(4 * c4 + q) * BN + cc];
+          ep.bn_dbpart[(size_t)((m0 + c4 * 64) / 64) * ep.ldo + col] = (float)t;
+        }
+        // coalesced store of the dz tile
+        TO* dzo = (TO*)ep.bn_dz;
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+          const int idx = it * NT + tid;
+          const int rl = idx / CPR, ch = idx % CPR;
+          const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
+          *(uint4v*)(dzo + (size_t)(m0 + rl) * ep.ldo + n0 + ch * OEPC) = v;
+        }
+        col_exit(ep.bn_sync + tn, ep.bn_sync + MMAD_BN_EXIT + tn, tiles_m, tid);
       }
     }
   }
@@ -881,15 +1134,22 @@ int mmad_gemm_ntiles(int cfg, int Mp, int Np) { return (Mp / CFG_BM[cfg]) * (Np 
 int mmad_gemm_tiles(int Mp, int Np) { return (Mp / 64) * (Np / 64); }
 
 // static choice when autotuning is off or impossible (stream capture)
-static int heuristic_cfg(int Mp, int Np, int epi) {
+template <typename Pred>
+static int heuristic_cfg(int Mp, int Np, int epi, Pred allowed) {
   const int order[] = {1, 0, 5, 4, 3};
   const int want[] = {200, 200, 200, 160, 0};
   for (int i = 0; i < 5; ++i) {
     const int c = order[i];
-    if (!cfg_fits(c, Mp, Np, epi)) continue;
+    if (!allowed(c)) continue;
     if (mmad_gemm_ntiles(c, Mp, Np) >= want[i]) return c;
   }
-  return cfg_fits(4, Mp, Np, epi) ? 4 : 0;
+  for (int c : {4, 0, 3, 5, 2, 1})
+    if (allowed(c)) return c;
+  (void)Mp; (void)Np; (void)epi;
+  return -1;
+}
+static int heuristic_cfg(int Mp, int Np, int epi) {
+  return heuristic_cfg(Mp, Np, epi, [&](int c) { return cfg_fits(c, Mp, Np, epi); });
 }
 
 template <typename T, typename TO, bool AK, bool BK_, int EPI>
@@ -920,6 +1180,75 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
   return MMAD_OK;
 }
 
+// ---- co-residency of a whole grid (the fused-BN column barrier needs it) ----
+template <typename T, typename TO, bool AK, bool BK_, int EPI>
+static const void* kernel_ptr(int cfg) {
+  switch (cfg) {
+    case 0: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 0, EPI>;
+    case 1: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 1, EPI>;
+    case 2: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 2, EPI>;
+    case 3: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI>;
+    case 4: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI>;
+    default: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI>;
+  }
+}
+static const void* kernel_for(int dtype, int epi, int cfg) {
+  if (dtype == MMAD_BF16) {
+    if (epi == GEMM_EPI_FWD) return kernel_ptr<bf16, bf16, true, true, GEMM_EPI_FWD>(cfg);
+    if (epi == GEMM_EPI_BWD_DATA) return kernel_ptr<bf16, bf16, true, false, GEMM_EPI_BWD_DATA>(cfg);
+  } else {
+    if (epi == GEMM_EPI_FWD) return kernel_ptr<float, float, true, true, GEMM_EPI_FWD>(cfg);
+    if (epi == GEMM_EPI_BWD_DATA) return kernel_ptr<float, float, true, false, GEMM_EPI_BWD_DATA>(cfg);
+  }
+  return nullptr;
+}
+namespace {
+std::mutex g_occ_mu;
+std::map<long, int> g_occ;   // (device, dtype, epi, cfg) -> resident grid capacity
+}  // namespace
+
+// blocks of (dtype, epi, cfg) that can be resident on the current device at
+// once: CUs x min(occupancy API, the LDS bound); 0 if unknown
+static int grid_capacity(int dtype, int epi, int cfg) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  const long key = (((long)dev * 4 + dtype) * 8 + epi) * 8 + cfg;
+  {
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    auto it = g_occ.find(key);
+    if (it != g_occ.end()) return it->second;
+  }
+  const void* fn = kernel_for(dtype, epi, cfg);
+  int per_cu = 0, cus = 0;
+  if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, CFG_NT[cfg], 0) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    per_cu = 0;
+  }
+  hipFuncAttributes fa{};
+  if (fn && hipFuncGetAttributes(&fa, fn) == hipSuccess && fa.sharedSizeBytes > 0) {
+    const int lds_bound = (int)(163840 / fa.sharedSizeBytes);
+    per_cu = per_cu < lds_bound ? per_cu : lds_bound;
+  }
+  (void)hipGetLastError();
+  const int cap = per_cu > 0 && cus > 0 ? per_cu * cus : 0;
+  std::lock_guard<std::mutex> lk(g_occ_mu);
+  g_occ[key] = cap;
+  return cap;
+}
+
+static bool coresident(int dtype, int epi, int cfg, int Mp, int Np) {
+  return mmad_gemm_ntiles(cfg, Mp, Np) <= grid_capacity(dtype, epi, cfg);
+}
+
+bool mmad_gemm_bn_fusable(int dtype, int epi, int Mp, int Np) {
+  if (epi != GEMM_EPI_FWD && epi != GEMM_EPI_BWD_DATA) return false;
+  if (Mp % 128 || Np % 128 || Np / 64 > MMAD_BN_EXIT) return false;
+  for (int c = 0; c < NCFG; ++c)
+    if (cfg_fits(c, Mp, Np, epi) && coresident(dtype, epi, c, Mp, Np)) return true;
+  return false;
+}
+
 static int launch_cfg(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,
                       int Np, int K, const GemmEpi& ep, int cfg, hipStream_t s) {
 #define MMAD_LT(T, TO, AK, BK_, EPI)                                                      \
@@ -945,10 +1274,10 @@ static int launch_cfg(int dtype, int epi, const void* A, int lda, const void* B,
 // ---- autotune: time every fitting tile config once per problem shape -------
 namespace {
 struct TuneKey {
-  int dtype, epi, Mp, Np, K;
+  int dtype, epi, Mp, Np, K, bnf;
   bool operator<(const TuneKey& o) const {
-    const int a[5] = {dtype, epi, Mp, Np, K}, b[5] = {o.dtype, o.epi, o.Mp, o.Np, o.K};
-    for (int i = 0; i < 5; ++i)
+    const int a[6] = {dtype, epi, Mp, Np, K, bnf}, b[6] = {o.dtype, o.epi, o.Mp, o.Np, o.K, o.bnf};
+    for (int i = 0; i < 6; ++i)
       if (a[i] != b[i]) return a[i] < b[i];
     return false;
   }
@@ -964,6 +1293,8 @@ static int tune_cfg(int dtype, int epi, const void* A, int lda, const void* B, i
   GemmEpi et = ep;
   et.ad_p = nullptr;
   et.sm_p = nullptr;
+  et.bn_rmean = nullptr;   // fused BN: no running-statistics update while timing
+  et.bn_rvar = nullptr;
   hipEvent_t e0, e1;
   MMAD_HIP_CHECK(hipEventCreate(&e0));
   MMAD_HIP_CHECK(hipEventCreate(&e1));
@@ -972,6 +1303,7 @@ static int tune_cfg(int dtype, int epi, const void* A, int lda, const void* B, i
   int rc = MMAD_OK;
   for (int c = 0; c < NCFG && rc == MMAD_OK; ++c) {
     if (!cfg_fits(c, Mp, Np, epi)) continue;
+    if (ep.bn_sync && !coresident(dtype, epi, c, Mp, Np)) continue;
     rc = launch_cfg(dtype, epi, A, lda, B, ldb, Mp, Np, K, et, c, s);   // warm
     if (rc != MMAD_OK) break;
     float ms = 0.f;
@@ -992,28 +1324,50 @@ static int tune_cfg(int dtype, int epi, const void* A, int lda, const void* B, i
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   if (rc != MMAD_OK) return rc;
+  if (best < 0) {
+    mmad_set_error("gemm autotune: no tile configuration fits (Mp=%d Np=%d epi=%d)", Mp, Np, epi);
+    return MMAD_EUNSUPPORTED;
+  }
   *out_cfg = best;
   return MMAD_OK;
 }
 
-// split factor for a shape (1, 2 or 4): a function of the shape only, so every
-// tile configuration of the shape accumulates over K in the same order
-int mmad_gemm_splitk(int Mp, int Np, int K, int dtype) {
+// split factor for a shape (1, 2, 4, 8 or 16): a function of the shape and
+// the epilogue only, so every tile configuration of a shape accumulates over
+// K in the same order
+int mmad_gemm_splitk(int Mp, int Np, int K, int dtype, int epi) {
   const int bk = dtype == MMAD_BF16 ? 64 : 32;            // K per stage
   const int t128 = (Mp / 128) * (Np / 128);              // 128x128 output tiles
-  // workspace bound (mmad_gemm_splitk_bytes): S * t128 <= 320
-  auto ok = [&](int S) { return K % (S * bk) == 0 && K / S >= 4 * bk && S * t128 <= 320; };
+  const int t64 = (Mp / 64) * (Np / 64);                 // 64x64 output tiles
+  // workspace bounds (mmad_gemm_splitk_bytes): S * t128 <= 320 slab tiles,
+  // (1 + S) control words per tile of the smallest configuration
+  auto ok = [&](int S) {
+    return K % (S * bk) == 0 && K / S >= 4 * bk && S * t128 <= 320 && t64 * (1 + S) < MMAD_SK_ERR_WORD;
+  };
+  auto valid = [](int S) { return S == 1 || S == 2 || S == 4 || S == 8 || S == 16; };
   const int env = mmad_splitk_override();
-  if (env == 1 || env == 2 || env == 4) return ok(env) ? env : 1;
+  if (valid(env)) return ok(env) ? env : 1;
   // the exact-fp32 parity path keeps one sequential K order per output (the
   // order closest to the reference's; a different fp32 order can flip the
   // LeakyReLU branch of a pre-activation at rounding level, e.g. 5.6e-7 in
   // tests/golden/mm192.npz); split-K is the bf16 performance path's
   if (dtype != MMAD_BF16) return 1;
-  // measured at the bench shapes (B=1024, widths 2048..100): the in-launch
-  // combine (slab round trip + ticket) costs more than the extra CUs buy back,
-  // so the default is no split; 2 and 4 stay available through the override
-  (void)t128;
+  if (epi == GEMM_EPI_BWD_WEIGHT) {
+    const int envw = mmad_splitk_dw_override();
+    if (valid(envw)) return ok(envw) ? envw : 1;
+    // dW = dz^T a contracts over the batch: the narrow layers have few
+    // output tiles and a long K loop.  Split until the launch has about
+    // SK_DW_BLOCKS 64x64-tile blocks, keeping >= SK_DW_MIN_STAGES K stages
+    // per slice (tools/splitk_sweep.py, profiles/r02*_splitk_dw*.log)
+    const int target = mmad_splitk_dw_blocks(), min_st = mmad_splitk_dw_min_stages();
+    int best = 1;
+    for (int S = 2; S <= 16; S *= 2)
+      if (ok(S) && t64 * S <= target && K / S >= min_st * bk) best = S;
+    return best;
+  }
+  // forward / bwd-data at the bench shapes (B=1024, widths 2048..100): the
+  // in-launch combine (slab round trip + ticket) costs more than the extra
+  // CUs buy back, so no split; the override keeps the others reachable
   return 1;
 }
 
@@ -1048,7 +1402,7 @@ int mmad_gemm_plan(int Mp, int Np, int K, int epi, int dtype) {
   const int env = mmad_tile_override();
   if (env >= 0 && env < NCFG && cfg_fits(env, Mp, Np, epi)) return env;
   std::lock_guard<std::mutex> lk(g_tune_mu);
-  auto it = g_tune.find(TuneKey{dtype, epi, Mp, Np, K});
+  auto it = g_tune.find(TuneKey{dtype, epi, Mp, Np, K, 0});
   return it != g_tune.end() ? it->second : heuristic_cfg(Mp, Np, epi);
 }
 
@@ -1060,19 +1414,28 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   MMAD_CHECK_ARG(dtype == MMAD_BF16 || dtype == MMAD_F32, "gemm: bad dtype %d", dtype);
   GemmEpi ep = ep_in;
   ep.dbg = mmad_dbg_override();
-  ep.splitk = (ep.sk_slab && ep.sk_ctl) ? mmad_gemm_splitk(Mp, Np, K, dtype) : 1;
+  const bool bnf = ep.bn_sync != nullptr;
+  MMAD_CHECK_ARG(!bnf || epi == GEMM_EPI_FWD || epi == GEMM_EPI_BWD_DATA,
+                 "gemm: fused BN only for the forward / bwd-data epilogues");
+  MMAD_CHECK_ARG(!bnf || Np / 64 <= MMAD_BN_EXIT, "gemm: fused BN: Np=%d too wide", Np);
+  // the fused BN barrier needs one block per output tile (no split) and the
+  // whole grid resident
+  ep.splitk = (ep.sk_slab && ep.sk_ctl && !bnf) ? mmad_gemm_splitk(Mp, Np, K, dtype, epi) : 1;
+  auto allowed = [&](int c) {
+    return c >= 0 && c < NCFG && cfg_fits(c, Mp, Np, epi) && (!bnf || coresident(dtype, epi, c, Mp, Np));
+  };
   const int env = mmad_tile_override();
   const int env_epi = ep.ad_p ? mmad_tile_adam_override() : mmad_tile_epi_override(epi);
   int cfg;
   const int force = ep.tile_force - 1;
-  if (force >= 0 && force < NCFG && cfg_fits(force, Mp, Np, epi)) {
+  if (allowed(force)) {
     cfg = force;
-  } else if (env_epi >= 0 && env_epi < NCFG && cfg_fits(env_epi, Mp, Np, epi)) {
+  } else if (allowed(env_epi)) {
     cfg = env_epi;
-  } else if (env >= 0 && env < NCFG && cfg_fits(env, Mp, Np, epi)) {
+  } else if (allowed(env)) {
     cfg = env;   // forced tile (tuning / tests); a shape it does not fit falls through
   } else {
-    const TuneKey key{dtype, epi, Mp, Np, K};
+    const TuneKey key{dtype, epi, Mp, Np, K, bnf ? 1 : 0};
     int found = -1;
     {
       std::lock_guard<std::mutex> lk(g_tune_mu);
@@ -1088,7 +1451,12 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
         int rc = tune_cfg(dtype, epi, A, lda, B, ldb, Mp, Np, K, ep, s, &cfg);
         if (rc != MMAD_OK) return rc;
       } else {
-        cfg = heuristic_cfg(Mp, Np, epi);
+        cfg = heuristic_cfg(Mp, Np, epi, allowed);
+        if (cfg < 0) {
+          mmad_set_error("gemm: no co-resident tile configuration for the fused BN epilogue "
+                         "(Mp=%d Np=%d)", Mp, Np);
+          return MMAD_EUNSUPPORTED;
+        }
       }
       std::lock_guard<std::mutex> lk(g_tune_mu);
       g_tune[key] = cfg;

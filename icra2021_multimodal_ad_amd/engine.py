@@ -199,7 +199,8 @@ class NativeAE:
         if need < 0:
             raise _native.NativeError("workspace size query failed")
         if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(need + 256, dtype=torch.uint8, device=self.device)
+            # zeroed: the split-K control words must start at zero
+            self._ws = torch.zeros(need + 256, dtype=torch.uint8, device=self.device)
         base = self._ws.data_ptr()
         aligned = (base + 255) // 256 * 256
         return ctypes.c_void_p(aligned), need

@@ -50,15 +50,23 @@ int mmad_pad_granule(void);
  * auto), knob 2 = per-shape autotune on first dispatch (1, default) or static
  * heuristic (0), knob 3 = diagnostics (tools/gemm_sweep; 4 = force the split-K
  * combine's timeout path, tests only), knob 4 = split-K
- * factor override for GEMMs given split-K workspace (0 = shape rule, 1/2/4),
+ * factor override for GEMMs given split-K workspace (0 = shape rule, 1/2/4/
+ * 8/16), knob 9 = the same for the dW GEMMs only, knobs 10 / 11 = the dW
+ * split rule's target number of 64x64-tile blocks (512) and minimum K stages
+ * per slice (8),
  * knob 5 = tile of the dW GEMMs with the fused Adam epilogue (default 3 =
  * 64x64; -1 = autotuned like the others), knobs 6 / 7 = tile of the bwd-data /
  * forward GEMMs (-1 = autotuned), knob 8 = tile of the Adam-fused dW GEMMs
  * run on the main stream at the end of the backward (-1 = knob 5).
  * Defaults from MMAD_GEMM_TILE / MMAD_GEMM_GROUP_M / MMAD_GEMM_AUTOTUNE /
  * MMAD_GEMM_SPLITK / MMAD_GEMM_TILE_ADAM / MMAD_GEMM_TILE_BWD_DATA /
- * MMAD_GEMM_TILE_FWD / MMAD_GEMM_TILE_ADAM_MAIN. */
+ * MMAD_GEMM_TILE_FWD / MMAD_GEMM_TILE_ADAM_MAIN / MMAD_GEMM_SPLITK_DW /
+ * MMAD_SPLITK_DW_BLOCKS / MMAD_SPLITK_DW_MIN_STAGES. */
 int mmad_tune_set(int knob, int value);
+/* The split-K factor the dispatcher picks for a padded GEMM shape (Mp x Np
+ * output, K deep) with epilogue `epi` (0 fwd, 1 MSE, 2 bwd-data, 3 dW,
+ * 4 score) under the current knobs: 1, 2, 4, 8 or 16 (query only). */
+int mmad_gemm_splitk_for(int Mp, int Np, int K, int dtype, int epi);
 
 /* ------------------------------------------------------------------------
  * Layer operators

@@ -1,0 +1,128 @@
+"""Train-mode BatchNorm fused into the producing GEMMs (MMAD_BN_MODE=2): the
+forward GEMM's epilogue finishes the whole-batch statistics and writes
+y = BN(a), the bwd-data GEMM's epilogue writes dz (per-column-tile barrier
+between the blocks of one output column; csrc/mmad_gemm_mfma.hip).
+
+Pinned against the reference goldens (fp32: the same bars as
+test_gpu_parity.py's train-step test -- loss rtol 1e-4, gradients within 1e-4
+of max|g| of the fp64 truth or 2x the reference's own fp32 deviation, running
+statistics rtol 1e-4), against the kernel-per-phase schedule (MMAD_BN_MODE=0)
+at the BASELINE C2 / C3 shapes, and for determinism (bit-identical repeats,
+bit-identical across forced tile configurations)."""
+import numpy as np
+import pytest
+import torch
+
+from icra2021_multimodal_ad_amd.common_utils import init_state_dict
+from icra2021_multimodal_ad_amd.data import synth_windows
+from icra2021_multimodal_ad_amd import _native
+
+from tests.test_gpu_parity import _model, _sd, _rel, _grads_flat, assert_grads_close, CASES
+
+pytestmark = pytest.mark.gpu
+
+
+def _mk(monkeypatch, mode, *a, **kw):
+    monkeypatch.setenv("MMAD_BN_MODE", str(mode))
+    return _model(*a, **kw)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_fused_bn_fp32_train_step_matches_reference(golden, name, monkeypatch):
+    g = golden(name)
+    d, btl, nl = int(g["meta_d"]), int(g["meta_btl"]), int(g["meta_n_layers"])
+    m, _ = _mk(monkeypatch, 2, d, btl, nl, _sd(g, "init/"))
+    x = torch.from_numpy(g["x/0"]).cuda()
+    loss = float(m._native.train_step(x))
+    m._native.check_status()
+    assert abs(loss - g["step1/loss"]) <= 1e-4 * g["step1/loss"]
+    assert_grads_close(_grads_flat(m), g, name)
+    sd = m.state_dict()
+    for k in sd:
+        if "running" in k:
+            assert _rel(sd[k].cpu().numpy(), g["after0/" + k]) < 1e-4, k
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_fused_bn_matches_kernel_schedule_c2(dtype, monkeypatch):
+    """C2 shape (D=2048, B=1024): fused vs kernel-per-phase, 3 Adam steps.
+    Step 1 (same parameters): fp32 loss rtol 1e-5 and per-layer weight
+    gradients within 5e-3 relative Frobenius of each other (this BN stack is
+    ill-conditioned at full size: fp32 implementations sit ~1e-3 from the
+    float64 truth, test_gpu_vib_full.py, which also pins the fused path
+    against that truth); bf16 loss within 1 % and gradient cosine > 0.999.  Later steps: the sign(g) amplification band the
+    reference's own trajectory test uses (Adam's first steps are nearly
+    sign(g) * lr: rounding-level gradient differences move single parameters
+    by up to 2 lr) -- fp32 loss within 5e-3 / 2e-2 at steps 2 / 3, running
+    statistics rtol 1e-3; bf16 loss within 1 %."""
+    sd = init_state_dict(2048, 100, 5, seed=11)
+    ma, _ = _mk(monkeypatch, 2, 2048, 100, 5, sd, dtype=dtype)
+    mb, _ = _mk(monkeypatch, 0, 2048, 100, 5, sd, dtype=dtype)
+    ma._native.sync_shadow(force=True)
+    mb._native.sync_shadow(force=True)
+    for s in range(3):
+        x = torch.from_numpy(synth_windows(1024, 2048, seed=50 + s)).cuda()
+        la = float(ma._native.train_step(x))
+        lb = float(mb._native.train_step(x))
+        if s == 0:
+            for l, L in enumerate(ma._native.layers):
+                n = L["Np"] * L["Kp"]
+                ga = ma._native.grads[L["w_off"]:L["w_off"] + n].double()
+                gb = mb._native.grads[L["w_off"]:L["w_off"] + n].double()
+                cos = float((ga * gb).sum() / (ga.norm() * gb.norm() + 1e-30))
+                assert cos > (0.99999 if dtype == "f32" else 0.999), (l, cos)
+                if dtype == "f32":
+                    fro = float((ga - gb).norm() / (gb.norm() + 1e-30))
+                    assert fro <= 5e-3, (l, fro)
+        tol = [1e-5, 5e-3, 2e-2][s] if dtype == "f32" else 1e-2
+        assert abs(la - lb) <= tol * abs(lb), (s, la, lb)
+        ma._native.adam()
+        mb._native.adam()
+    ma._native.check_status()
+    torch.cuda.synchronize()
+    if dtype == "f32":
+        assert _rel(ma._native.running.cpu().numpy(), mb._native.running.cpu().numpy()) < 1e-3
+
+
+def test_fused_bn_fused_adam_step_c3_vib(monkeypatch):
+    """C3 shape (VIB-AE, D=2048, B=4096, bf16) through the single-call fused
+    step (dW+Adam on the side stream): finite, within 1 % of the
+    kernel-per-phase loss over 3 steps, no barrier timeout."""
+    sd = init_state_dict(2048, 100, 5, seed=12, enc_out=200)
+    ma, _ = _mk(monkeypatch, 2, 2048, 100, 5, sd, dtype="bf16", models="vib_ae", k=1)
+    mb, _ = _mk(monkeypatch, 0, 2048, 100, 5, sd, dtype="bf16", models="vib_ae", k=1)
+    ma._native.sync_shadow(force=True)
+    mb._native.sync_shadow(force=True)
+    eps = torch.randn(1, 4096, 100, device="cuda")
+    for s in range(3):
+        x = torch.from_numpy(synth_windows(4096, 2048, seed=60 + s)).cuda()
+        la = float(ma._native.train_step_fused(x, eps=eps, beta_kl=1.0))
+        lb = float(mb._native.train_step_fused(x, eps=eps, beta_kl=1.0))
+        assert np.isfinite(la)
+        assert abs(la - lb) <= 1e-2 * abs(lb), (s, la, lb)
+    ma._native.check_status()
+
+
+def test_fused_bn_deterministic_and_tile_independent(monkeypatch):
+    """Same inputs -> bit-identical loss / grads / running stats, whichever
+    co-resident tile configuration each GEMM gets (knob 0 forces one)."""
+    sd = init_state_dict(2048, 100, 5, seed=13)
+    x = torch.from_numpy(synth_windows(1024, 2048, seed=70)).cuda()
+    lib = _native.load()
+    outs = []
+    try:
+        for tile in (-1, -1, 3, 4, 0):
+            lib.mmad_tune_set(0, tile)
+            m, _ = _mk(monkeypatch, 2, 2048, 100, 5, sd, dtype="bf16")
+            m._native.sync_shadow(force=True)
+            loss = m._native.train_step(x).clone()
+            m._native.check_status()
+            outs.append((loss, m._native.grads.clone(), m._native.running.clone()))
+    finally:
+        lib.mmad_tune_set(0, -1)
+    for o in outs[1:]:
+        # the loss is summed from one partial per MSE output tile: tile-dependent order
+        assert abs(float(outs[0][0]) - float(o[0])) <= 1e-5 * abs(float(o[0]))
+        assert torch.equal(outs[0][1], o[1])
+        assert torch.equal(outs[0][2], o[2])
+    assert torch.equal(outs[0][0], outs[1][0])   # same tiles: bit-identical loss too

@@ -81,8 +81,12 @@ def _torch_cpu_grads(x, sd, eps):
     return float(loss.detach()), {n: p.grad.double().numpy() for n, p in m.named_parameters()}
 
 
-@pytest.mark.parametrize("d", [2048, 1728])
-def test_vib_ae_full_size_fp32_matches_oracle(d):
+@pytest.mark.parametrize("d,bn_mode", [(2048, None), (1728, None), (2048, "2")])
+def test_vib_ae_full_size_fp32_matches_oracle(d, bn_mode, monkeypatch):
+    """bn_mode "2": train-mode BN fused into the producing GEMMs (the layers
+    whose grid is co-resident; the rest fall back to the apply kernels)."""
+    if bn_mode is not None:
+        monkeypatch.setenv("MMAD_BN_MODE", bn_mode)
     sd = init_state_dict(d, 100, 5, seed=40 + d % 7, enc_out=200)
     x = synth_windows(B, d, seed=41)
     eps = np.random.default_rng(42).standard_normal((K_SAMPLES, B, 100)).astype(np.float32)
