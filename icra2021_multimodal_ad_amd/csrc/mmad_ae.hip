@@ -103,8 +103,16 @@ struct mmad_ae {
   // bwd-data GEMM's epilogue writes dz (a per-column-tile barrier between the
   // blocks of one column, mmad_gemm_mfma.hip) -- no finalize / fold / apply
   // launches.  Layers whose grid cannot be co-resident fall back to mode 0
-  // (apply kernels).  0 = apply kernels, 1 = fold, 2 = fused.
+  // (apply kernels).  0 = apply kernels, 1 = fold, 2 = fused.  Default: bf16
+  // 2 up to bn_fused_rows padded rows per call (measured: D=2048 B=1024
+  // 0.495 ms/step fused vs 0.531 apply vs 0.536 fold; B=4096 VIB 1.33 fused
+  // vs 1.32 apply vs 1.27 fold -- more tiles per column, longer barrier
+  // waits), fold above; fp32 0 (the parity path).
   int bn_mode = 0;
+  int bn_fused_rows = [] {
+    const char* e = getenv("MMAD_BN_FUSED_MAX_ROWS");
+    return e ? atoi(e) : 2048;
+  }();
   // fused step: record the "bwd-data of l done" event only every ev_every-th
   // side-stream layer (each record costs a bubble on the main stream); the dW
   // GEMMs of the layers in between wait for the next recorded one
@@ -197,6 +205,7 @@ struct AeWS {
   unsigned* sk_ctl[2];
   size_t sk_ctl_bytes;   // both split-K control blocks + the fused-BN counters
   unsigned* bn_err;      // fused-BN barrier timeout word
+  int bn_mode;           // this call's train-mode BN schedule (0 apply, 1 fold, 2 fused)
   std::vector<LayerWS> l;
   int64_t bytes;
 };
@@ -314,11 +323,11 @@ int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, i
   {
     const char* e = getenv("MMAD_BN_FOLD");
     h->fold = e ? (atoi(e) != 0) : (dtype == MMAD_BF16);
-    h->bn_mode = h->fold ? 1 : 0;
+    h->bn_mode = e ? (h->fold ? 1 : 0) : (dtype == MMAD_BF16 ? 2 : 0);
     const char* m = getenv("MMAD_BN_MODE");
     if (m && atoi(m) >= 0 && atoi(m) <= 2) {
       h->bn_mode = atoi(m);
-      h->fold = h->bn_mode == 1;
+      h->fold = h->bn_mode != 0 && dtype == MMAD_BF16;   // fold: mode 1, mode 2's fallback
     }
   }
   for (int side = 0; side < 2; ++side) {
@@ -465,7 +474,7 @@ static const void* input_of(const mmad_ae* h, const AeWS& w, int l, bool train,
   const AeLayer& p = h->L[l - 1];
   const LayerWS& ps = w.l[l - 1];
   if (!p.bn) return ps.out;
-  if (!train || !h->fold) return ps.y;
+  if (!train || w.bn_mode != 1) return ps.y;
   *scale = ps.scale;
   *shift = ps.shift;
   return ps.out;
@@ -490,6 +499,9 @@ static int prepare_ws(const mmad_ae* h, int B, int k, void* ws, int64_t ws_bytes
   // every split GEMM leaves them zero again, so a workspace is zeroed once
   // when this handle first sees it (and mmad_ae_status re-zeroes after a
   // timed-out combine); only when a split can be chosen at all
+  w.bn_mode = h->bn_mode;
+  if (w.bn_mode == 2 && w.Mpd > h->bn_fused_rows) w.bn_mode = h->fold ? 1 : 0;
+  if (w.bn_mode == 1 && !h->fold) w.bn_mode = 0;
   if ((splitk_possible(h->dtype) || h->bn_mode == 2) && ws != h->ws_zeroed) {
     MMAD_HIP_CHECK(hipMemsetAsync(w.sk_ctl[0], 0, w.sk_ctl_bytes, st));
     const_cast<mmad_ae*>(h)->ws_zeroed = ws;
@@ -584,7 +596,7 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
     } else if (a.bn && train) {
       GemmEpi ep = fwd_epi(h, w, a, s, M, s.out, folded);
       ep.part = s.stats;
-      s.fwd_fused = h->bn_mode == 2 && mmad_gemm_bn_fusable(dt, GEMM_EPI_FWD, Mp, a.Np);
+      s.fwd_fused = w.bn_mode == 2 && mmad_gemm_bn_fusable(dt, GEMM_EPI_FWD, Mp, a.Np);
       if (s.fwd_fused) {
         // BN finished inside the GEMM: a (for the backward) and y = BN(a)
         ep.bn_sync = s.sync_f;
@@ -603,7 +615,7 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
                      PROBE_FWD + l));
       if (s.fwd_fused) {
         // nothing left to launch
-      } else if (!h->fold) {
+      } else if (w.bn_mode != 1) {
         // exact-fp32 path: normalise into y (the consumer GEMM and its dW read
         // y as the reference's layers do: no fold, no fix-up cancellation)
         RET_IF(mmad_bn_train_apply(dt, M, a.N, Mp, a.Np, s.out, s.stats, h->params + a.g_off,
@@ -745,7 +757,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
         ep.bn_mean = ps.mean;
         ep.bn_rstd = ps.rstd;
         ep.bn_part = ps.bnpart;
-        ps.bwd_fused = h->bn_mode == 2 && mmad_gemm_bn_fusable(dt, GEMM_EPI_BWD_DATA, Mp, a.Kp);
+        ps.bwd_fused = w.bn_mode == 2 && mmad_gemm_bn_fusable(dt, GEMM_EPI_BWD_DATA, Mp, a.Kp);
         if (ps.bwd_fused) {
           // BN + activation backward of layer l-1 inside this GEMM: dz directly
           ep.out = nullptr;

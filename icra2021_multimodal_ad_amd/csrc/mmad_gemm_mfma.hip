@@ -263,19 +263,42 @@ __device__ __forceinline__ double ld_sc1(const double* p) {
                                                       __HIP_MEMORY_SCOPE_AGENT));
 }
 
-// Barrier of the `target` blocks sharing one output column tile.  Bounded:
-// a barrier that does not complete within ~2^20 polls (about a second) sets
-// the sticky error word and returns false (the caller skips its outputs; the
-// host reports it through mmad_ae_status) instead of hanging the GPU.
-__device__ __forceinline__ bool col_barrier(unsigned* arrive, unsigned target, unsigned* err,
-                                            int tid, unsigned* shw) {
+// Barrier of the `target` blocks sharing one output column tile: counter
+// ctr[0] and generation word ctr[MMAD_BN_EXIT].  Each block reads the
+// generation (`gen0`, read before it arrives: the caller loads it early),
+// adds one arrival; the last arriver resets the counter and bumps the
+// generation, the others poll the generation (sc1).  The counter is zero
+// again when the barrier opens, whatever tile configuration used it last.
+// Bounded: a barrier that does not open within ~2^20 polls (about a second)
+// sets the sticky error word and returns false (the caller skips its
+// outputs; the host reports it through mmad_ae_status) instead of hanging.
+__device__ __forceinline__ unsigned col_gen(const unsigned* ctr) {
+  return __hip_atomic_load(ctr + MMAD_BN_EXIT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// arrive: after every wave's partial stores have landed, one lane adds an
+// arrival; the last arriver resets the counter and opens the barrier
+__device__ __forceinline__ void col_arrive(unsigned* ctr, unsigned target, int tid, unsigned* shw) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's partial stores landed
   __syncthreads();                                   // ... and every other wave's
   if (tid == 0) {
-    __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned ok = 0u;
-    for (unsigned spins = 0; spins < (1u << 20); ++spins) {
-      if (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) {
+    const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned last = 0u;
+    if (old + 1u == target) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(ctr + MMAD_BN_EXIT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = 1u;
+    }
+    shw[1] = last;   // read by lane 0 only (col_wait)
+  }
+}
+// wait: lane 0 polls the generation word unless its block arrived last; the
+// block joins it at a workgroup barrier (then reads the partials, sc1)
+__device__ __forceinline__ bool col_wait(unsigned* ctr, unsigned gen0, unsigned* err, int tid,
+                                         unsigned* shw) {
+  if (tid == 0) {
+    unsigned ok = shw[1];
+    for (unsigned spins = 0; !ok && spins < (1u << 20); ++spins) {
+      if (col_gen(ctr) != gen0) {
         ok = 1u;
         break;
       }
@@ -286,19 +309,6 @@ __device__ __forceinline__ bool col_barrier(unsigned* arrive, unsigned target, u
   }
   __syncthreads();
   return shw[0] != 0u;
-}
-
-// every block of the column has read the partials: the last one out resets
-// both counters for the next launch (stream-ordered after this one)
-__device__ __forceinline__ void col_exit(unsigned* arrive, unsigned* exitc, unsigned target, int tid) {
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned old = __hip_atomic_fetch_add(exitc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1u == target) {
-      __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(exitc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 }  // namespace
@@ -332,7 +342,10 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   constexpr int OSTRIDE = BN * (int)sizeof(TO) + 16;
   constexpr int OBYTES = BM * OSTRIDE + (EPI == GEMM_EPI_BWD_DATA ? BM * BN / 2 : 0);   // + fp64 [BM/16][BN]
   // fused train-mode BN: per-column merge results (2 x fp64 [BN]) + a flag word
-  constexpr int XBYTES = (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_BWD_DATA) ? 2 * BN * 8 + 64 : 0;
+  // (fwd: 4 chunk-group Welford merges + scale/shift; bwd-data: the sums --
+  // its chunk-group sums reuse the fp64 piece scratch)
+  constexpr int XBYTES = EPI == GEMM_EPI_FWD ? 12 * BN * 8 + 2 * BN * 4 + 64
+                         : EPI == GEMM_EPI_BWD_DATA ? 6 * BN * 8 + 64 : 0;
   constexpr int LDS_BYTES = (NS * SLOT > OBYTES + XBYTES) ? NS * SLOT : OBYTES + XBYTES;
   static_assert((NS - 1) * NL <= 63, "vmcnt range");
   static_assert(LDS_BYTES <= 163840, "LDS budget");
@@ -395,6 +408,12 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         }
       }
     }
+  }
+  // fused BN: this column's barrier generation, read before this block can
+  // arrive (its latency hides under the main loop)
+  unsigned gen0 = 0u;
+  if constexpr (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_BWD_DATA) {
+    if (ep.bn_sync && tid == 0) gen0 = col_gen(ep.bn_sync + tn);
   }
   float e_g[QG];
   // db[n] (bias gradient of this layer's output n) is needed by the dW fix-up
@@ -736,6 +755,12 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   }
 
   // ===================== epilogue, LDS-staged coalesced store ===============
+  // fused BN (forward): the Welford partials are out -- arrive at the column
+  // barrier now, store the a tile while the other blocks catch up
+  unsigned* bn_shw = (unsigned*)(smem + OBYTES + XBYTES - 64);
+  if constexpr (EPI == GEMM_EPI_FWD) {
+    if (ep.bn_sync) col_arrive(ep.bn_sync + tn, (unsigned)(ntl / ep.tiles_n), tid, bn_shw);
+  }
   __syncthreads();  // main-loop LDS no longer read
   if constexpr (EPI == GEMM_EPI_MSE) {
     if (ep.lossp) {
@@ -872,34 +897,60 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
       // the column computes the same bits), then y = a*scale + shift from the
       // fp32 activations still in registers
       const unsigned tiles_m = (unsigned)(ntl / ep.tiles_n);
-      unsigned* shw = (unsigned*)(smem + OBYTES + 2 * BN * 8);
-      if (!col_barrier(ep.bn_sync + tn, tiles_m, ep.bn_err, tid, shw)) return;
-      float* s_sc = (float*)(smem + OBYTES);
+      double* s_gn = (double*)(smem + OBYTES);          // [4][BN] group merges
+      double* s_gm = s_gn + 4 * BN;
+      double* s_gq = s_gm + 4 * BN;
+      float* s_sc = (float*)(s_gq + 4 * BN);
       float* s_sh = s_sc + BN;
+      static_assert(12 * BN * 8 + 2 * BN * 4 <= XBYTES - 64, "fused-BN scratch");
+      if (!col_wait(ep.bn_sync + tn, gen0, ep.bn_err, tid, bn_shw)) return;
+      {
+        // chunk group q (= 0..3) merges partials q, q+4, ... in order (Chan et
+        // al. pairwise update); the threads of a column split the groups;
+        // every partial of a group is loaded before the first use
+        constexpr int NGT = NT / BN;
+        const int cc = tid % BN, grp = tid / BN, col = n0 + cc;
+        const int nparts = (int)tiles_m * BM / MMAD_PART_ROWS;   // a multiple of 4
+        for (int q = grp; q < 4; q += NGT) {
+          double n = 0.0, mean = 0.0, m2 = 0.0;
+          constexpr int U = 8;
+          for (int u0 = 0; u0 < nparts / 4; u0 += U) {
+            float mb[U], qb[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const int i = q + 4 * min(u0 + u, nparts / 4 - 1);
+              mb[u] = ld_sc1(ep.part + (size_t)i * 2 * ep.ldpart + col);
+              qb[u] = ld_sc1(ep.part + ((size_t)i * 2 + 1) * ep.ldpart + col);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const int i = q + 4 * (u0 + u);
+              int cnt = ep.M - i * MMAD_PART_ROWS;
+              cnt = cnt < 0 ? 0 : (cnt > MMAD_PART_ROWS ? MMAD_PART_ROWS : cnt);
+              if (u0 + u >= nparts / 4 || cnt == 0) continue;
+              const double nb = (double)cnt, nn = n + nb, d = (double)mb[u] - mean;
+              mean += d * (nb / nn);
+              m2 += (double)qb[u] + d * d * (n * nb / nn);
+              n = nn;
+            }
+          }
+          s_gn[q * BN + cc] = n;
+          s_gm[q * BN + cc] = mean;
+          s_gq[q * BN + cc] = m2;
+        }
+      }
+      __syncthreads();
       if (tid < BN) {
         const int c = n0 + tid;
-        const int nparts = (int)tiles_m * BM / MMAD_PART_ROWS;
-        constexpr int U = 16;
         double n = 0.0, mean = 0.0, m2 = 0.0;
-        for (int i0 = 0; i0 < nparts; i0 += U) {
-          float mb[U], qb[U];
 #pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int i = i0 + u < nparts ? i0 + u : nparts - 1;
-            mb[u] = ld_sc1(ep.part + (size_t)i * 2 * ep.ldpart + c);
-            qb[u] = ld_sc1(ep.part + ((size_t)i * 2 + 1) * ep.ldpart + c);
-          }
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int i = i0 + u;
-            int cnt = ep.M - i * MMAD_PART_ROWS;
-            cnt = cnt < 0 ? 0 : (cnt > MMAD_PART_ROWS ? MMAD_PART_ROWS : cnt);
-            if (i >= nparts || cnt == 0) continue;
-            const double nb = (double)cnt, nn = n + nb, d = (double)mb[u] - mean;
-            mean += d * (nb / nn);
-            m2 += (double)qb[u] + d * d * (n * nb / nn);
-            n = nn;
-          }
+        for (int q = 0; q < 4; ++q) {
+          const double nb = s_gn[q * BN + tid];
+          if (nb == 0.0) continue;
+          const double nn = n + nb, d = s_gm[q * BN + tid] - mean;
+          mean += d * (nb / nn);
+          m2 += s_gq[q * BN + tid] + d * d * (n * nb / nn);
+          n = nn;
         }
         const float var = n > 0.0 ? (float)(m2 / n) : 0.f;
         const float mu = (float)mean;
@@ -933,7 +984,9 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
           for (int r = 0; r < 4; ++r) {
             const int rl = wm * 16 * TM + i * 16 + 4 * g + r;
             const int cl = wn * 16 * TN + j * 16 + c;
-            const float yv = m0 + rl < ep.M ? acc[i][j][r] * s_sc[cl] + s_sh[cl] : 0.f;
+            // from the stored (TO-rounded) a, as the backward's xhat sees it
+            const float av = to_f32<TO>(from_f32<TO>(acc[i][j][r]));
+            const float yv = m0 + rl < ep.M ? av * s_sc[cl] + s_sh[cl] : 0.f;
             *(TO*)(smem + rl * OSTRIDE + cl * (int)sizeof(TO)) = from_f32<TO>(yv);
           }
       __syncthreads();
@@ -945,7 +998,6 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
         *(uint4v*)(yo + (size_t)(m0 + rl) * ep.ldo + n0 + ch * OEPC) = v;
       }
-      col_exit(ep.bn_sync + tn, ep.bn_sync + MMAD_BN_EXIT + tn, tiles_m, tid);
     }
   }
   if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
@@ -993,6 +1045,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
       const TO* an = (const TO*)ep.bn_a;
       double* scr = (double*)(smem + BM * OSTRIDE);    // [PIECES][BN]
       double ps1[PPT], ps2[PPT];
+      float areg[PPT][16];
 #pragma unroll
       for (int u = 0; u < PPT; ++u) {
         const int pc = grp + u * NG;
@@ -1002,7 +1055,9 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
           for (int r = 0; r < 16; ++r) {
             const int rl = pc * 16 + r;
             const double dy = to_f32<TO>(*(const TO*)(smem + rl * OSTRIDE + cc * (int)sizeof(TO)));
-            const double av = to_f32<TO>(an[(size_t)(m0 + rl) * ep.ldo + col]);
+            const float avf = to_f32<TO>(an[(size_t)(m0 + rl) * ep.ldo + col]);
+            areg[u][r] = avf;   // kept for the fused dz below
+            const double av = avf;
             s1 += dy;
             s2 += dy * ((av - mu) * rs);
           }
@@ -1034,27 +1089,44 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         // dz = act'(a) * gamma*rstd/M * (M dy - sum dy - xhat sum dy*xhat)
         // (fp64 bracket, as bn_bwd_apply_k) in place in the staged tile
         const unsigned tiles_m = (unsigned)(ntl / ep.tiles_n);
-        unsigned* shw = (unsigned*)(smem + OBYTES + 2 * BN * 8);
-        if (!col_barrier(ep.bn_sync + tn, tiles_m, ep.bn_err, tid, shw)) return;
-        double* s_t1 = (double*)(smem + OBYTES);
+        double* s_g1 = scr;                               // [4][BN] group sums (scr is free here)
+        double* s_g2 = (double*)(smem + OBYTES);          // [4][BN]
+        double* s_t1 = s_g2 + 4 * BN;
         double* s_t2 = s_t1 + BN;
+        static_assert(PIECES >= 4, "group sums need 4 x BN doubles of the piece scratch");
+        static_assert(6 * BN * 8 <= XBYTES - 64, "fused-BN scratch");
+        col_arrive(ep.bn_sync + tn, tiles_m, tid, bn_shw);
+        if (!col_wait(ep.bn_sync + tn, gen0, ep.bn_err, tid, bn_shw)) return;
+        {
+          // chunk group q (= 0..3) sums partials q, q+4, ... in order; the
+          // threads of a column split the groups, each group's loads in flight
+          // together; then ((g0 + g1) + g2) + g3
+          const int nch = (int)tiles_m * BM / 64;
+          for (int q = grp; q < 4; q += NG) {
+            double t1 = 0.0, t2 = 0.0;
+            constexpr int U = 8;
+            const int per = (nch - q + 3) / 4;          // chunks q, q+4, ... < nch
+            for (int u0 = 0; u0 < per; u0 += U) {
+              double p1[U], p2[U];
+#pragma unroll
+              for (int u = 0; u < U; ++u) {
+                const int i = q + 4 * min(u0 + u, per - 1);
+                p1[u] = ld_sc1(ep.bn_part + (size_t)i * 2 * ep.ldo + col);
+                p2[u] = ld_sc1(ep.bn_part + ((size_t)i * 2 + 1) * ep.ldo + col);
+              }
+#pragma unroll
+              for (int u = 0; u < U; ++u)
+                if (u0 + u < per) { t1 += p1[u]; t2 += p2[u]; }
+            }
+            s_g1[q * BN + cc] = t1;
+            s_g2[q * BN + cc] = t2;
+          }
+        }
+        __syncthreads();
         if (tid < BN) {
           const int c = n0 + tid;
-          const int nch = (int)tiles_m * BM / 64;
-          constexpr int U = 16;
-          double t1 = 0.0, t2 = 0.0;
-          for (int i0 = 0; i0 < nch; i0 += U) {
-            double p1[U], p2[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-              const int i = i0 + u < nch ? i0 + u : nch - 1;
-              p1[u] = ld_sc1(ep.bn_part + (size_t)i * 2 * ep.ldo + c);
-              p2[u] = ld_sc1(ep.bn_part + ((size_t)i * 2 + 1) * ep.ldo + c);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-              if (i0 + u < nch) { t1 += p1[u]; t2 += p2[u]; }
-          }
+          double t1 = ((s_g1[tid] + s_g1[BN + tid]) + s_g1[2 * BN + tid]) + s_g1[3 * BN + tid];
+          double t2 = ((s_g2[tid] + s_g2[BN + tid]) + s_g2[2 * BN + tid]) + s_g2[3 * BN + tid];
           if (c >= ep.N) { t1 = 0.0; t2 = 0.0; }
           if (tm == 0) {
             ep.bn_dbeta[c] = (float)t1;
@@ -1078,7 +1150,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
               const int rl = pc * 16 + r;
               TO* slot = (TO*)(smem + rl * OSTRIDE + cc * (int)sizeof(TO));
               const double dy = to_f32<TO>(*slot);
-              const float av = to_f32<TO>(an[(size_t)(m0 + rl) * ep.ldo + col]);
+              const float av = areg[u][r];
               const double xh = ((double)av - mu) * rs;
               const double da = cf * (Md * dy - t1 - xh * t2);
               float d = (float)(da * (double)act_grad_from_out(av, ep.bn_act, ep.slope));
@@ -1113,7 +1185,6 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
           const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
           *(uint4v*)(dzo + (size_t)(m0 + rl) * ep.ldo + n0 + ch * OEPC) = v;
         }
-        col_exit(ep.bn_sync + tn, ep.bn_sync + MMAD_BN_EXIT + tn, tiles_m, tid);
       }
     }
   }

