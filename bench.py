@@ -107,10 +107,18 @@ def dw_adam_bytes(N, K, B, es=2):
     return 26 * N * K + es * B * (N + K)
 
 
-def pick_dominant_layer(nat):
-    """Largest parameter count (ties: the first, encoder layer 1)."""
-    best = max(range(len(nat.layers)), key=lambda l: (nat.layers[l]["N"] * nat.layers[l]["K"], -l))
-    return best
+def pick_dominant_layer(nat, batch):
+    """Largest parameter count among the layers whose dW GEMM carries the
+    fused Adam epilogue.  Below 4096 windows every layer does (ties: the
+    first, encoder layer 1, on the main stream at the end of the chain); from
+    4096 windows (MMAD_DW_SPLIT default) layers 0 and 1 (l < MMAD_DW_MAIN = 2)
+    run as a dW GEMM + flat Adam pass instead (ties: the last, the decoder's
+    output layer on the side stream)."""
+    sp = os.environ.get("MMAD_DW_SPLIT", "-1")
+    split = sp not in ("-1", "0") or (sp == "-1" and batch >= 4096)
+    if not split:
+        return max(range(len(nat.layers)), key=lambda l: (nat.layers[l]["N"] * nat.layers[l]["K"], -l))
+    return max(range(2, len(nat.layers)), key=lambda l: (nat.layers[l]["N"] * nat.layers[l]["K"], l))
 
 
 def _pmc_file(kind, workload):
@@ -258,7 +266,7 @@ def run(args):
     for i in range(args.warmup):
         model.train_step_async(pool[i % len(pool)], opt)
     torch.cuda.synchronize()
-    probe_layer = pick_dominant_layer(nat)
+    probe_layer = pick_dominant_layer(nat, batch)
     lib = _native.load()
     if world > 1:
         dist.barrier()

@@ -75,6 +75,19 @@ struct mmad_ae {
   }();
   hipStream_t tail = nullptr;
   hipEvent_t ev_tail = nullptr;
+  // fused step, layers < dw_main (the end of the backward chain): the dW
+  // GEMM (with the small-segment Adam in its epilogue) and a flat Adam pass
+  // over the weights instead of one Adam-fused dW GEMM: layer l >= 1's GEMM
+  // starts on the tail stream as soon as dz_l exists, its Adam once
+  // bwd-data(l) has read W_l, both overlapping the end of the chain
+  // (MMAD_DW_SPLIT=0: the fused form on the main stream).  Default (-1): split
+  // from 4096 rows per call (VIB D=2048 B=4096: 1.217 vs 1.244 ms/step), fused
+  // below (D=2048 B=1024: 0.496 fused vs 0.520 split -- the early dW_1 GEMM
+  // slows the bwd-data chain it overlaps; profiles/r02o_*)
+  int dw_split = [] {
+    const char* e = getenv("MMAD_DW_SPLIT");
+    return e ? atoi(e) : -1;
+  }();
   int mse_tiles = 0;   // loss partials written by the last MSE GEMM
   // data parallelism: RCCL communicator (not owned), its stream and events
   mmad_comm* comm = nullptr;
@@ -420,7 +433,7 @@ int mmad_ae_bind(mmad_ae* h, float* params, float* grads, float* adam_m, float* 
       MMAD_HIP_CHECK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking,
                                                  (sp && atoi(sp) == 1) ? greatest : least));
     }
-    if (h->dw_tail) MMAD_HIP_CHECK(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
+    if (h->dw_tail || h->dw_split) MMAD_HIP_CHECK(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
     const size_t n = h->L.size();
     h->ev_fork.resize(n);
     h->ev_data.resize(n);
@@ -691,6 +704,45 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
   hipStream_t side = h->side;
   std::vector<PendingDW> pending;   // side-stream dW GEMMs waiting for a recorded event
   bool used_tail = false;
+  // layer l's Adam terms for a dW epilogue: the weight tile's (ad_*, unless
+  // weights_too is false) and the small segment [bias | gamma | beta]'s
+  auto fill_adam = [&](GemmEpi& e, int l, bool weights_too) {
+    const AeLayer& a = h->L[l];
+    const BiasSrc bs = bias_src(h, w, l, from_mse);
+    if (weights_too) {
+      e.ad_p = h->params + a.w_off;
+      e.ad_m = h->m + a.w_off;
+      e.ad_v = h->v + a.w_off;
+      e.ad_shadow = adam_shadow(h, a);
+      // the gradient is consumed by the fused Adam in registers; materialise
+      // it only when asked (h->keep_grads)
+      e.dw_nostore = h->keep_grads ? 0 : 1;
+    }
+    e.ad_b1 = adam->b1;
+    e.ad_b2 = adam->b2;
+    e.ad_eps = adam->eps;
+    e.ad_step = adam->step_size;
+    e.ad_bc2 = adam->bc2_sqrt;
+    e.dyn = w.dyn;
+    e.sm_p = h->params + a.b_off;
+    e.sm_g = h->grads + a.b_off;
+    e.sm_m = h->m + a.b_off;
+    e.sm_v = h->v + a.b_off;
+    e.sm_n = a.bn ? 3 * a.Np : a.Np;
+    e.gb_src = bs.src;
+    e.gb_parts = bs.nparts;
+    e.gb_stride = bs.stride;
+    e.sm_bN = a.N;
+    e.sm_bNp = a.Np;
+  };
+  // the flat Adam pass over layer l's weight tile (split layers)
+  auto weight_adam = [&](int l, hipStream_t s_) -> int {
+    const AeLayer& a = h->L[l];
+    const int64_t n = (int64_t)a.Np * a.Kp;
+    return mmad_adam_dyn(n, h->params + a.w_off, h->grads + a.w_off, h->m + a.w_off, h->v + a.w_off,
+                         adam->b1, adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt,
+                         adam_shadow(h, a), h->dtype == MMAD_BF16 ? n : 0, w.dyn, s_);
+  };
   for (int l = nL - 1; l >= 0; --l) {
     const AeLayer& a = h->L[l];
     LayerWS& s = w.l[l];
@@ -723,8 +775,11 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     // the DP exchange and by side-stream dW GEMMs (every ev_every-th layer;
     // the lowest side layer always records, flushing the deferred ones)
     const bool side_dw = adam && !dp && !ping && l >= h->dw_main;
-    const bool tail_dw = adam && !dp && !ping && h->tail && l > 0 && l < h->dw_main;
-    const bool rec = dp || tail_dw ||
+    const bool split = adam && !dp && !ping && h->tail && l < h->dw_main &&
+                       (h->dw_split > 0 || (h->dw_split < 0 && w.Mpe >= 4096));
+    const bool tail_dw = adam && !dp && !ping && !split && h->tail && h->dw_tail && l > 0 &&
+                         l < h->dw_main;
+    const bool rec = dp || tail_dw || split ||
                      (side_dw && (h->ev_every <= 1 || l == h->dw_main ||
                                   (l - h->dw_main) % h->ev_every == 0));
     if (!adam || dp) {
@@ -734,6 +789,18 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
                      nullptr, PROBE_DW + l));
       if (dp) MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l], side));
+    }
+    if (split && l > 0) {
+      // dz_l is complete on the main stream: dW_l (+ the small-segment Adam)
+      // on the tail stream now, overlapping bwd-data(l)
+      GemmEpi e = dwe;
+      fill_adam(e, l, false);
+      e.tile_force = mmad_tile_adam_main_override() + 1;
+      MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
+      MMAD_HIP_CHECK(hipStreamWaitEvent(h->tail, h->ev_fork[l], 0));
+      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, e, h->tail,
+                     nullptr, PROBE_DW + l));
+      used_tail = true;
     }
     if (l > 0) {
       const AeLayer& p = h->L[l - 1];
@@ -805,30 +872,22 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       // (bwd-data of l); the rest of the chain keeps overlapping it.
       if (rec && (l == 0 || !(h->L[l - 1].bn) || (h->vib && l == h->n_enc)))
         MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
-      const BiasSrc bs = bias_src(h, w, l, from_mse);
-      dwe.ad_p = h->params + a.w_off;
-      dwe.ad_m = h->m + a.w_off;
-      dwe.ad_v = h->v + a.w_off;
-      dwe.ad_shadow = adam_shadow(h, a);
-      dwe.ad_b1 = adam->b1;
-      dwe.ad_b2 = adam->b2;
-      dwe.ad_eps = adam->eps;
-      dwe.ad_step = adam->step_size;
-      dwe.ad_bc2 = adam->bc2_sqrt;
-      dwe.dyn = w.dyn;
-      dwe.sm_p = h->params + a.b_off;
-      dwe.sm_g = h->grads + a.b_off;
-      dwe.sm_m = h->m + a.b_off;
-      dwe.sm_v = h->v + a.b_off;
-      dwe.sm_n = a.bn ? 3 * a.Np : a.Np;
-      dwe.gb_src = bs.src;
-      dwe.gb_parts = bs.nparts;
-      dwe.gb_stride = bs.stride;
-      dwe.sm_bN = a.N;
-      dwe.sm_bNp = a.Np;
-      // the gradient is consumed by the fused Adam in registers; materialise
-      // it only when asked (h->keep_grads)
-      dwe.dw_nostore = h->keep_grads ? 0 : 1;
+      if (split) {
+        if (l > 0) {
+          // W_l has been read by bwd-data(l): its Adam on the tail stream
+          MMAD_HIP_CHECK(hipStreamWaitEvent(h->tail, h->ev_data[l], 0));
+          RET_IF(weight_adam(l, h->tail));
+        } else {
+          GemmEpi e = dwe;
+          fill_adam(e, l, false);
+          e.tile_force = mmad_tile_adam_main_override() + 1;
+          RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, e, st,
+                         nullptr, PROBE_DW + l));
+          RET_IF(weight_adam(l, st));
+        }
+        continue;
+      }
+      fill_adam(dwe, l, true);
       // the last dW GEMMs of the chain go to the main stream, which is idle
       // by then, instead of queueing behind the side stream's backlog
       const bool on_main = l < h->dw_main;

@@ -419,7 +419,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   // db[n] (bias gradient of this layer's output n) is needed by the dW fix-up
   // (BN producer) and by the fused bias Adam (column-tile-0 blocks)
   const bool need_db = EPI == GEMM_EPI_BWD_WEIGHT && ep.gb_src &&
-                       (ep.b_scale || (ep.ad_p && ep.sm_p && tn == 0));
+                       (ep.b_scale || (ep.sm_p && tn == 0));
   if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
     if (ep.b_scale) {
 #pragma unroll
@@ -437,6 +437,29 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
           const int pp = min(q, ep.gb_parts - 1);
           e_g[q] = ep.gb_src[(size_t)pp * ep.gb_stride + m0 + tid];
         }
+      }
+    }
+  }
+
+  // fused Adam (dW epilogue): this tile's p / m / v loaded now, before the
+  // operand ring, so their HBM latency and bandwidth overlap the main loop
+  // instead of following it (256-thread tiles of <= 8 chunks per thread: 48 /
+  // 96 VGPRs; the 512-thread tiles would spill at their 256-VGPR budget;
+  // not with split-K, where only the last slice to arrive runs the epilogue)
+  constexpr int CPR_E = BN * (int)sizeof(TO) / 16;
+  constexpr int ITERS_E = BM * CPR_E / NT;
+  constexpr bool APF = EPI == GEMM_EPI_BWD_WEIGHT && ITERS_E <= 8 && NT == 256;
+  floatx4 apP[APF ? ITERS_E : 1], apM[APF ? ITERS_E : 1], apV[APF ? ITERS_E : 1];
+  const bool apf = APF && ep.ad_p != nullptr && S == 1 && !(ep.dbg & 8);
+  if constexpr (APF) {
+    if (apf) {
+#pragma unroll
+      for (int u = 0; u < ITERS_E; ++u) {
+        const int idx = u * NT + tid;
+        const size_t off = (size_t)(m0 + idx / CPR_E) * ep.ldo + n0 + (idx % CPR_E) * 4;
+        apP[u] = *(const floatx4*)(ep.ad_p + off);
+        apM[u] = *(const floatx4*)(ep.ad_m + off);
+        apV[u] = *(const floatx4*)(ep.ad_v + off);
       }
     }
   }
@@ -584,8 +607,8 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
     } else {
       // ((p0 + p1) + p2) + ... in split order, G slabs per round trip (slot
       // sk was never written: loaded anyway, then replaced by acc).  G = 2
-      // for the 8-wave / 64x64-wave-tile configurations (register budget).
-      constexpr int G = TM * TN <= 8 ? 4 : 2;
+      // / 1 for the larger wave tiles (register budget: no spills).
+      constexpr int G = TM * TN <= 4 ? 4 : (TM * TN <= 8 ? 2 : 1);
       floatx4 r[TM][TN];
       for (int t0 = 0; t0 < S; t0 += G) {
         floatx4 lb[G][TM][TN];
@@ -816,9 +839,20 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         const int idx = (i0 + u) * NT + tid;
         const int rl = idx / CPR, ch = idx % CPR;
         off[u] = (size_t)(m0 + rl) * ep.ldo + n0 + ch * OEPC;
-        P[u] = *(const floatx4*)(ep.ad_p + off[u]);
-        Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
-        Vv[u] = *(const floatx4*)(ep.ad_v + off[u]);
+        bool have = false;
+        if constexpr (APF) {
+          if (apf) {
+            P[u] = apP[i0 + u];
+            Mm[u] = apM[i0 + u];
+            Vv[u] = apV[i0 + u];
+            have = true;
+          }
+        }
+        if (!have) {
+          P[u] = *(const floatx4*)(ep.ad_p + off[u]);
+          Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
+          Vv[u] = *(const floatx4*)(ep.ad_v + off[u]);
+        }
       }
 #pragma unroll
       for (int u = 0; u < AG; ++u) {
@@ -1001,7 +1035,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
     }
   }
   if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
-    if (ep.ad_p && ep.sm_p) {
+    if (ep.sm_p) {   // with or without the weight tile's own Adam (ad_p)
       // the layer's small segment [bias | gamma | beta].  Bias: the
       // column-tile-0 blocks, one output row per thread, g = db (computed
       // above from the same partials the flat path reduces, same order).
@@ -1045,7 +1079,10 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
       const TO* an = (const TO*)ep.bn_a;
       double* scr = (double*)(smem + BM * OSTRIDE);    // [PIECES][BN]
       double ps1[PPT], ps2[PPT];
-      float areg[PPT][16];
+      // fused BN: this thread's a values kept for the dz pass (up to 32
+      // registers; the 8-wave 256-row / 256-column tiles reload them instead)
+      constexpr bool AREG = PPT <= 2;
+      float areg[AREG ? PPT : 1][16];
 #pragma unroll
       for (int u = 0; u < PPT; ++u) {
         const int pc = grp + u * NG;
@@ -1056,7 +1093,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
             const int rl = pc * 16 + r;
             const double dy = to_f32<TO>(*(const TO*)(smem + rl * OSTRIDE + cc * (int)sizeof(TO)));
             const float avf = to_f32<TO>(an[(size_t)(m0 + rl) * ep.ldo + col]);
-            areg[u][r] = avf;   // kept for the fused dz below
+            if constexpr (AREG) areg[u][r] = avf;   // kept for the fused dz below
             const double av = avf;
             s1 += dy;
             s2 += dy * ((av - mu) * rs);
@@ -1139,8 +1176,9 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         const double t1 = s_t1[cc], t2 = s_t2[cc];
         const double cf = col < ep.N ? (double)ep.bn_gamma[col] * rs / (double)ep.M : 0.0;
         const double Md = (double)ep.M;
-        double pz[PPT];
-#pragma unroll
+        // (the piece sums go straight to the fp64 piece scratch: its group-sum
+        // use above is finished)
+#pragma unroll AREG ? PPT : 1
         for (int u = 0; u < PPT; ++u) {
           const int pc = grp + u * NG;
           double sz = 0.0;
@@ -1150,7 +1188,9 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
               const int rl = pc * 16 + r;
               TO* slot = (TO*)(smem + rl * OSTRIDE + cc * (int)sizeof(TO));
               const double dy = to_f32<TO>(*slot);
-              const float av = areg[u][r];
+              float av;
+              if constexpr (AREG) av = areg[u][r];
+              else av = to_f32<TO>(an[(size_t)(m0 + rl) * ep.ldo + col]);
               const double xh = ((double)av - mu) * rs;
               const double da = cf * (Md * dy - t1 - xh * t2);
               float d = (float)(da * (double)act_grad_from_out(av, ep.bn_act, ep.slope));
@@ -1159,15 +1199,8 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
               *slot = dt;
               sz += (double)to_f32<TO>(dt);
             }
+            scr[pc * BN + cc] = sz;
           }
-          pz[u] = sz;
-        }
-        // per-64-row column sums of dz (the producer's bias gradient), the
-        // same piece order as bn_part
-#pragma unroll
-        for (int u = 0; u < PPT; ++u) {
-          const int pc = grp + u * NG;
-          if (pc < PIECES) scr[pc * BN + cc] = pz[u];
         }
         __syncthreads();
         for (int c4 = grp; c4 < BM / 64; c4 += NG) {

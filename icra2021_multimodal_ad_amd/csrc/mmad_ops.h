@@ -44,6 +44,10 @@ struct MmadAdamSeg {
   float* p; float* g; float* m; float* v; void* shadow; int64_t n;
   const float* bsrc; int bparts, bstride, bN, bNp;
 };
+// mmad_adam with the step terms read from `dyn` when non-null (graph capture)
+int mmad_adam_dyn(int64_t n, float* p, const float* g, float* m, float* v, float beta1, float beta2,
+                  float eps, float step_size, float bc2_sqrt, void* shadow, int64_t n_shadow,
+                  const MmadDyn* dyn, void* stream);
 int mmad_adam2(const MmadAdamSeg& s0, const MmadAdamSeg& s1, float beta1, float beta2, float eps,
                float step_size, float bc2_sqrt, void* stream);
 

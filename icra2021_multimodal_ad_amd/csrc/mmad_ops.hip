@@ -615,9 +615,13 @@ __global__ __launch_bounds__(256) void adam_k(int64_t n, float* __restrict__ p,
                                               const float* __restrict__ g, float* __restrict__ m,
                                               float* __restrict__ v, float b1, float b2, float eps,
                                               float step_size, float bc2_sqrt, bf16* shadow,
-                                              int64_t n_shadow) {
+                                              int64_t n_shadow, const MmadDyn* dyn) {
   const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i4 >= n) return;
+  if (dyn) {   // graph-captured step: this step's bias-correction terms
+    step_size = dyn->ad_step;
+    bc2_sqrt = dyn->ad_bc2;
+  }
   if (i4 + 4 <= n) {
     floatx4 pp = *(floatx4*)(p + i4), gg = *(const floatx4*)(g + i4);
     floatx4 mm = *(floatx4*)(m + i4), vv = *(floatx4*)(v + i4);
@@ -1046,7 +1050,20 @@ int mmad_adam(int64_t n, float* p, const float* g, float* m, float* v, float bet
   MMAD_CHECK_ARG(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
                  "adam: buffers must be 16-byte aligned");
   adam_k<<<nblk((n + 3) / 4, 256), 256, 0, (hipStream_t)stream>>>(
-      n, p, g, m, v, beta1, beta2, eps, step_size, bc2_sqrt, (bf16*)shadow, n_shadow);
+      n, p, g, m, v, beta1, beta2, eps, step_size, bc2_sqrt, (bf16*)shadow, n_shadow, nullptr);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_adam_dyn(int64_t n, float* p, const float* g, float* m, float* v, float beta1, float beta2,
+                  float eps, float step_size, float bc2_sqrt, void* shadow, int64_t n_shadow,
+                  const MmadDyn* dyn, void* stream) {
+  MMAD_CHECK_ARG(n >= 0 && n_shadow >= 0 && n_shadow <= n, "adam: bad sizes");
+  if (n == 0) return MMAD_OK;
+  MMAD_CHECK_ARG(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
+                 "adam: buffers must be 16-byte aligned");
+  adam_k<<<nblk((n + 3) / 4, 256), 256, 0, (hipStream_t)stream>>>(
+      n, p, g, m, v, beta1, beta2, eps, step_size, bc2_sqrt, (bf16*)shadow, n_shadow, dyn);
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
 }
