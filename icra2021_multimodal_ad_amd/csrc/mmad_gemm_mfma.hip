@@ -441,29 +441,6 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
     }
   }
 
-  // fused Adam (dW epilogue): this tile's p / m / v loaded now, before the
-  // operand ring, so their HBM latency and bandwidth overlap the main loop
-  // instead of following it (256-thread tiles of <= 8 chunks per thread: 48 /
-  // 96 VGPRs; the 512-thread tiles would spill at their 256-VGPR budget;
-  // not with split-K, where only the last slice to arrive runs the epilogue)
-  constexpr int CPR_E = BN * (int)sizeof(TO) / 16;
-  constexpr int ITERS_E = BM * CPR_E / NT;
-  constexpr bool APF = EPI == GEMM_EPI_BWD_WEIGHT && ITERS_E <= 8 && NT == 256;
-  floatx4 apP[APF ? ITERS_E : 1], apM[APF ? ITERS_E : 1], apV[APF ? ITERS_E : 1];
-  const bool apf = APF && ep.ad_p != nullptr && S == 1 && !(ep.dbg & 8);
-  if constexpr (APF) {
-    if (apf) {
-#pragma unroll
-      for (int u = 0; u < ITERS_E; ++u) {
-        const int idx = u * NT + tid;
-        const size_t off = (size_t)(m0 + idx / CPR_E) * ep.ldo + n0 + (idx % CPR_E) * 4;
-        apP[u] = *(const floatx4*)(ep.ad_p + off);
-        apM[u] = *(const floatx4*)(ep.ad_m + off);
-        apV[u] = *(const floatx4*)(ep.ad_v + off);
-      }
-    }
-  }
-
   auto issue = [&](int s) {
     char* base = smem + (s % NS) * SLOT;
     const int k0 = kbase + s * IA::BK;
@@ -839,20 +816,9 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         const int idx = (i0 + u) * NT + tid;
         const int rl = idx / CPR, ch = idx % CPR;
         off[u] = (size_t)(m0 + rl) * ep.ldo + n0 + ch * OEPC;
-        bool have = false;
-        if constexpr (APF) {
-          if (apf) {
-            P[u] = apP[i0 + u];
-            Mm[u] = apM[i0 + u];
-            Vv[u] = apV[i0 + u];
-            have = true;
-          }
-        }
-        if (!have) {
-          P[u] = *(const floatx4*)(ep.ad_p + off[u]);
-          Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
-          Vv[u] = *(const floatx4*)(ep.ad_v + off[u]);
-        }
+        P[u] = *(const floatx4*)(ep.ad_p + off[u]);
+        Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
+        Vv[u] = *(const floatx4*)(ep.ad_v + off[u]);
       }
 #pragma unroll
       for (int u = 0; u < AG; ++u) {
