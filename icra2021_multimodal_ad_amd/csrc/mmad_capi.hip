@@ -59,6 +59,10 @@ static int env_int(const char* name, int dflt) {
 static int g_splitk_dw = env_int("MMAD_GEMM_SPLITK_DW", 0);
 static int g_splitk_dw_blocks = env_int("MMAD_SPLITK_DW_BLOCKS", 512);
 static int g_splitk_dw_min_stages = env_int("MMAD_SPLITK_DW_MIN_STAGES", 8);
+static int g_dw_ws = env_int("MMAD_DW_WS", 0);
+static int g_dw_ws_blocks = env_int("MMAD_DW_WS_BLOCKS", 256);
+int mmad_dw_ws_enabled() { return g_dw_ws; }
+int mmad_dw_ws_blocks() { return g_dw_ws_blocks; }
 int mmad_splitk_dw_override() { return g_splitk_dw; }
 int mmad_splitk_dw_blocks() { return g_splitk_dw_blocks; }
 int mmad_splitk_dw_min_stages() { return g_splitk_dw_min_stages; }
@@ -107,6 +111,8 @@ int mmad_tune_set(int knob, int value) {
     case 9: g_splitk_dw = value; return MMAD_OK;
     case 10: g_splitk_dw_blocks = value; return MMAD_OK;
     case 11: g_splitk_dw_min_stages = value; return MMAD_OK;
+    case 12: g_dw_ws = value; return MMAD_OK;
+    case 13: g_dw_ws_blocks = value; return MMAD_OK;
     default: mmad_set_error("tune_set: unknown knob %d", knob); return MMAD_EINVAL;
   }
 }

@@ -85,9 +85,10 @@ struct GemmEpi {
   // Train-mode BatchNorm fused into the producing GEMM (bn_sync != null):
   // the tiles_m blocks of one output column tile publish their column
   // partials (sc1 stores), meet at a counter barrier (bn_sync[tn] arrivals,
-  // bn_sync[MMAD_BN_EXIT + tn] exits; zero before the launch, left zero) and
-  // each finishes the whole-batch statistics for its columns itself.  Needs
-  // every block of the grid co-resident (mmad_gemm_coresident) and S = 1.
+  // reset by the last arriver, which bumps the generation word
+  // bn_sync[MMAD_BN_EXIT + tn] the others poll; zero before the first launch)
+  // and each finishes the whole-batch statistics for its columns itself.
+  // Needs every block of the grid co-resident (mmad_gemm_bn_fusable), S = 1.
   //  FWD: part = Welford partials; writes out = a (pre-BN activation) and
   //       bn_y = BN(a) = a*scale + shift; the tm == 0 blocks write
   //       bn_save_mean/rstd and update the running statistics (nullable).
@@ -122,6 +123,8 @@ int mmad_splitk_override();   // 0 = shape rule; 1, 2, 4, 8, 16 = forced split f
 int mmad_splitk_dw_override();     // the same for the dW GEMMs only (knob 9)
 int mmad_splitk_dw_blocks();       // dW split rule: target 64x64-tile blocks (knob 10)
 int mmad_splitk_dw_min_stages();   // dW split rule: minimum K stages per slice (knob 11)
+int mmad_dw_ws_enabled();          // Adam-fused dW GEMMs on the warp-specialised kernel (knob 12)
+int mmad_dw_ws_blocks();           // its persistent grid cap (knob 13)
 int mmad_tile_adam_override();  // >= 0: tile of the Adam-fused dW GEMMs
 int mmad_tile_adam_main_override();  // >= 0: ... of those on the main stream
 int mmad_tile_epi_override(int epi);  // >= 0: tile of this epilogue's GEMMs
@@ -144,7 +147,7 @@ void mmad_gemm_splitk_bytes(int Mp, int Np, size_t* slab_bytes, size_t* ctl_byte
 // `s`: MMAD_OK, or MMAD_EHIP with the error string set
 int mmad_gemm_read_status(unsigned* ctl, hipStream_t s, const char* who);
 
-// offset of the exit counters inside a fused-BN barrier block; words per block
+// offset of the generation words inside a fused-BN barrier block; words per block
 #define MMAD_BN_EXIT 64
 #define MMAD_BN_SYNC_WORDS 128
 // can a GEMM with the fused train-mode BN epilogue (bn_sync) run this shape:

@@ -59,6 +59,8 @@ template <> struct Cfg<2> { static constexpr int BM = 128, BN = 256, WM = 2, WN 
 template <> struct Cfg<3> { static constexpr int BM = 64, BN = 64, WM = 2, WN = 2, NS = 4, NT = 256; };
 template <> struct Cfg<4> { static constexpr int BM = 64, BN = 128, WM = 2, WN = 2, NS = 5, NT = 256; };
 template <> struct Cfg<5> { static constexpr int BM = 128, BN = 128, WM = 2, WN = 2, NS = 4, NT = 256; };
+// the MMA half of the warp-specialised dW + Adam kernel (mmad_dw_adam_ws_kernel)
+template <> struct Cfg<6> { static constexpr int BM = 64, BN = 64, WM = 2, WN = 2, NS = 7, NT = 256; };
 constexpr int NCFG = 6;
 constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128};
 constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128};
@@ -1190,6 +1192,289 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
 }
 
 // -------------------------------------------------------------------------
+// dW GEMM + fused Adam, warp-specialised and persistent (bf16 operands).
+//
+// The Adam-fused dW GEMM of mmad_gemm_kernel runs its K loop and then streams
+// the tile's Adam state (26 B per parameter) in the same waves, so HBM idles
+// during the loop and the MFMAs idle during the stream (in-situ 39 us for
+// 1658x2048 at B=1024: 26 % MFMA-busy, half the achievable HBM rate,
+// profiles/r02p_pmc_dw.json).  Here a 512-thread workgroup holds 4 MMA waves
+// (a 64x64 dW tile, 32x32 per wave, a 7-stage LDS-DMA ring, the same K order
+// as mmad_gemm_kernel: bit-identical results; a 128x64 tile spills with the
+// Adam state in registers) and 4 Adam waves, and walks tiles
+// vt = blockIdx.x + j * gridDim.x:
+//   * during tile j's K loop the Adam waves load tile j's p / m / v into
+//     registers (their own vmcnt: the MMA waves' counted waits never see
+//     these loads) and update tile j-1 from the fp32 dW tile the MMA waves left
+//     in LDS, one 4-wide chunk per loop barrier;
+//   * after the loop the MMA waves apply the BN-producer fix-up and stage
+//     dW in LDS; the last tile's update drains after the walk.
+// Both roles run the same barrier sequence (every s_barrier counts all 8
+// waves).  Measured (tuning knob 12, off by default): 56.6 us vs 38.0 us for
+// the plain kernel at 1658x2048, B=1024, cold Adam state (81 us with a
+// 128-workgroup grid; profiles/r02t_*): one 130 KB workgroup per CU keeps a
+// single tile's K loop in flight where the plain kernel runs two 64 KB
+// workgroups per CU, and the K loop is the latency-bound part.  The layer's small segment [bias | gamma | beta] is updated by the
+// Adam waves as in mmad_gemm_kernel (tile-indexed, every element once).
+template <int CFG>
+__global__ __launch_bounds__(2 * Cfg<CFG>::NT, 1) void mmad_dw_adam_ws_kernel(
+    const bf16* __restrict__ A, int lda, const bf16* __restrict__ B, int ldb, int K, GemmEpi ep,
+    int ntiles) {
+  using C = Cfg<CFG>;
+  constexpr int BM = C::BM, BN = C::BN, WM = C::WM, WN = C::WN, NS = C::NS, NT = C::NT;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  using IA = Img<bf16, false, BM, NT>;
+  using IB = Img<bf16, false, BN, NT>;
+  constexpr int SLOT = IA::BYTES + IB::BYTES;
+  constexpr int NL = IA::CHUNKS + IB::CHUNKS;
+  constexpr int OSTRIDE = BN * 4 + 16;                 // fp32 dW staging row
+  constexpr int HBYTES = BM * OSTRIDE;
+  constexpr int CPR = BN * 4 / 16;                     // 16-B chunks per dW row
+  constexpr int ITA = BM * CPR / NT;                   // Adam chunks per Adam thread
+  constexpr int QG = 32;
+  constexpr int LDS_BYTES = NS * SLOT + HBYTES + 2 * BM * 4;
+  static_assert((NS - 1) * NL <= 63, "vmcnt range");
+  static_assert(LDS_BYTES <= 163840, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+  char* H = smem + NS * SLOT;                          // fp32 dW tile of the previous tile
+  float* dbl = (float*)(H + HBYTES);                   // [2][BM] db of the rows of tile j & 1
+
+  const int tid = threadIdx.x;
+  const bool mma = tid < NT;
+  const int t2 = mma ? tid : tid - NT;                 // index within the role
+  const int lane = tid & 63, w = t2 >> 6;
+  const int wm = w / WN, wn = w % WN;
+  const int g = lane >> 4, c = lane & 15;
+  const int grid = gridDim.x, bid = blockIdx.x;
+  const int my_tiles = bid < ntiles ? (ntiles - bid + grid - 1) / grid : 0;
+  const int nt = K / IA::BK;
+
+  float ad_step = ep.ad_step, ad_bc2 = ep.ad_bc2;
+  if (ep.dyn) {
+    ad_step = ep.dyn->ad_step;
+    ad_bc2 = ep.dyn->ad_bc2;
+  }
+  // logical tile -> (m0, n0): the XCD-aware grouped order of mmad_gemm_kernel
+  // (grid is a multiple of 8, so every tile of this block maps to its XCD)
+  auto coords = [&](int vt, int& m0, int& n0, int& tnn) {
+    const int q = ntiles >> 3, r = ntiles & 7, xcd = vt & 7;
+    const int lt = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (vt >> 3);
+    const int tiles_m = ntiles / ep.tiles_n;
+    const int per_group = ep.group_m * ep.tiles_n;
+    const int first_m = (lt / per_group) * ep.group_m;
+    const int gsz = min(tiles_m - first_m, ep.group_m);
+    const int tmm = first_m + (lt % per_group) % gsz;
+    tnn = (lt % per_group) / gsz;
+    m0 = tmm * BM;
+    n0 = tnn * BN;
+    return lt;
+  };
+
+  // the small segment of tile (lt, rows m0p.., column tile tnp): bias rows
+  // (tn == 0 tiles, g = db of those rows) and gamma | beta spread over tiles
+  auto small_segment = [&](int ltp, int m0p, int tnp, const float* dbrow) {
+    if (!ep.sm_p) return;
+    if (tnp == 0 && t2 < BM && m0p + t2 < ep.sm_bNp) {
+      const int n = m0p + t2;
+      float gg = ep.gb_src ? (n < ep.sm_bN ? dbrow[t2] : 0.f) : ep.sm_g[n];
+      if (ep.gb_src) ep.sm_g[n] = gg;
+      float pp = ep.sm_p[n], mm = ep.sm_m[n], vv = ep.sm_v[n];
+      adam_elem(pp, mm, vv, gg, ep.ad_b1, ep.ad_b2, ep.ad_eps, ad_step, ad_bc2);
+      ep.sm_p[n] = pp;
+      ep.sm_m[n] = mm;
+      ep.sm_v[n] = vv;
+    }
+    for (int q = ltp * NT + t2; ep.sm_bNp + q * 4 < ep.sm_n; q += ntiles * NT) {
+      const int i4 = ep.sm_bNp + q * 4;
+      const floatx4 gg = *(const floatx4*)(ep.sm_g + i4);
+      floatx4 pp = *(floatx4*)(ep.sm_p + i4), mm = *(floatx4*)(ep.sm_m + i4);
+      floatx4 vv = *(floatx4*)(ep.sm_v + i4);
+      adam4(pp, mm, vv, gg, ep.ad_b1, ep.ad_b2, ep.ad_eps, ad_step, ad_bc2);
+      *(floatx4*)(ep.sm_p + i4) = pp;
+      *(floatx4*)(ep.sm_m + i4) = mm;
+      *(floatx4*)(ep.sm_v + i4) = vv;
+    }
+  };
+
+  // The two roles run separate loops (disjoint register lifetimes: the MMA
+  // accumulators / fragments and the Adam state are never live together)
+  // with the same barrier sequence per tile j: B0, nt - 1 loop barriers (only
+  // for a real tile), B_end.  j = my_tiles is the Adam waves' drain.
+  if (mma) {
+    using FR = typename SubFrag<bf16>::F;
+    const int ra = wm * 16 * TM, rb = wn * 16 * TN;
+    for (int j = 0; j <= my_tiles; ++j) {
+      const bool has = j < my_tiles;
+      int m0 = 0, n0 = 0, tn = 0;
+      if (has) (void)coords(bid + j * grid, m0, n0, tn);
+      floatx4 acc[TM][TN];
+      float e_s[TN], e_t[TN];
+      if (has) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int jj = 0; jj < TN; ++jj) acc[i][jj] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (ep.b_scale) {   // epilogue constants first (their latency hides under the loop)
+#pragma unroll
+          for (int jj = 0; jj < TN; ++jj) {
+            const int col = n0 + wn * 16 * TN + jj * 16 + c;
+            e_s[jj] = ep.b_scale[col];
+            e_t[jj] = ep.b_shift[col];
+          }
+        }
+#pragma unroll
+        for (int st = 0; st < NS; ++st)
+          if (st < nt) {
+            char* base = smem + st * SLOT;
+            issue_stage<bf16, false, BM, NT>(base, A, lda, m0, st * IA::BK, t2);
+            issue_stage<bf16, false, BN, NT>(base + IA::BYTES, B, ldb, n0, st * IA::BK, t2);
+          }
+        if (nt >= NS) wait_vmcnt<(NS - 1) * NL>();
+        else wait_vmcnt<0>();
+      }
+      block_barrier();                                 // B0: stage 0 visible
+      if (has) {
+        FR f0a[TM], f0b[TN], f1a[TM], f1b[TN];
+        read_sub<bf16, false, false, true, BM, BN, TM, TN>(smem, smem + IA::BYTES, ra, rb, 0, lane, f0a, f0b);
+        wait_lgkm0();
+        auto issue = [&](int st) {
+          char* base = smem + (st % NS) * SLOT;
+          issue_stage<bf16, false, BM, NT>(base, A, lda, m0, st * IA::BK, t2);
+          issue_stage<bf16, false, BN, NT>(base + IA::BYTES, B, ldb, n0, st * IA::BK, t2);
+        };
+        auto step = [&](int t, auto issue_c, auto last_c) {
+          constexpr bool ISSUE = decltype(issue_c)::value, LAST = decltype(last_c)::value;
+          const char* sa = smem + (t % NS) * SLOT;
+          mma_half<bf16, TM, TN, 0>(acc, f0a, f0b);
+          __builtin_amdgcn_sched_barrier(0);
+          read_sub<bf16, false, false, true, BM, BN, TM, TN>(sa, sa + IA::BYTES, ra, rb, 1, lane, f1a, f1b);
+          __builtin_amdgcn_sched_barrier(0);
+          mma_half<bf16, TM, TN, 1>(acc, f0a, f0b);
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (!LAST) {
+            if constexpr (ISSUE) wait_vmcnt<(NS - 2) * NL>();
+            else wait_tail<NL>(nt - t - 2);
+            wait_lgkm0();
+            block_barrier();
+            if constexpr (ISSUE) issue(t + NS);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          mma_half<bf16, TM, TN, 0>(acc, f1a, f1b);
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (!LAST) {
+            const char* sn = smem + ((t + 1) % NS) * SLOT;
+            read_sub<bf16, false, false, true, BM, BN, TM, TN>(sn, sn + IA::BYTES, ra, rb, 0, lane, f0a, f0b);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          mma_half<bf16, TM, TN, 1>(acc, f1a, f1b);
+          __builtin_amdgcn_sched_barrier(0);
+        };
+        using T_ = std::true_type;
+        using F_ = std::false_type;
+        int t = 0;
+        for (; t < nt - NS; ++t) step(t, T_{}, F_{});
+        for (; t < nt - 1; ++t) step(t, F_{}, F_{});
+        step(nt - 1, F_{}, T_{});
+        // BN-producer fix-up, then the fp32 dW tile into H (the previous
+        // tile's update finished reading H before the last loop barrier)
+        if (ep.b_scale) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float db = dbl[(j & 1) * BM + wm * 16 * TM + i * 16 + 4 * g + r];
+#pragma unroll
+              for (int jj = 0; jj < TN; ++jj) acc[i][jj][r] = fmaf(e_s[jj], acc[i][jj][r], e_t[jj] * db);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int jj = 0; jj < TN; ++jj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int rl = wm * 16 * TM + i * 16 + 4 * g + r;
+              const int cl = wn * 16 * TN + jj * 16 + c;
+              *(float*)(H + rl * OSTRIDE + cl * 4) = acc[i][jj][r];
+            }
+      }
+      block_barrier();                                 // B_end: H holds tile j; ring free
+    }
+  } else {
+    // Adam role (the same barrier count as the MMA role: B0, nt - 1, B_end):
+    //  bi = 0..ITA-1: chunk bi of the previous tile's update (its state loads
+    //    were issued a whole loop ago), the small segment after the last;
+    //  bi = 1: db of this tile's rows -> dbl (the MMA epilogue reads it
+    //    after the last loop barrier); bi = ITA: this tile's state loads.
+    // The dispatcher guarantees nt - 1 >= ITA (every H read precedes the
+    // last loop barrier, after which the MMA waves overwrite H).
+    floatx4 aP[ITA], aM[ITA], aV[ITA];
+    int prev_m0 = 0, prev_n0 = 0, prev_tn = 0, prev_lt = 0;
+    for (int j = 0; j <= my_tiles; ++j) {
+      const bool has = j < my_tiles;
+      int m0 = 0, n0 = 0, tn = 0, lt = 0;
+      if (has) lt = coords(bid + j * grid, m0, n0, tn);
+      block_barrier();                                 // B0
+      const int nb = has ? nt - 1 : 0;
+      for (int bi = 0; bi <= nb; ++bi) {
+        if (j > 0) {
+          if (bi == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int u = 0; u < ITA; ++u) {
+            if (has && u != bi) continue;
+            const int idx = u * NT + t2;
+            const int rl = idx / CPR, ch = idx % CPR;
+            const size_t off = (size_t)(prev_m0 + rl) * ep.ldo + prev_n0 + ch * 4;
+            const uint4v v = *(const uint4v*)(H + rl * OSTRIDE + ch * 16);
+            if (!ep.dw_nostore) *(uint4v*)((float*)ep.out + off) = v;
+            adam4(aP[u], aM[u], aV[u], __builtin_bit_cast(floatx4, v), ep.ad_b1, ep.ad_b2, ep.ad_eps,
+                  ad_step, ad_bc2);
+            *(floatx4*)(ep.ad_p + off) = aP[u];
+            *(floatx4*)(ep.ad_m + off) = aM[u];
+            *(floatx4*)(ep.ad_v + off) = aV[u];
+            if (ep.ad_shadow) {
+              bf16x4 sh;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) sh[e] = (bf16)aP[u][e];
+              *(bf16x4*)((bf16*)ep.ad_shadow + off) = sh;
+            }
+          }
+          if (!has || bi == ITA - 1) small_segment(prev_lt, prev_m0, prev_tn, dbl + ((j - 1) & 1) * BM);
+        }
+        if (has && bi == 1 && ep.gb_src && t2 < BM) {
+          // sequential partial order (= the flat reduction's), loads in flight together
+          float e_g[QG];
+#pragma unroll
+          for (int q = 0; q < QG; ++q)
+            e_g[q] = ep.gb_src[(size_t)min(q, ep.gb_parts - 1) * ep.gb_stride + m0 + t2];
+          float db = 0.f;
+#pragma unroll
+          for (int q = 0; q < QG; ++q) db += q < ep.gb_parts ? e_g[q] : 0.f;
+          for (int q = QG; q < ep.gb_parts; ++q) db += ep.gb_src[(size_t)q * ep.gb_stride + m0 + t2];
+          dbl[(j & 1) * BM + t2] = db;
+        }
+        if (has && bi == ITA) {
+#pragma unroll
+          for (int u = 0; u < ITA; ++u) {
+            const int idx = u * NT + t2;
+            const size_t off = (size_t)(m0 + idx / CPR) * ep.ldo + n0 + (idx % CPR) * 4;
+            aP[u] = *(const floatx4*)(ep.ad_p + off);
+            aM[u] = *(const floatx4*)(ep.ad_m + off);
+            aV[u] = *(const floatx4*)(ep.ad_v + off);
+          }
+        }
+        if (bi < nb) block_barrier();
+      }
+      block_barrier();                                 // B_end
+      prev_m0 = m0;
+      prev_n0 = n0;
+      prev_tn = tn;
+      prev_lt = lt;
+    }
+  }
+}
+
+// -------------------------------------------------------------------------
 // host-side planning and launch
 // -------------------------------------------------------------------------
 static bool cfg_fits(int cfg, int Mp, int Np, int epi) {
@@ -1476,6 +1761,33 @@ int mmad_gemm_plan(int Mp, int Np, int K, int epi, int dtype) {
   return it != g_tune.end() ? it->second : heuristic_cfg(Mp, Np, epi);
 }
 
+// the warp-specialised dW + Adam kernel for an Adam-fused dW GEMM (bf16, no
+// split): 64x64 tiles, a persistent grid of at most mmad_dw_ws_blocks()
+// workgroups (a multiple of 8), >= 9 K stages (its Adam schedule needs
+// nt - 1 >= 8 loop barriers)
+static bool dw_ws_fits(int dtype, int epi, const GemmEpi& ep, int Mp, int Np, int K) {
+  return mmad_dw_ws_enabled() && epi == GEMM_EPI_BWD_WEIGHT && dtype == MMAD_BF16 && ep.ad_p &&
+         ep.splitk <= 1 && Mp % 128 == 0 && Np % 64 == 0 && K % 64 == 0 && K / 64 >= 9;
+}
+static int launch_dw_ws(const void* A, int lda, const void* B, int ldb, int Mp, int Np, int K,
+                        const GemmEpi& ep_in, hipStream_t s) {
+  constexpr int BM = Cfg<6>::BM, BN = Cfg<6>::BN;
+  GemmEpi ep = ep_in;
+  const int tiles_m = Mp / BM, tiles_n = Np / BN, ntiles = tiles_m * tiles_n;
+  ep.tiles_n = tiles_n;
+  int gm = (int)(sqrt(ntiles / 8.0 * BN / BM) + 0.5);
+  const int env_gm = mmad_group_override();
+  if (env_gm > 0) gm = env_gm;
+  ep.group_m = gm < 1 ? 1 : (gm > tiles_m ? tiles_m : gm);
+  int cap = mmad_dw_ws_blocks();
+  cap = cap < 8 ? 8 : cap / 8 * 8;
+  const int grid = ntiles < cap ? (ntiles + 7) / 8 * 8 : cap;
+  mmad_dw_adam_ws_kernel<6><<<dim3(grid), dim3(2 * Cfg<6>::NT), 0, s>>>(
+      (const bf16*)A, lda, (const bf16*)B, ldb, K, ep, ntiles);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
 int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,
                        int Np, int K, const GemmEpi& ep_in, hipStream_t s, int* cfg_used) {
   MMAD_CHECK_ARG(Mp % 128 == 0 && Np % 128 == 0 && K % 128 == 0,
@@ -1494,6 +1806,10 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   auto allowed = [&](int c) {
     return c >= 0 && c < NCFG && cfg_fits(c, Mp, Np, epi) && (!bnf || coresident(dtype, epi, c, Mp, Np));
   };
+  if (dw_ws_fits(dtype, epi, ep, Mp, Np, K)) {
+    if (cfg_used) *cfg_used = 6;
+    return launch_dw_ws(A, lda, B, ldb, Mp, Np, K, ep, s);
+  }
   const int env = mmad_tile_override();
   const int env_epi = ep.ad_p ? mmad_tile_adam_override() : mmad_tile_epi_override(epi);
   int cfg;

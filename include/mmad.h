@@ -53,7 +53,9 @@ int mmad_pad_granule(void);
  * factor override for GEMMs given split-K workspace (0 = shape rule, 1/2/4/
  * 8/16), knob 9 = the same for the dW GEMMs only, knobs 10 / 11 = the dW
  * split rule's target number of 64x64-tile blocks (512) and minimum K stages
- * per slice (8),
+ * per slice (8), knob 12 = Adam-fused dW GEMMs on the warp-specialised
+ * persistent kernel (1) or the plain tile kernel (0, default: measured
+ * faster), knob 13 = that kernel's grid cap (256 workgroups),
  * knob 5 = tile of the dW GEMMs with the fused Adam epilogue (default 3 =
  * 64x64; -1 = autotuned like the others), knobs 6 / 7 = tile of the bwd-data /
  * forward GEMMs (-1 = autotuned), knob 8 = tile of the Adam-fused dW GEMMs
@@ -61,7 +63,7 @@ int mmad_pad_granule(void);
  * Defaults from MMAD_GEMM_TILE / MMAD_GEMM_GROUP_M / MMAD_GEMM_AUTOTUNE /
  * MMAD_GEMM_SPLITK / MMAD_GEMM_TILE_ADAM / MMAD_GEMM_TILE_BWD_DATA /
  * MMAD_GEMM_TILE_FWD / MMAD_GEMM_TILE_ADAM_MAIN / MMAD_GEMM_SPLITK_DW /
- * MMAD_SPLITK_DW_BLOCKS / MMAD_SPLITK_DW_MIN_STAGES. */
+ * MMAD_SPLITK_DW_BLOCKS / MMAD_SPLITK_DW_MIN_STAGES / MMAD_DW_WS / MMAD_DW_WS_BLOCKS. */
 int mmad_tune_set(int knob, int value);
 /* The split-K factor the dispatcher picks for a padded GEMM shape (Mp x Np
  * output, K deep) with epilogue `epi` (0 fwd, 1 MSE, 2 bwd-data, 3 dW,
