@@ -75,6 +75,13 @@ struct mmad_ae {
   }();
   hipStream_t tail = nullptr;
   hipEvent_t ev_tail = nullptr;
+  // side-stream GEMM launches reserve this much extra LDS per workgroup
+  // (MMAD_SIDE_LDS_PAD bytes): fewer side workgroups per CU, so the main
+  // stream's chain always finds room next to them
+  int side_lds_pad = [] {
+    const char* e = getenv("MMAD_SIDE_LDS_PAD");
+    return e ? atoi(e) : 0;
+  }();
   // fused step, layers < dw_main (the end of the backward chain): the dW
   // GEMM (with the small-segment Adam in its epilogue) and a flat Adam pass
   // over the weights instead of one Adam-fused dW GEMM: layer l >= 1's GEMM
@@ -533,6 +540,7 @@ static int ae_gemm(const mmad_ae* h, const AeWS& w, int dt, int epi, const void*
   const int r = (h->side && s == h->side) ? 1 : 0;
   ep.sk_slab = w.sk_slab[r];
   ep.sk_ctl = w.sk_ctl[r];
+  if (r == 1) ep.lds_pad = h->side_lds_pad;
   if (h->tail && s == h->tail) {   // no split-K workspace of its own: never split
     ep.sk_slab = nullptr;
     ep.sk_ctl = nullptr;

@@ -79,6 +79,8 @@ struct GemmEpi {
   int splitk;
   int tiles_n, group_m;
   int tile_force;        // caller's tile choice + 1 (0 = none; ignored if it does not fit)
+  int lds_pad;           // extra (unused) dynamic LDS per workgroup: caps the
+                         // workgroups of this launch per CU (side-stream dW GEMMs)
   // graph-captured step (nullable): MSE target = dyn->x, Adam step terms
   // from dyn (see MmadDyn)
   const MmadDyn* dyn;

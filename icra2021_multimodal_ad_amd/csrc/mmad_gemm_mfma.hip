@@ -1523,13 +1523,14 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
   if (env_gm > 0) gm = env_gm;
   ep.group_m = gm < 1 ? 1 : (gm > tiles_m ? tiles_m : gm);
   dim3 grd(ntiles * S), blk(CFG_NT[cfg]);
+  const size_t dyn = ep.lds_pad > 0 ? (size_t)ep.lds_pad : 0;
   switch (cfg) {
-    case 0: mmad_gemm_kernel<T, TO, AK, BK_, 0, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
-    case 1: mmad_gemm_kernel<T, TO, AK, BK_, 1, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
-    case 2: mmad_gemm_kernel<T, TO, AK, BK_, 2, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
-    case 3: mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
-    case 4: mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
-    default: mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI><<<grd, blk, 0, s>>>(A, lda, B, ldb, K, ep); break;
+    case 0: mmad_gemm_kernel<T, TO, AK, BK_, 0, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
+    case 1: mmad_gemm_kernel<T, TO, AK, BK_, 1, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
+    case 2: mmad_gemm_kernel<T, TO, AK, BK_, 2, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
+    case 3: mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
+    case 4: mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
+    default: mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
   }
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
