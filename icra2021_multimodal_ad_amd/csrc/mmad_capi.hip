@@ -68,13 +68,21 @@ int mmad_splitk_dw_blocks() { return g_splitk_dw_blocks; }
 int mmad_splitk_dw_min_stages() { return g_splitk_dw_min_stages; }
 // tile for the dW GEMMs with the fused Adam epilogue (the autotuner times
 // them without Adam, which under-weights the epilogue's HBM traffic: it picks
-// 128x128 for the large layers, 208 blocks for 256 CUs).  Default 64x64 (cfg
-// 3): 0.522 vs 0.529 ms/step at D=2048 B=1024 (tools/tile_adam_sweep.py).
+// 128x128 for the large layers, 208 blocks for 256 CUs).  Default (-2) = a
+// shape rule: 128x128 (cfg 0) when the GEMM is deep (K = batch >= 2048) and
+// large (>= 1.5 M parameters), 64x64 (cfg 3) otherwise -- B=1024: 64x64
+// everywhere (0.522 vs 0.529 ms/step, tools/tile_adam_sweep.py); B=4096:
+// 67 vs 87 us at 1658x2048, 63 vs 78 at 1268x1658, 64x64 better below
+// (profiles/r02j_splitk_dw4096_vib.log).
 static int g_tile_adam = [] {
   const char* e = getenv("MMAD_GEMM_TILE_ADAM");
-  return e ? atoi(e) : 3;
+  return e ? atoi(e) : -2;
 }();
 int mmad_tile_adam_override() { return g_tile_adam; }
+int mmad_tile_adam_for(int Mp, int Np, int K) {
+  if (g_tile_adam != -2) return g_tile_adam;
+  return (K >= 2048 && (long)Mp * Np >= 1500000L) ? 0 : 3;
+}
 // tile of the Adam-fused dW GEMMs that run on the main stream at the end of
 // the backward (nothing else on the GPU then; -1 = same as knob 5)
 static int g_tile_adam_main = [] {

@@ -127,7 +127,8 @@ int mmad_splitk_dw_blocks();       // dW split rule: target 64x64-tile blocks (k
 int mmad_splitk_dw_min_stages();   // dW split rule: minimum K stages per slice (knob 11)
 int mmad_dw_ws_enabled();          // Adam-fused dW GEMMs on the warp-specialised kernel (knob 12)
 int mmad_dw_ws_blocks();           // its persistent grid cap (knob 13)
-int mmad_tile_adam_override();  // >= 0: tile of the Adam-fused dW GEMMs
+int mmad_tile_adam_override();  // >= 0: tile of the Adam-fused dW GEMMs (-2: shape rule)
+int mmad_tile_adam_for(int Mp, int Np, int K);   // ... for a shape
 int mmad_tile_adam_main_override();  // >= 0: ... of those on the main stream
 int mmad_tile_epi_override(int epi);  // >= 0: tile of this epilogue's GEMMs
 

@@ -1812,7 +1812,7 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
     return launch_dw_ws(A, lda, B, ldb, Mp, Np, K, ep, s);
   }
   const int env = mmad_tile_override();
-  const int env_epi = ep.ad_p ? mmad_tile_adam_override() : mmad_tile_epi_override(epi);
+  const int env_epi = ep.ad_p ? mmad_tile_adam_for(Mp, Np, K) : mmad_tile_epi_override(epi);
   int cfg;
   const int force = ep.tile_force - 1;
   if (allowed(force)) {

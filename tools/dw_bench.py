@@ -69,7 +69,7 @@ def main():
             continue
         finally:
             lib.mmad_tune_set(0, -1)
-            lib.mmad_tune_set(5, 3)
+            lib.mmad_tune_set(5, -2)
         print(json.dumps({"shape": [M, N, K], "cfg": cfg, "gemm_us": round(t_g, 2),
                           "gemm_tflops": round(flops / t_g / 1e6, 1), "fused_us": round(t_f, 2),
                           "fused_gbs": round(adam_bytes / t_f / 1e3, 1)}), flush=True)

@@ -58,7 +58,7 @@ for li, (K, N) in enumerate(shapes):
                 continue
             rows.append({"tile": tile, "S": S, "us": round(t, 2)})
     lib.mmad_tune_set(9, 0)
-    lib.mmad_tune_set(5, 3)
+    lib.mmad_tune_set(5, -2)
     base = next(r["us"] for r in rows if r.get("tile") == 3 and r.get("S") == 1 and "us" in r)
     best = min((r for r in rows if "us" in r), key=lambda r: r["us"])
     # what the default rule picks (knob 9 = 0) at the default tile
