@@ -46,6 +46,8 @@ SIGNATURES = {
     "mmad_bn_act_bwd": (_I, [_I, _I, _F, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                              _P]),
     "mmad_act_bwd": (_I, [_I, _I, _F, _I, _I, _I, _P, _P, _P, _P, _P]),
+    "mmad_activation_fwd": (_I, [_I, _F, _I, _I, _P, _I64, _P, _I64, _P]),
+    "mmad_activation_bwd": (_I, [_I, _F, _I, _I, _P, _I64, _P, _I64, _P, _I64, _P]),
     "mmad_colsum": (_I, [_I, _I, _I, _P, _I, _F, _P, _P]),
     "mmad_sum": (_I, [_I64, _P, _F, _P, _I, _P]),
     "mmad_pack_input": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _P]),

@@ -1143,3 +1143,118 @@ int mmad_act_bwd(int dtype, int act, float slope, int M, int Mp, int Np, const v
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Standalone Activation (modules/activation.py:20-45), fp32: element-wise
+// forms one thread per 4 values; softmax / logsoftmax one wave per row
+// (max, sum of exp by wave shuffles; rows of any width).
+namespace {
+__device__ __forceinline__ float act_elem(int act, float v, float slope) {
+  switch (act) {
+    case MMAD_ACT_LEAKYRELU: return v > 0.f ? v : v * slope;
+    case MMAD_ACT_RELU: return v > 0.f ? v : 0.f;
+    case MMAD_ACT_SIGMOID: return 1.f / (1.f + expf(-v));
+    case MMAD_ACT_TANH: return tanhf(v);
+    case MMAD_ACT_LOGSIGMOID: return fminf(v, 0.f) - log1pf(expf(-fabsf(v)));
+    default: return v;
+  }
+}
+__device__ __forceinline__ float act_elem_grad(int act, float y, float dy, float slope) {
+  switch (act) {
+    case MMAD_ACT_LEAKYRELU: return y > 0.f ? dy : dy * slope;
+    case MMAD_ACT_RELU: return y > 0.f ? dy : 0.f;
+    case MMAD_ACT_SIGMOID: return dy * y * (1.f - y);
+    case MMAD_ACT_TANH: return dy * (1.f - y * y);
+    case MMAD_ACT_LOGSIGMOID: return dy * (1.f - expf(y));   // d/dx log sigma(x) = 1 - sigma(x)
+    default: return dy;
+  }
+}
+__global__ __launch_bounds__(256) void act_elem_fwd_k(int act, float slope, int M, int N, const float* x,
+                                                      int64_t ldx, float* y, int64_t ldy) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r = i / N, c = i % N;
+  if (r >= M) return;
+  y[r * ldy + c] = act_elem(act, x[r * ldx + c], slope);
+}
+__global__ __launch_bounds__(256) void act_elem_bwd_k(int act, float slope, int M, int N, const float* y,
+                                                      int64_t ldy, const float* dy, int64_t lddy,
+                                                      float* dx, int64_t lddx) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r = i / N, c = i % N;
+  if (r >= M) return;
+  dx[r * lddx + c] = act_elem_grad(act, y[r * ldy + c], dy[r * lddy + c], slope);
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+// one 64-lane wave per row, 4 rows per block
+__global__ __launch_bounds__(256) void act_row_fwd_k(int logsm, int M, int N, const float* x, int64_t ldx,
+                                                     float* y, int64_t ldy) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* xr = x + (int64_t)row * ldx;
+  float mx = -INFINITY;
+  for (int c = lane; c < N; c += 64) mx = fmaxf(mx, xr[c]);
+  mx = wave_max(mx);
+  float s = 0.f;
+  for (int c = lane; c < N; c += 64) s += expf(xr[c] - mx);
+  s = wave_sum(s);
+  const float ls = logf(s);
+  float* yr = y + (int64_t)row * ldy;
+  for (int c = lane; c < N; c += 64) {
+    const float z = xr[c] - mx;
+    yr[c] = logsm ? z - ls : expf(z) / s;
+  }
+}
+__global__ __launch_bounds__(256) void act_row_bwd_k(int logsm, int M, int N, const float* y, int64_t ldy,
+                                                     const float* dy, int64_t lddy, float* dx,
+                                                     int64_t lddx) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* yr = y + (int64_t)row * ldy;
+  const float* gr = dy + (int64_t)row * lddy;
+  float s = 0.f;
+  for (int c = lane; c < N; c += 64) s += logsm ? gr[c] : gr[c] * yr[c];
+  s = wave_sum(s);
+  float* dr = dx + (int64_t)row * lddx;
+  for (int c = lane; c < N; c += 64)
+    dr[c] = logsm ? gr[c] - expf(yr[c]) * s : yr[c] * (gr[c] - s);
+}
+}  // namespace
+
+int mmad_activation_fwd(int act, float slope, int M, int N, const float* x, int64_t ldx, float* y,
+                        int64_t ldy, void* stream) {
+  MMAD_CHECK_ARG(act >= MMAD_ACT_NONE && act <= MMAD_ACT_LOGSOFTMAX, "activation_fwd: bad act %d", act);
+  MMAD_CHECK_ARG(M >= 0 && N >= 0 && ldx >= N && ldy >= N && (M == 0 || N == 0 || (x && y)),
+                 "activation_fwd: bad arguments");
+  if (M == 0 || N == 0) return MMAD_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (act == MMAD_ACT_SOFTMAX || act == MMAD_ACT_LOGSOFTMAX) {
+    act_row_fwd_k<<<(M + 3) / 4, 256, 0, s>>>(act == MMAD_ACT_LOGSOFTMAX, M, N, x, ldx, y, ldy);
+  } else {
+    const int64_t n = (int64_t)M * N;
+    act_elem_fwd_k<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(act, slope, M, N, x, ldx, y, ldy);
+  }
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_activation_bwd(int act, float slope, int M, int N, const float* y, int64_t ldy,
+                        const float* dy, int64_t lddy, float* dx, int64_t lddx, void* stream) {
+  MMAD_CHECK_ARG(act >= MMAD_ACT_NONE && act <= MMAD_ACT_LOGSOFTMAX, "activation_bwd: bad act %d", act);
+  MMAD_CHECK_ARG(M >= 0 && N >= 0 && ldy >= N && lddy >= N && lddx >= N &&
+                     (M == 0 || N == 0 || (y && dy && dx)),
+                 "activation_bwd: bad arguments");
+  if (M == 0 || N == 0) return MMAD_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (act == MMAD_ACT_SOFTMAX || act == MMAD_ACT_LOGSOFTMAX) {
+    act_row_bwd_k<<<(M + 3) / 4, 256, 0, s>>>(act == MMAD_ACT_LOGSOFTMAX, M, N, y, ldy, dy, lddy, dx, lddx);
+  } else {
+    const int64_t n = (int64_t)M * N;
+    act_elem_bwd_k<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(act, slope, M, N, y, ldy, dy, lddy, dx, lddx);
+  }
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}

@@ -25,11 +25,47 @@ ACT_NAMES = ("sigmoid", "logsigmoid", "softmax", "logsoftmax", "tanh", "relu", "
 LEAKY_SLOPE = 0.2  # modules/activation.py:37-38
 
 
+# MMAD_ACT_* (include/mmad.h)
+ACT_ENUM = {None: 0, "leakyrelu": 1, "relu": 2, "sigmoid": 3, "tanh": 4, "logsigmoid": 5,
+            "softmax": 6, "logsoftmax": 7}
+
+
+class _ActivationFn(torch.autograd.Function):
+    """Standalone activation on the device (mmad_activation_fwd / _bwd): the
+    backward works from the saved OUTPUT (every supported form's derivative
+    is a function of it)."""
+
+    @staticmethod
+    def forward(ctx, x, act):
+        _native.require_gpu(x)
+        shape, dtype = x.shape, x.dtype
+        n = shape[-1] if x.dim() > 0 else 1
+        x2 = x.reshape(-1, n).float().contiguous()
+        y = torch.empty_like(x2)
+        call("mmad_activation_fwd", act, LEAKY_SLOPE, x2.shape[0], n, ptr(x2), n, ptr(y), n,
+             stream_ptr())
+        ctx.save_for_backward(y)
+        ctx.act, ctx.dtype = act, dtype
+        return y.view(shape).to(dtype)
+
+    @staticmethod
+    def backward(ctx, gy):
+        (y,) = ctx.saved_tensors
+        g2 = gy.reshape(y.shape).float().contiguous()
+        dx = torch.empty_like(g2)
+        n = y.shape[1]
+        call("mmad_activation_bwd", ctx.act, LEAKY_SLOPE, y.shape[0], n, ptr(y), n, ptr(g2), n,
+             ptr(dx), n, stream_ptr())
+        return dx.view(gy.shape).to(ctx.dtype), None
+
+
 class Activation(nn.Module):
     """modules/activation.py:20-45.  ``name`` selects the nonlinearity; unknown
     names (incl. None) are the identity.  Element-wise activations are fused
-    into the FC kernel epilogue; softmax/logsoftmax/logsigmoid exist for
-    surface parity and run through torch when used standalone."""
+    into the FC kernel epilogue inside an FCLayer; called standalone, every
+    form (softmax / logsoftmax over dim=-1 included) runs the native
+    activation kernels, differentiably.  ``act`` keeps the torch module the
+    reference holds (surface parity: printing, state); it is never called."""
 
     def __init__(self, act):
         super().__init__()
@@ -56,9 +92,9 @@ class Activation(nn.Module):
         return self.name in (None, "leakyrelu", "relu", "sigmoid", "tanh")
 
     def forward(self, x):
-        if self.act is not None:
-            return self.act(x)
-        return x
+        if self.act is None:
+            return x
+        return _ActivationFn.apply(x, ACT_ENUM[self.name])
 
 
 class Loss(nn.Module):

@@ -38,7 +38,7 @@ enum { MMAD_OK = 0, MMAD_EINVAL = -1, MMAD_EUNSUPPORTED = -2, MMAD_EHIP = -3, MM
 enum { MMAD_F32 = 0, MMAD_BF16 = 1 };
 /* modules/activation.py:20-45 (names 'leakyrelu', 'relu', 'sigmoid', 'tanh', None) */
 enum { MMAD_ACT_NONE = 0, MMAD_ACT_LEAKYRELU = 1, MMAD_ACT_RELU = 2, MMAD_ACT_SIGMOID = 3,
-       MMAD_ACT_TANH = 4 };
+       MMAD_ACT_TANH = 4, MMAD_ACT_LOGSIGMOID = 5, MMAD_ACT_SOFTMAX = 6, MMAD_ACT_LOGSOFTMAX = 7 };
 
 const char* mmad_last_error_string(void);
 int mmad_abi_version(void);
@@ -149,6 +149,18 @@ int mmad_fc_bwd_data(int dtype, int M, int N, int K, int Mp, int Np, int Kp, con
 /* dW[Np][Kp] (fp32) = dz[Mp][Np]^T . x[Mp][Kp] (K = batch). */
 int mmad_fc_bwd_weight(int dtype, int Mp, int Np, int Kp, const void* dz, const void* x,
                        float* dw, void* stream);
+
+/* The standalone Activation module (modules/activation.py:20-45) on fp32
+ * [M][ld] rows of N values: act = any MMAD_ACT_* (softmax / logsoftmax over
+ * each row, dim=-1, max-subtracted; logsigmoid = -softplus(-x); leaky slope
+ * `slope`).  mmad_activation_bwd: dx from the forward OUTPUT y and dy
+ * (sigmoid y(1-y), tanh 1-y^2, relu/leaky by the sign of y, logsigmoid
+ * 1-exp(y), softmax y(dy - sum dy y), logsoftmax dy - exp(y) sum dy).
+ * x / y / dy / dx may share ld; y may alias x (in place), dx may alias dy. */
+int mmad_activation_fwd(int act, float slope, int M, int N, const float* x, int64_t ldx, float* y,
+                        int64_t ldy, void* stream);
+int mmad_activation_bwd(int act, float slope, int M, int N, const float* y, int64_t ldy,
+                        const float* dy, int64_t lddy, float* dx, int64_t lddx, void* stream);
 
 /* dW as mmad_fc_bwd_weight with torch.optim.Adam's step (as mmad_adam) fused
  * into the GEMM epilogue (loss.backward() + optimizer.step() for one

@@ -151,3 +151,26 @@ def test_vib_autoencoder_forward_is_differentiable():
     grads = [p.grad for p in m.parameters()]
     assert all(g is not None and torch.isfinite(g).all() for g in grads)
     assert any(float(g.abs().sum()) > 0 for g in grads[:4])
+
+
+@pytest.mark.parametrize("act", ["sigmoid", "logsigmoid", "softmax", "logsoftmax", "tanh", "relu",
+                                 "leakyrelu", None])
+@pytest.mark.parametrize("shape", [(37, 129), (5, 3, 1000), (1, 1)])
+def test_standalone_activation_matches_torch(act, shape):
+    """modules/activation.py:20-45 standalone (softmax / logsoftmax over dim=-1):
+    the native forward and backward against torch's modules, fp32, 1e-6."""
+    from icra2021_multimodal_ad_amd.fc_module import Activation
+    ref = {"sigmoid": torch.nn.Sigmoid(), "logsigmoid": torch.nn.LogSigmoid(),
+           "softmax": torch.nn.Softmax(dim=-1), "logsoftmax": torch.nn.LogSoftmax(dim=-1),
+           "tanh": torch.nn.Tanh(), "relu": torch.nn.ReLU(), "leakyrelu": torch.nn.LeakyReLU(0.2),
+           None: torch.nn.Identity()}[act]
+    g = torch.Generator().manual_seed(hash((act, shape)) & 0xffff)
+    x = (torch.randn(*shape, generator=g) * 4.0).cuda().requires_grad_(True)
+    gy = torch.randn(*shape, generator=g).cuda()
+    y = Activation(act)(x)
+    y.backward(gy)
+    xr = x.detach().clone().requires_grad_(True)
+    yr = ref(xr)
+    yr.backward(gy)
+    assert torch.allclose(y, yr, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(x.grad, xr.grad, rtol=1e-5, atol=1e-6)
