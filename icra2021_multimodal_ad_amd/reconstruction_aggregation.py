@@ -76,14 +76,36 @@ def sap_from_layer_sq(layer_sq, widths, start_layer_index=0, end_layer_index=Non
     return layer_sq[sel].sum(0) / float(sum(widths[sel]))
 
 
+def nap_fit(x, device=None):
+    """Rotater.fit + Standardizer.fit (utils/normalize.py:52-70, :25-34) of the
+    NAP score on train diffs x [N, W] -> {'mu_r', 'v', 'mu_s', 'var'} (device
+    fp32; v is [W, min(N, W)]) through mmad_nap_fit: fp64 Gram of the centred
+    diffs + rocSOLVER eigensolve (V = right singular vectors, descending), fp32
+    rotation with fp64 statistics."""
+    from ._native import call, load, ptr, stream_ptr, require_gpu
+    dev = torch.device(device) if device is not None else x.device
+    x = torch.as_tensor(x).to(dev, torch.float32).contiguous()
+    require_gpu(x)
+    if x.dim() != 2 or x.shape[0] < 2:
+        raise ValueError("NAP fit needs [N >= 2, W] train diffs, got %s" % (tuple(x.shape),))
+    N, W = x.shape
+    R = min(N, W)
+    ws_b = int(load().mmad_nap_fit_ws_bytes(N, W))
+    ws = torch.empty(ws_b, device=dev, dtype=torch.uint8)
+    out = {"mu_r": torch.empty(W, device=dev), "v": torch.empty((W, R), device=dev),
+           "mu_s": torch.empty(R, device=dev), "var": torch.empty(R, device=dev)}
+    call("mmad_nap_fit", N, W, ptr(x), x.stride(0), ptr(out["mu_r"]), ptr(out["v"]),
+         ptr(out["mu_s"]), ptr(out["var"]), ptr(ws), ws_b, stream_ptr())
+    return out
+
+
 class NapScorer:
     """NAP score (utils/metric.py:183-238 get_d_norm_loss with Rotater
     utils/normalize.py:47-103 and Standardizer :20-45).
 
     fit: the rotation (mu_r, V) from the SVD of the centred train diffs and the
-    standardiser (mu_s, ddof=1 variance of the rotated train diffs) -- a
-    one-time host-side fit done with torch.linalg in float64 on the device, as
-    the reference's own Rotater.fit calls torch's SVD.
+    standardiser (mu_s, ddof=1 variance of the rotated train diffs), on the
+    device through mmad_nap_fit (see nap_fit).
     run: ONE native GEMM per batch (mmad_nap_score): the concatenated diffs
     times V^T with the centring/standardising folded into a bias and a
     per-column weight, squared-mean reduced in the epilogue -- the rotated
@@ -133,23 +155,7 @@ class NapScorer:
         ready fit_state {'mu_r','v','mu_s','var'} (e.g. the reference's)."""
         dev = self.device
         if fit_state is None:
-            x = self._cat(train_diffs).to(dev, torch.float64)
-            mu_r = x.mean(0)
-            xc = x - mu_r
-            n, wdt = xc.shape
-            if n > wdt:
-                # V = right singular vectors of xc = eigenvectors of the Gram
-                # xc^T xc, in descending eigenvalue order (one [W x W]
-                # symmetric eigensolve instead of an [N x W] SVD)
-                _, evec = torch.linalg.eigh(xc.T @ xc)
-                v = evec.flip(1)
-            else:
-                _, _, vh = torch.linalg.svd(xc, full_matrices=False)
-                v = vh.T
-            rot = (xc.float() @ v.float()).double()     # Rotater.run is fp32 matmul
-            mu_s = rot.mean(0)
-            var = ((rot - mu_s) ** 2).sum(0) / max(rot.shape[0] - 1, 1)
-            fit_state = {"mu_r": mu_r.float(), "v": v.float(), "mu_s": mu_s.float(), "var": var.float()}
+            fit_state = nap_fit(self._cat(train_diffs), dev)
         fit_state = {k: torch.as_tensor(np.asarray(v) if not torch.is_tensor(v) else v).to(dev)
                      for k, v in fit_state.items()}
         self.fit_state = fit_state

@@ -140,6 +140,20 @@ int mmad_nap_score(int dtype, int M, int K, int R, int Mp, int Kp, int Rp, const
                    const void* vt, const float* bias, const float* w, float* rowsq, float* score,
                    void* stream);
 
+/* NAP fit (Rotater.fit utils/normalize.py:52-70, then Standardizer.fit
+ * :25-34 on the rotated train diffs; utils/metric.py:183-238 fits both on the
+ * train diffs).  x: train diffs, device fp32 [N][ldx] (concatenated layers).
+ * Outputs (device fp32): mu_r [W] = mean(x), v [W][R] (R = min(N, W)) = the
+ * right singular vectors of x - mu_r in descending singular-value order (the
+ * eigenvectors of the fp64 Gram, rocSOLVER dsyevd; column signs are the
+ * solver's, as the reference's are its SVD's -- NAP scores do not depend on
+ * them), mu_s [R] / var [R] = mean and ddof-1 variance of rot = (x - mu_r) v
+ * (fp32 product, fp64 statistics as np.cov).  N >= 2.  Deterministic.
+ * Synchronises `stream` once (eigensolver convergence flag). */
+size_t mmad_nap_fit_ws_bytes(int64_t N, int W);
+int mmad_nap_fit(int64_t N, int W, const float* x, int64_t ldx, float* mu_r, float* v, float* mu_s,
+                 float* var, void* ws, size_t ws_bytes, void* stream);
+
 /* Backward of Linear (autograd of layers/fc_layer.py:38):
  * dx[Mp][Kp] = dz[Mp][Np] . w[Np][Kp]; colsum (nullable, [Mp/32][2][Kp]
  * slot 0) = per-chunk column sums of dx (bias grad of a no-BN producer). */

@@ -518,3 +518,41 @@ def test_graph_step_equals_eager_step(dtype, models, monkeypatch):
     for a, b in zip(res[False][1:], res[True][1:]):
         assert torch.equal(a, b)
     assert res[False][0] == res[True][0]
+
+
+@pytest.mark.parametrize("shape", [(3000, 48), (40, 300), (5000, 700)])
+def test_nap_fit_native_matches_reference_and_oracle(golden, shape):
+    """mmad_nap_fit (Rotater.fit + Standardizer.fit, utils/normalize.py:25-70)
+    against the reference's own fit state on nap.npz (mu_r 1e-6, var rtol 1e-4,
+    each V column parallel to the reference's up to sign: |cos| >= 1 - 1e-5 --
+    the nap.npz spectrum is well separated), and against the float64 oracle
+    (oracle.nap_fit) on seeded data, including N < W (rank-deficient: only the
+    N - 1 informative directions are compared; the rest are an arbitrary
+    orthonormal completion in either implementation).  Repeat runs are
+    bit-identical."""
+    from icra2021_multimodal_ad_amd.reconstruction_aggregation import nap_fit
+    N, W = shape
+    if shape == (3000, 48):
+        g = golden("nap")
+        x = g["train"]
+        ref = {k: g[k] for k in ("mu_r", "v", "mu_s", "var")}
+    else:
+        rng = np.random.default_rng(N + W)
+        x = (rng.standard_normal((N, W)) * np.linspace(3.0, 0.2, W) + 0.5).astype(np.float32)
+        ref = O.nap_fit(x)
+    got = nap_fit(torch.from_numpy(x).cuda())
+    again = nap_fit(torch.from_numpy(x).cuda())
+    for k in got:
+        assert torch.equal(got[k], again[k]), k
+    got = {k: t.cpu().numpy().astype(np.float64) for k, t in got.items()}
+    R = min(N, W)
+    assert got["v"].shape == (W, R)
+    assert np.abs(got["mu_r"] - ref["mu_r"]).max() <= 1e-6 * max(1.0, np.abs(ref["mu_r"]).max())
+    keep = R if N > W else N - 1
+    v, rv = got["v"][:, :keep], np.asarray(ref["v"], np.float64)[:, :keep]
+    cos = np.abs((v * rv).sum(0)) / (np.linalg.norm(v, axis=0) * np.linalg.norm(rv, axis=0))
+    assert cos.min() >= 1 - 1e-5, cos.min()
+    assert np.abs(got["var"][:keep] - ref["var"][:keep]).max() <= 1e-4 * ref["var"][:keep].max()
+    assert np.abs(got["mu_s"][:keep]).max() <= 1e-4 * np.sqrt(ref["var"][:keep].max())
+    vtv = got["v"].T @ got["v"]
+    assert np.abs(vtv - np.eye(R)).max() < 1e-5
