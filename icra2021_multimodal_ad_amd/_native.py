@@ -88,6 +88,8 @@ SIGNATURES = {
     "mmad_allreduce_bucket": (_I, [_P, _P, _I64, _P]),
     "mmad_ae_set_comm": (_I, [_P, _P]),
     "mmad_nap_fit_ws_bytes": (ctypes.c_size_t, [_I64, _I]),
+    "mmad_minmax_norm_ws_bytes": (ctypes.c_size_t, [_I64, _I]),
+    "mmad_minmax_norm": (_I, [_I64, _I, _P, _I, _I, _P, _P, ctypes.c_size_t, _P]),
     "mmad_nap_fit": (_I, [_I64, _I, _P, _I64, _P, _P, _P, _P, _P, ctypes.c_size_t, _P]),
     "mmad_rank_metrics_ws_bytes": (ctypes.c_size_t, [_I64]),
     "mmad_rank_metrics": (_I, [_I64, _P, _P, _P, _P, ctypes.c_size_t, _P]),

@@ -176,3 +176,108 @@ int mmad_hsr_fuse(int n, const float* r, const float* d, const float* t, const f
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
 }
+
+// ---- sensor-stream normalisation (TabularDataset, utils/data_loaders.py) ---
+// norm_vec_np (:447-456): per column (v - min) / (max - min) over the n
+// windows, NaN -> 0 (a constant column); the reference computes it in fp64
+// (its uint8 / uint16 image arrays subtract exactly, the quotient is a
+// float64 division), then casts to fp32 (:367-394).  Images additionally
+// take the reference's view + F.interpolate(size=32) (nearest, 24 -> 32 rows:
+// src row = floor(y * 24 / 32), columns unchanged): out [n][C][32][32] from
+// the HWC-flattened [24][32][C] row reinterpreted as [C][24][32] (:368-378).
+namespace {
+
+constexpr int NORM_ROWS = 1024;    // rows per min/max partial
+
+template <typename V> __device__ __forceinline__ double ldv(const void* v, int64_t i) {
+  return (double)((const V*)v)[i];
+}
+__device__ __forceinline__ double load_any(const void* v, int vtype, int64_t i) {
+  switch (vtype) {
+    case MMAD_SRC_U8: return ldv<uint8_t>(v, i);
+    case MMAD_SRC_U16: return ldv<uint16_t>(v, i);
+    case MMAD_SRC_I32: return ldv<int32_t>(v, i);
+    case MMAD_SRC_F32: return ldv<float>(v, i);
+    default: return ldv<double>(v, i);
+  }
+}
+
+__global__ __launch_bounds__(256) void colminmax_k(int64_t n, int F, const void* __restrict__ v,
+                                                   int vtype, double* __restrict__ part) {
+  const int f = blockIdx.x * 256 + threadIdx.x;
+  if (f >= F) return;
+  const int64_t r0 = (int64_t)blockIdx.y * NORM_ROWS;
+  const int64_t r1 = r0 + NORM_ROWS < n ? r0 + NORM_ROWS : n;
+  double lo = load_any(v, vtype, r0 * F + f), hi = lo;
+  for (int64_t r = r0 + 1; r < r1; ++r) {
+    const double x = load_any(v, vtype, r * F + f);
+    lo = x < lo ? x : lo;
+    hi = x > hi ? x : hi;
+  }
+  part[((int64_t)blockIdx.y * 2 + 0) * F + f] = lo;
+  part[((int64_t)blockIdx.y * 2 + 1) * F + f] = hi;
+}
+
+__global__ __launch_bounds__(256) void colrange_k(int F, int nparts, double* __restrict__ part) {
+  const int f = blockIdx.x * 256 + threadIdx.x;
+  if (f >= F) return;
+  double lo = part[f], hi = part[F + f];
+  for (int p = 1; p < nparts; ++p) {
+    const double a = part[((int64_t)p * 2 + 0) * F + f], b = part[((int64_t)p * 2 + 1) * F + f];
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  part[f] = lo;
+  part[F + f] = hi;
+}
+
+// one thread per OUTPUT element
+__global__ __launch_bounds__(256) void minmax_apply_k(int64_t n, int F, const void* __restrict__ v,
+                                                      int vtype, const double* __restrict__ range,
+                                                      int layout, int64_t out_row,
+                                                      float* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n * out_row) return;
+  const int64_t row = e / out_row;
+  const int o = (int)(e - row * out_row);
+  int f = o;
+  if (layout == MMAD_NORM_IMG24) {
+    const int c = o >> 10, y = (o >> 5) & 31, x = o & 31;
+    f = c * 768 + ((y * 24) >> 5) * 32 + x;
+  }
+  const double lo = range[f], span = range[F + f] - lo;
+  const double q = (load_any(v, vtype, row * F + f) - lo) / span;
+  out[e] = q == q ? (float)q : 0.f;   // 0/0 (constant column) -> 0
+}
+
+}  // namespace
+
+size_t mmad_minmax_norm_ws_bytes(int64_t n, int F) {
+  if (n < 1 || F < 1) return 0;
+  return (size_t)((n + NORM_ROWS - 1) / NORM_ROWS) * 2 * F * sizeof(double);
+}
+
+int mmad_minmax_norm(int64_t n, int F, const void* v, int vtype, int layout, float* out, void* ws,
+                     size_t ws_bytes, void* stream) {
+  MMAD_CHECK_ARG(n >= 1 && F >= 1 && v && out && ws, "minmax_norm: bad arguments (n=%lld F=%d)",
+                 (long long)n, F);
+  MMAD_CHECK_ARG(vtype >= MMAD_SRC_F64 && vtype <= MMAD_SRC_F32, "minmax_norm: unknown source type %d",
+                 vtype);
+  MMAD_CHECK_ARG(layout == MMAD_NORM_FLAT || (layout == MMAD_NORM_IMG24 && F % 768 == 0),
+                 "minmax_norm: layout %d does not fit F=%d", layout, F);
+  MMAD_CHECK_ARG(ws_bytes >= mmad_minmax_norm_ws_bytes(n, F), "minmax_norm: workspace too small");
+  MMAD_CHECK_ARG(n / NORM_ROWS < 65535, "minmax_norm: n=%lld too large", (long long)n);
+  hipStream_t s = (hipStream_t)stream;
+  double* part = (double*)ws;
+  const int nparts = (int)((n + NORM_ROWS - 1) / NORM_ROWS);
+  colminmax_k<<<dim3((F + 255) / 256, nparts), 256, 0, s>>>(n, F, v, vtype, part);
+  MMAD_LAUNCH_CHECK();
+  colrange_k<<<(F + 255) / 256, 256, 0, s>>>(F, nparts, part);
+  MMAD_LAUNCH_CHECK();
+  const int64_t out_row = layout == MMAD_NORM_IMG24 ? (int64_t)(F / 768) * 1024 : F;
+  const int64_t total = n * out_row;
+  minmax_apply_k<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(n, F, v, vtype, part, layout, out_row,
+                                                                  out);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}

@@ -19,9 +19,11 @@ What is kept from the reference (file:line):
 * ``get_transformed_data`` (:528-552): the whole split in sampler order --
   here ONE device gather instead of the per-index Python loop.
 
-What differs: the dataset is the seeded synthetic window generator
-(data.synth_windows; the HSR recordings are not public, README.md:15) and
-every random choice (row order, sampler order, balancing) comes from a seeded
+The dataset is the HSR export when ``config.data_folder_name`` holds one
+(``hsr_dataset.TabularDataset``: the data_sum CSV schema, PNG look-ups, native
+normalisation and HSR_Net fusion), else the seeded synthetic window generator
+(data.synth_windows; the HSR recordings are not public, README.md:15); every
+random choice (row order, sampler order, balancing) comes from a seeded
 numpy PCG64 generator, so a run is reproducible and the reference can be fed
 the very same batches (tests/golden/gen_e2e.py).
 """
@@ -140,12 +142,33 @@ class SyntheticWindowDataset:
 class TabularDatasetManager:
     """utils/data_loaders.py:465-598."""
 
-    def __init__(self, config, dataset=None, device="cpu"):
-        self.train_dataset = dataset if dataset is not None else SyntheticWindowDataset(config, device)
-        self.total_x = self.train_dataset.data
-        self.total_y = self.train_dataset.targets
+    def __init__(self, config, dataset=None, device="cpu", shuffle=False, data_size=0):
+        if dataset is None:
+            dataset = self._get_dataset(config, device)
+        self.train_dataset = dataset
+        # :476-486: the last data_size windows (0 = all), optionally permuted
+        x, y = dataset.data, dataset.targets
+        if data_size:
+            x, y = x[-data_size:], y[-data_size:]
+        if shuffle:
+            rng = np.random.Generator(np.random.PCG64(int(getattr(config, "data_seed", 0)) + 2))
+            perm = torch.from_numpy(rng.permutation(len(x)))
+            x, y = x[perm.to(x.device)], y[perm]
+        dataset.data, dataset.targets = x, y
+        self.total_x = x
+        self.total_y = y
         self.total_size = len(self.total_x)
         self.sampler_seed = int(getattr(config, "sampler_seed", getattr(config, "data_seed", 0)))
+
+    @staticmethod
+    def _get_dataset(config, device):
+        """utils/data_loaders.py:501-505: the HSR recordings when an export is
+        there (config.data_folder_name / file_name, hsr_dataset.TabularDataset),
+        else the seeded synthetic windows."""
+        from .hsr_dataset import TabularDataset, has_recordings
+        if has_recordings(config):
+            return TabularDataset(config, device=device)
+        return SyntheticWindowDataset(config, device)
 
     def get_indexes(self, ratios=None, labels=None):
         """utils/data_loaders.py:507-526."""

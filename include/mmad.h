@@ -450,6 +450,28 @@ int mmad_hsr_weight_count(void);
 int mmad_hsr_fuse(int n, const float* r, const float* d, const float* t, const float* m,
                   const float* weights, int unimodal, float* out, int ld_out, void* stream);
 
+/* Sensor-stream normalisation of the dataset ingest (TabularDataset,
+ * utils/data_loaders.py:233-434): norm_vec_np (:447-456) = per column
+ * (v - min) / (max - min) over the n windows in float64, NaN (constant
+ * column) -> 0, cast to fp32 -- for the hand-camera / head-depth pixel arrays
+ * (:338-378), the F/T weight (:380-385) and the MFCCs (:386-394).
+ * v: device [n][F] of type vtype (MMAD_SRC_*: the PNG arrays' uint8 / uint16
+ * or the CSV's float64, converted exactly inside the kernel).
+ * layout MMAD_NORM_FLAT: out fp32 [n][F]; MMAD_NORM_IMG24: F = C*24*32 in the
+ * reference's HWC flatten, reinterpreted [C][24][32] (its .view) and
+ * nearest-upsampled to [C][32][32] (its F.interpolate(size=32)): out fp32
+ * [n][C*1024], ready for mmad_hsr_fuse.  ws: mmad_minmax_norm_ws_bytes. */
+#define MMAD_SRC_F64 0
+#define MMAD_SRC_U8 1
+#define MMAD_SRC_U16 2
+#define MMAD_SRC_I32 3
+#define MMAD_SRC_F32 4
+#define MMAD_NORM_FLAT 0
+#define MMAD_NORM_IMG24 1
+size_t mmad_minmax_norm_ws_bytes(int64_t n, int F);
+int mmad_minmax_norm(int64_t n, int F, const void* v, int vtype, int layout, float* out, void* ws,
+                     size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
