@@ -61,8 +61,10 @@ static int g_splitk_dw_blocks = env_int("MMAD_SPLITK_DW_BLOCKS", 512);
 static int g_splitk_dw_min_stages = env_int("MMAD_SPLITK_DW_MIN_STAGES", 8);
 static int g_dw_ws = env_int("MMAD_DW_WS", 0);
 static int g_dw_ws_blocks = env_int("MMAD_DW_WS_BLOCKS", 256);
+static int g_adam_prefetch = env_int("MMAD_ADAM_PREFETCH", 0);
 int mmad_dw_ws_enabled() { return g_dw_ws; }
 int mmad_dw_ws_blocks() { return g_dw_ws_blocks; }
+int mmad_adam_prefetch_enabled() { return g_adam_prefetch; }
 int mmad_splitk_dw_override() { return g_splitk_dw; }
 int mmad_splitk_dw_blocks() { return g_splitk_dw_blocks; }
 int mmad_splitk_dw_min_stages() { return g_splitk_dw_min_stages; }
@@ -121,6 +123,7 @@ int mmad_tune_set(int knob, int value) {
     case 11: g_splitk_dw_min_stages = value; return MMAD_OK;
     case 12: g_dw_ws = value; return MMAD_OK;
     case 13: g_dw_ws_blocks = value; return MMAD_OK;
+    case 14: g_adam_prefetch = value; return MMAD_OK;
     default: mmad_set_error("tune_set: unknown knob %d", knob); return MMAD_EINVAL;
   }
 }

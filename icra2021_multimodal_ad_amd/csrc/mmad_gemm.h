@@ -112,8 +112,11 @@ struct GemmEpi {
   float* bn_dbeta;
   float* bn_dbpart;
   int bn_act;            // BWD_DATA: the BN producer's activation (act' from a)
+  int apf;               // set by the launcher: Adam-state prefetch under the K loop (knob 14)
   int dbg;               // diagnostics (tools/gemm_sweep): 1 skip main loop, 2 skip epilogue,
-                         // 4 force the split-K combine's timeout path (tests)
+                         // 4 force the split-K combine's timeout path (tests),
+                         // 8 skip the FWD Welford partial stores (tools/gemm_phase),
+                         // 16 no Adam-state prefetch
 };
 
 int mmad_group_override();
@@ -127,6 +130,7 @@ int mmad_splitk_dw_blocks();       // dW split rule: target 64x64-tile blocks (k
 int mmad_splitk_dw_min_stages();   // dW split rule: minimum K stages per slice (knob 11)
 int mmad_dw_ws_enabled();          // Adam-fused dW GEMMs on the warp-specialised kernel (knob 12)
 int mmad_dw_ws_blocks();           // its persistent grid cap (knob 13)
+int mmad_adam_prefetch_enabled();  // Adam state loaded under the dW K loop (knob 14)
 int mmad_tile_adam_override();  // >= 0: tile of the Adam-fused dW GEMMs (-2: shape rule)
 int mmad_tile_adam_for(int Mp, int Np, int K);   // ... for a shape
 int mmad_tile_adam_main_override();  // >= 0: ... of those on the main stream

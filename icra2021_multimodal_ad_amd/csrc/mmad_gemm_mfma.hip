@@ -97,6 +97,22 @@ __device__ __forceinline__ int swz(int r) {
   else return r & 7;
 }
 
+// One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4) into the wave's
+// 1 KiB at `dst` (wave-uniform), as inline asm.  Through the builtin, hipcc's
+// wait-count pass tracks the DMA as an LDS write it cannot tell apart from
+// the transposing fragment reads (ds_read_b64_tr_b16) of other ring slots
+// and puts an s_waitcnt vmcnt(0) in front of them -- inside the main loop
+// that drains the whole NS-stage ring every K stage.  Hidden from that pass,
+// the ring is ordered exactly as designed: counted vmcnt + workgroup barrier
+// before a slot is read, a barrier before it is refilled.  (Compiler-tracked
+// loads only see MORE operations outstanding than they count, so their own
+// waits stay correct, just stricter.)
+__device__ __forceinline__ void dma16(const void* src, char* dst) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(MMAD_LDS void*)dst);
+  asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(lds) : "memory");
+}
+
 // issue one stage of one operand: global -> LDS, 16 B per lane, no registers
 template <typename T, bool KMAJ, int ROWS, int NT>
 __device__ __forceinline__ void issue_stage(char* img, const T* __restrict__ G, int ld, int r0,
@@ -110,8 +126,7 @@ __device__ __forceinline__ void issue_stage(char* img, const T* __restrict__ G, 
     const int j = (p % I::CPROW) ^ swz<T, KMAJ, I::RB>(row);
     const T* src = KMAJ ? G + (size_t)(r0 + row) * ld + k0 + j * EPC
                         : G + (size_t)(k0 + row) * ld + r0 + j * EPC;
-    __builtin_amdgcn_global_load_lds((const void*)src,
-                                     (MMAD_LDS void*)(img + (NT * i + (tid & ~63)) * 16), 16, 0, 0);
+    dma16(src, img + (NT * i + (tid & ~63)) * 16);
   }
 }
 
@@ -313,6 +328,11 @@ __device__ __forceinline__ bool col_wait(unsigned* ctr, unsigned gen0, unsigned*
   return shw[0] != 0u;
 }
 
+// Adam-state prefetch under the K loop (knob 14, default off: the held p/m/v
+// registers cost more than the hidden round trip, 36.6 vs 32.9 us on the
+// largest c2 layer; dbg bit 16 turns it off per launch)
+__device__ __forceinline__ bool mmad_apf_on(const GemmEpi& ep) { return ep.apf && !(ep.dbg & 16); }
+
 }  // namespace
 
 // -------------------------------------------------------------------------
@@ -459,12 +479,38 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   // hipcc's lgkmcnt bookkeeping stays exact, and sched_barriers pin the order.
   using FR = typename SubFrag<T>::F;
   const int ra = wm * 16 * TM, rb = wn * 16 * TN;
+  // Adam-fused dW on the 64x64 tile: the tile's p/m/v (4 chunks per thread)
+  // are loaded into registers right after stage 0 has landed, so their HBM
+  // round trip runs under the first NS-1 K stages instead of after the loop.
+  // In issue order they sit behind stages 1..NS-1, so only the waits for
+  // those stages (iterations t <= NS-2) allow APF more newer operations; the
+  // wait for stage NS (older than nothing of them) retires them as well.
+  constexpr int APF_IT = (EPI == GEMM_EPI_BWD_WEIGHT && sizeof(TO) == 4)
+                             ? BM * (BN * (int)sizeof(TO) / 16) / NT : 0;
+  constexpr bool APF_OK = APF_IT > 0 && APF_IT <= 4;
+  constexpr int APF = APF_OK ? 3 * APF_IT : 0;          // vm ops: p, m, v chunks
+  static_assert((NS - 2) * NL + APF <= 63, "vmcnt range");
+  floatx4 aP[APF_OK ? APF_IT : 1], aM[APF_OK ? APF_IT : 1], aV[APF_OK ? APF_IT : 1];
+  const bool apf = APF_OK && ep.ad_p && S == 1 && nt >= 2 * NS - 1 && mmad_apf_on(ep);
   if (nt > 0) {
 #pragma unroll
     for (int s = 0; s < NS; ++s)
       if (s < nt) issue(s);
     if (nt >= NS) wait_vmcnt<(NS - 1) * NL>();
     else wait_vmcnt<0>();
+    if constexpr (APF_OK) {
+      if (apf) {
+        constexpr int CPRA = BN * (int)sizeof(TO) / 16;
+#pragma unroll
+        for (int u = 0; u < APF_IT; ++u) {
+          const int idx = u * NT + tid;
+          const size_t off = (size_t)(m0 + idx / CPRA) * ep.ldo + n0 + (idx % CPRA) * 4;
+          aP[u] = *(const floatx4*)(ep.ad_p + off);
+          aM[u] = *(const floatx4*)(ep.ad_m + off);
+          aV[u] = *(const floatx4*)(ep.ad_v + off);
+        }
+      }
+    }
     block_barrier();
     FR f0a[TM], f0b[TN], f1a[TM], f1b[TN];
     read_sub<T, AK, BK_, NAT, BM, BN, TM, TN>(smem, smem + IA::BYTES, ra, rb, 0, lane, f0a, f0b);
@@ -479,8 +525,12 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
       mma_half<T, TM, TN, 1>(acc, f0a, f0b);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (!LAST) {
-        if constexpr (ISSUE) wait_vmcnt<(NS - 2) * NL>();
-        else wait_tail<NL>(nt - t - 2);
+        if constexpr (ISSUE) {
+          if (APF_OK && apf && t <= NS - 2) wait_vmcnt<(NS - 2) * NL + APF>();
+          else wait_vmcnt<(NS - 2) * NL>();
+        } else {
+          wait_tail<NL>(nt - t - 2);
+        }
         wait_lgkm0();
         block_barrier();                     // stage t+1 visible; slot t free
         if constexpr (ISSUE) issue(t + NS);
@@ -735,7 +785,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
             }
           q += __shfl_xor(q, 16);
           q += __shfl_xor(q, 32);
-          if (g == 0) {
+          if (g == 0 && !(ep.dbg & 8)) {
             if (ep.bn_sync) {   // handed to the other blocks of this column: sc1
               st_sc1(part + col, mean);
               st_sc1(part + ep.ldpart + col, q);
@@ -809,6 +859,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
     // (the three state arrays may alias as far as the compiler knows).
     constexpr int AG = ITERS < 4 ? ITERS : 4;
     static_assert(ITERS % AG == 0, "Adam chunk groups");
+    static_assert(!APF_OK || ITERS == APF_IT, "Adam prefetch layout");
 #pragma unroll
     for (int i0 = 0; i0 < ITERS; i0 += AG) {
       floatx4 P[AG], Mm[AG], Vv[AG];
@@ -818,9 +869,15 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         const int idx = (i0 + u) * NT + tid;
         const int rl = idx / CPR, ch = idx % CPR;
         off[u] = (size_t)(m0 + rl) * ep.ldo + n0 + ch * OEPC;
-        P[u] = *(const floatx4*)(ep.ad_p + off[u]);
-        Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
-        Vv[u] = *(const floatx4*)(ep.ad_v + off[u]);
+        if (APF_OK && apf) {
+          P[u] = aP[(i0 + u) % (APF_OK ? APF_IT : 1)];
+          Mm[u] = aM[(i0 + u) % (APF_OK ? APF_IT : 1)];
+          Vv[u] = aV[(i0 + u) % (APF_OK ? APF_IT : 1)];
+        } else {
+          P[u] = *(const floatx4*)(ep.ad_p + off[u]);
+          Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
+          Vv[u] = *(const floatx4*)(ep.ad_v + off[u]);
+        }
       }
 #pragma unroll
       for (int u = 0; u < AG; ++u) {
@@ -1797,6 +1854,7 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   MMAD_CHECK_ARG(dtype == MMAD_BF16 || dtype == MMAD_F32, "gemm: bad dtype %d", dtype);
   GemmEpi ep = ep_in;
   ep.dbg = mmad_dbg_override();
+  ep.apf = mmad_adam_prefetch_enabled();
   const bool bnf = ep.bn_sync != nullptr;
   MMAD_CHECK_ARG(!bnf || epi == GEMM_EPI_FWD || epi == GEMM_EPI_BWD_DATA,
                  "gemm: fused BN only for the forward / bwd-data epilogues");

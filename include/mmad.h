@@ -55,7 +55,9 @@ int mmad_pad_granule(void);
  * split rule's target number of 64x64-tile blocks (512) and minimum K stages
  * per slice (8), knob 12 = Adam-fused dW GEMMs on the warp-specialised
  * persistent kernel (1) or the plain tile kernel (0, default: measured
- * faster), knob 13 = that kernel's grid cap (256 workgroups),
+ * faster), knob 13 = that kernel's grid cap (256 workgroups), knob 14 = load
+ * the Adam state of a 64x64 Adam-fused dW tile under its K loop (1) or after it
+ * (0, default: measured faster, 32.9 vs 36.6 us for the largest c2 layer),
  * knob 5 = tile of the dW GEMMs with the fused Adam epilogue (default 3 =
  * 64x64; -1 = autotuned like the others), knobs 6 / 7 = tile of the bwd-data /
  * forward GEMMs (-1 = autotuned), knob 8 = tile of the Adam-fused dW GEMMs
