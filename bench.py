@@ -110,11 +110,11 @@ def dw_adam_bytes(N, K, B, es=2):
 def pick_dominant_layer(nat, batch):
     """Largest parameter count among the layers whose dW GEMM carries the
     fused Adam epilogue.  Below 4096 windows every layer does (ties: the
-    first, encoder layer 1, on the main stream at the end of the chain); from
-    4096 windows (MMAD_DW_SPLIT default) layers 0 and 1 (l < MMAD_DW_MAIN = 2)
-    run as a dW GEMM + flat Adam pass instead (ties: the last, the decoder's
-    output layer on the side stream)."""
-    sp = os.environ.get("MMAD_DW_SPLIT", "-1")
+    first, encoder layer 1, on the main stream at the end of the chain); with
+    the split tail (MMAD_DW_SPLIT=1, or -1 from 4096 windows) layers 0 and 1
+    (l < MMAD_DW_MAIN = 2) run as a dW GEMM + flat Adam pass instead (ties:
+    the last, the decoder's output layer on the side stream)."""
+    sp = os.environ.get("MMAD_DW_SPLIT", "0")
     split = sp not in ("-1", "0") or (sp == "-1" and batch >= 4096)
     if not split:
         return max(range(len(nat.layers)), key=lambda l: (nat.layers[l]["N"] * nat.layers[l]["K"], -l))

@@ -87,13 +87,14 @@ struct mmad_ae {
   // over the weights instead of one Adam-fused dW GEMM: layer l >= 1's GEMM
   // starts on the tail stream as soon as dz_l exists, its Adam once
   // bwd-data(l) has read W_l, both overlapping the end of the chain
-  // (MMAD_DW_SPLIT=0: the fused form on the main stream).  Default (-1): split
-  // from 4096 rows per call (VIB D=2048 B=4096: 1.217 vs 1.244 ms/step), fused
-  // below (D=2048 B=1024: 0.496 fused vs 0.520 split -- the early dW_1 GEMM
-  // slows the bwd-data chain it overlaps; profiles/r02o_*)
+  // (MMAD_DW_SPLIT=0: the fused form on the main stream; -1: split from 4096
+  // rows per call).  Default 0: since the dW GEMM loop stopped draining its
+  // LDS ring every K stage (asm LDS-DMA) the fused form wins at both sizes
+  // (VIB D=2048 B=4096: 0.991-0.996 vs 1.013 ms/step; D=2048 B=1024: 0.455 vs
+  // 0.468; profiles/r02ad_*, r02ae_*; before: split 1.217 vs 1.244 at 4096)
   int dw_split = [] {
     const char* e = getenv("MMAD_DW_SPLIT");
-    return e ? atoi(e) : -1;
+    return e ? atoi(e) : 0;
   }();
   int mse_tiles = 0;   // loss partials written by the last MSE GEMM
   // data parallelism: RCCL communicator (not owned), its stream and events

@@ -57,7 +57,10 @@ static int env_int(const char* name, int dflt) {
   return e ? atoi(e) : dflt;
 }
 static int g_splitk_dw = env_int("MMAD_GEMM_SPLITK_DW", 0);
-static int g_splitk_dw_blocks = env_int("MMAD_SPLITK_DW_BLOCKS", 512);
+// dW split-K target blocks (0 = no split): 512 paid before the dW loop stopped
+// draining its LDS ring every K stage; since then no split measures faster
+// (VIB B=4096 0.991-0.996 vs 1.013 ms/step with the split tail off; r02ae_*)
+static int g_splitk_dw_blocks = env_int("MMAD_SPLITK_DW_BLOCKS", 0);
 static int g_splitk_dw_min_stages = env_int("MMAD_SPLITK_DW_MIN_STAGES", 8);
 static int g_dw_ws = env_int("MMAD_DW_WS", 0);
 static int g_dw_ws_blocks = env_int("MMAD_DW_WS_BLOCKS", 256);

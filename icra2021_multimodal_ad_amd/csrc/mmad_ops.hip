@@ -185,7 +185,9 @@ __global__ __launch_bounds__(256) void bn_fold_k(int M, int N, int Np, const flo
                                                  float* shift, const float* __restrict__ W,
                                                  TW* __restrict__ wout, float* __restrict__ cpart,
                                                  int cp_stride) {
-  constexpr int U = 8;
+  // all of a group's partials in flight at once (128 partial rows = 4096
+  // windows in one round trip; the merge order below is unchanged)
+  constexpr int U = 32;
   __shared__ double pm[4][64], pq[4][64], pn[4][64];
   __shared__ float s_sc[64], s_sh[64];
   const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64 * FOLD_RPT, tid = threadIdx.x;

@@ -52,7 +52,7 @@ int mmad_pad_granule(void);
  * combine's timeout path, tests only), knob 4 = split-K
  * factor override for GEMMs given split-K workspace (0 = shape rule, 1/2/4/
  * 8/16), knob 9 = the same for the dW GEMMs only, knobs 10 / 11 = the dW
- * split rule's target number of 64x64-tile blocks (512) and minimum K stages
+ * split rule's target number of 64x64-tile blocks (0 = no split, default) and minimum K stages
  * per slice (8), knob 12 = Adam-fused dW GEMMs on the warp-specialised
  * persistent kernel (1) or the plain tile kernel (0, default: measured
  * faster), knob 13 = that kernel's grid cap (256 workgroups), knob 14 = load

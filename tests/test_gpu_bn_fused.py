@@ -138,3 +138,25 @@ def test_fused_bn_deterministic_and_tile_independent(monkeypatch):
         assert torch.equal(outs[0][1], o[1])
         assert torch.equal(outs[0][2], o[2])
     assert torch.equal(outs[0][0], outs[1][0])   # same tiles: bit-identical loss too
+
+
+@pytest.mark.parametrize("rows", [1024, 4096])
+def test_split_tail_matches_fused_tail(monkeypatch, rows):
+    """The split tail (MMAD_DW_SPLIT=1: layers 0 and 1 as a plain dW GEMM on a
+    tail stream + a flat Adam pass) against the default fused tail (Adam in
+    the dW epilogue): the same dW accumulation and the same Adam formula, so
+    the same parameters bit for bit after 3 steps, and the same losses."""
+    sd = init_state_dict(2048, 100, 5, seed=14)
+    ms = []
+    for split in ("1", "0"):
+        monkeypatch.setenv("MMAD_DW_SPLIT", split)
+        m, _ = _mk(monkeypatch, 1, 2048, 100, 5, sd, dtype="bf16")
+        m._native.sync_shadow(force=True)
+        ms.append(m)
+    for s in range(3):
+        x = torch.from_numpy(synth_windows(rows, 2048, seed=80 + s)).cuda()
+        la, lb = (float(m._native.train_step_fused(x)) for m in ms)
+        assert la == lb, (s, la, lb)
+    for m in ms:
+        m._native.check_status()
+    assert torch.equal(ms[0]._native.params, ms[1]._native.params)
