@@ -96,6 +96,20 @@ struct mmad_ae {
     const char* e = getenv("MMAD_DW_SPLIT");
     return e ? atoi(e) : 0;
   }();
+  // fused step, layers < dw_main (the main-stream tail): the dW GEMM without
+  // Adam publishing each fp32 tile (tile flags) and the streamed Adam
+  // (mmad_adam_stream_kernel) consuming the tiles as they complete on the tail
+  // stream, so the tile's K loop and the Adam state stream overlap instead of
+  // running one after the other in the same waves (MMAD_ADAM_STREAM; grid
+  // MMAD_ADAM_STREAM_GRID workgroups, at most one per CU)
+  int adam_stream = [] {
+    const char* e = getenv("MMAD_ADAM_STREAM");
+    return e ? atoi(e) : 1;
+  }();
+  int adam_stream_grid = [] {
+    const char* e = getenv("MMAD_ADAM_STREAM_GRID");
+    return e ? atoi(e) : 256;
+  }();
   int mse_tiles = 0;   // loss partials written by the last MSE GEMM
   // data parallelism: RCCL communicator (not owned), its stream and events
   mmad_comm* comm = nullptr;
@@ -212,6 +226,7 @@ struct LayerWS {
   bool fwd_fused, bwd_fused;
   unsigned* sync_f;   // fused-BN barrier counters (MMAD_BN_SYNC_WORDS each)
   unsigned* sync_b;
+  unsigned* tflag;    // streamed-Adam tile flags of this layer's dW GEMM ((Np/64)*(Kp/64))
 };
 struct AeWS {
   int B, k, Mpe, Mpd;
@@ -249,7 +264,11 @@ static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
     mmad_gemm_splitk_bytes(0, 0, &slab, &ctl);
     ctl = (ctl + 255) / 256 * 256;
     // + fused-BN barrier counters: 2 blocks per layer, then the error word
-    const size_t bn_ctl = ((size_t)(2 * h->L.size() * MMAD_BN_SYNC_WORDS + 64) * 4 + 255) / 256 * 256;
+    // + the streamed-Adam tile flags, one word per 64x64 dW tile of every layer
+    size_t tf_words = 0;
+    for (const AeLayer& a : h->L) tf_words += (size_t)(a.Np / 64) * (a.Kp / 64);
+    const size_t bn_ctl =
+        ((size_t)(2 * h->L.size() * MMAD_BN_SYNC_WORDS + 64 + tf_words) * 4 + 255) / 256 * 256;
     w.sk_ctl_bytes = 2 * ctl + bn_ctl;
     char* c = take((int64_t)w.sk_ctl_bytes);
     w.sk_ctl[0] = (unsigned*)c;
@@ -257,10 +276,13 @@ static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
     unsigned* bc = c ? (unsigned*)(c + 2 * ctl) : nullptr;
     w.bn_err = bc ? bc + 2 * h->L.size() * MMAD_BN_SYNC_WORDS : nullptr;
     w.l.resize(h->L.size());
+    unsigned* tf = bc ? bc + 2 * h->L.size() * MMAD_BN_SYNC_WORDS + 64 : nullptr;
     for (size_t i = 0; i < h->L.size(); ++i) {
       w.l[i].sync_f = bc ? bc + (2 * i) * MMAD_BN_SYNC_WORDS : nullptr;
       w.l[i].sync_b = bc ? bc + (2 * i + 1) * MMAD_BN_SYNC_WORDS : nullptr;
       w.l[i].fwd_fused = w.l[i].bwd_fused = false;
+      w.l[i].tflag = tf;
+      if (tf) tf += (size_t)(h->L[i].Np / 64) * (h->L[i].Kp / 64);
     }
   }
   w.B = B;
@@ -441,7 +463,8 @@ int mmad_ae_bind(mmad_ae* h, float* params, float* grads, float* adam_m, float* 
       MMAD_HIP_CHECK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking,
                                                  (sp && atoi(sp) == 1) ? greatest : least));
     }
-    if (h->dw_tail || h->dw_split) MMAD_HIP_CHECK(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
+    if (h->dw_tail || h->dw_split || h->adam_stream)
+      MMAD_HIP_CHECK(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
     const size_t n = h->L.size();
     h->ev_fork.resize(n);
     h->ev_data.resize(n);
@@ -523,7 +546,7 @@ static int prepare_ws(const mmad_ae* h, int B, int k, void* ws, int64_t ws_bytes
   w.bn_mode = h->bn_mode;
   if (w.bn_mode == 2 && w.Mpd > h->bn_fused_rows) w.bn_mode = h->fold ? 1 : 0;
   if (w.bn_mode == 1 && !h->fold) w.bn_mode = 0;
-  if ((splitk_possible(h->dtype) || h->bn_mode == 2) && ws != h->ws_zeroed) {
+  if ((splitk_possible(h->dtype) || h->bn_mode == 2 || h->adam_stream) && ws != h->ws_zeroed) {
     MMAD_HIP_CHECK(hipMemsetAsync(w.sk_ctl[0], 0, w.sk_ctl_bytes, st));
     const_cast<mmad_ae*>(h)->ws_zeroed = ws;
   }
@@ -905,6 +928,34 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
         MMAD_HIP_CHECK(hipStreamWaitEvent(h->tail, h->ev_data[l], 0));
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, h->tail,
                        nullptr, PROBE_DW + l));
+        used_tail = true;
+      } else if (on_main && h->adam_stream && h->tail) {
+        // dW GEMM (small-segment Adam in its epilogue) publishing its tiles
+        // on the main stream, the weight Adam streamed beside it on the tail
+        // stream, started when the GEMM is (bwd-data(l), which read W_l, is
+        // before it on the main stream)
+        GemmEpi e = dwe;
+        fill_adam(e, l, false);
+        e.tile_flag = s.tflag;
+        e.dw_nostore = 0;
+        const bool prb = PROBE_DW + l == h->probe_id && !h->capturing &&
+                         2 * h->probe_n < (int)h->probe_ev.size();
+        MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
+        MMAD_HIP_CHECK(hipStreamWaitEvent(h->tail, h->ev_fork[l], 0));
+        if (prb) MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n], st));
+        int cfg = -1;
+        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, e, st, &cfg));
+        GemmEpi c{};
+        fill_adam(c, l, true);
+        c.sm_p = nullptr;                  // the GEMM's epilogue did the small segment
+        c.tile_flag = s.tflag;
+        c.bn_err = w.bn_err;
+        RET_IF(mmad_adam_stream(cfg, h->grads + a.w_off, a.Kp, a.Np, a.Kp, c, h->adam_stream_grid,
+                                h->tail));
+        if (prb) {
+          MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n + 1], h->tail));
+          ++h->probe_n;
+        }
         used_tail = true;
       } else if (on_main) {
         dwe.tile_force = mmad_tile_adam_main_override() + 1;
@@ -1327,13 +1378,13 @@ int mmad_ae_status(mmad_ae* h, void* ws, int64_t ws_bytes, void* stream) {
   MMAD_CHECK_ARG(h, "ae_status: null handle");
   // no split-K GEMM / fused-BN barrier can have run unless the dtype /
   // override / BN mode allows one
-  if ((!splitk_possible(h->dtype) && h->bn_mode != 2) || !ws) return MMAD_OK;
+  if ((!splitk_possible(h->dtype) && h->bn_mode != 2 && !h->adam_stream) || !ws) return MMAD_OK;
   AeWS w;
   carve(h, 1, 1, (char*)ws, w);
   MMAD_CHECK_ARG(ws_bytes >= w.bytes, "ae_status: workspace too small");
   for (int r = 0; r < 2; ++r)
     RET_IF(mmad_gemm_read_status(w.sk_ctl[r], (hipStream_t)stream, "ae_status"));
-  if (h->bn_mode == 2 && w.bn_err) {
+  if ((h->bn_mode == 2 || h->adam_stream) && w.bn_err) {
     unsigned word = 0;
     MMAD_HIP_CHECK(hipMemcpyAsync(&word, w.bn_err, sizeof(word), hipMemcpyDeviceToHost, (hipStream_t)stream));
     MMAD_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
@@ -1342,8 +1393,8 @@ int mmad_ae_status(mmad_ae* h, void* ws, int64_t ws_bytes, void* stream) {
       // counters raised) for the next call
       MMAD_HIP_CHECK(hipMemsetAsync(w.sk_ctl[0], 0, w.sk_ctl_bytes, (hipStream_t)stream));
       MMAD_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
-      mmad_set_error("ae_status: a fused BatchNorm column barrier timed out; the outputs of that "
-                     "call are invalid");
+      mmad_set_error("ae_status: a fused BatchNorm column barrier or a streamed-Adam tile wait timed "
+                     "out; the outputs of that call are invalid");
       return MMAD_EHIP;
     }
   }

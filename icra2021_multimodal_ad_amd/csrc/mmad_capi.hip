@@ -65,6 +65,8 @@ static int g_splitk_dw_min_stages = env_int("MMAD_SPLITK_DW_MIN_STAGES", 8);
 static int g_dw_ws = env_int("MMAD_DW_WS", 0);
 static int g_dw_ws_blocks = env_int("MMAD_DW_WS_BLOCKS", 256);
 static int g_adam_prefetch = env_int("MMAD_ADAM_PREFETCH", 0);
+static int g_adam_nt = env_int("MMAD_ADAM_NT", 0);
+int mmad_adam_nt_enabled() { return g_adam_nt; }
 int mmad_dw_ws_enabled() { return g_dw_ws; }
 int mmad_dw_ws_blocks() { return g_dw_ws_blocks; }
 int mmad_adam_prefetch_enabled() { return g_adam_prefetch; }
@@ -127,6 +129,7 @@ int mmad_tune_set(int knob, int value) {
     case 12: g_dw_ws = value; return MMAD_OK;
     case 13: g_dw_ws_blocks = value; return MMAD_OK;
     case 14: g_adam_prefetch = value; return MMAD_OK;
+    case 15: g_adam_nt = value; return MMAD_OK;
     default: mmad_set_error("tune_set: unknown knob %d", knob); return MMAD_EINVAL;
   }
 }

@@ -113,6 +113,10 @@ struct GemmEpi {
   float* bn_dbpart;
   int bn_act;            // BWD_DATA: the BN producer's activation (act' from a)
   int apf;               // set by the launcher: Adam-state prefetch under the K loop (knob 14)
+  int ad_nt;             // set by the launcher: non-temporal Adam-state loads/stores (knob 15)
+  // BWD_WEIGHT without ad_p: the fp32 tile is stored write-through and the
+  // block raises tile_flag[blockIdx] for the streamed Adam (mmad_adam_stream)
+  unsigned* tile_flag;
   int dbg;               // diagnostics (tools/gemm_sweep): 1 skip main loop, 2 skip epilogue,
                          // 4 force the split-K combine's timeout path (tests),
                          // 8 skip the FWD Welford partial stores (tools/gemm_phase),
@@ -131,6 +135,7 @@ int mmad_splitk_dw_min_stages();   // dW split rule: minimum K stages per slice 
 int mmad_dw_ws_enabled();          // Adam-fused dW GEMMs on the warp-specialised kernel (knob 12)
 int mmad_dw_ws_blocks();           // its persistent grid cap (knob 13)
 int mmad_adam_prefetch_enabled();  // Adam state loaded under the dW K loop (knob 14)
+int mmad_adam_nt_enabled();        // non-temporal Adam-state accesses in the dW epilogue (knob 15)
 int mmad_tile_adam_override();  // >= 0: tile of the Adam-fused dW GEMMs (-2: shape rule)
 int mmad_tile_adam_for(int Mp, int Np, int K);   // ... for a shape
 int mmad_tile_adam_main_override();  // >= 0: ... of those on the main stream
@@ -165,5 +170,9 @@ int mmad_gemm_read_status(unsigned* ctl, hipStream_t s, const char* who);
 bool mmad_gemm_bn_fusable(int dtype, int epi, int Mp, int Np);
 
 // cfg_used (nullable) receives the tile configuration launched
+// Adam over a flagged dW GEMM's tiles as they complete (launch on another
+// stream AFTER the GEMM; grid rounded to a multiple of 8, <= one block per CU)
+int mmad_adam_stream(int cfg, const float* g, int ld, int Mp, int Np, const GemmEpi& ep, int grid,
+                     hipStream_t s);
 int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,
                        int Np, int K, const GemmEpi& ep, hipStream_t s, int* cfg_used = nullptr);

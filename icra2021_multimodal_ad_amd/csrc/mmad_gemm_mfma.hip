@@ -873,6 +873,11 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
           P[u] = aP[(i0 + u) % (APF_OK ? APF_IT : 1)];
           Mm[u] = aM[(i0 + u) % (APF_OK ? APF_IT : 1)];
           Vv[u] = aV[(i0 + u) % (APF_OK ? APF_IT : 1)];
+        } else if (ep.ad_nt) {
+          // streaming state: keep the K loop's operand panels in L2
+          P[u] = __builtin_nontemporal_load((const floatx4*)(ep.ad_p + off[u]));
+          Mm[u] = __builtin_nontemporal_load((const floatx4*)(ep.ad_m + off[u]));
+          Vv[u] = __builtin_nontemporal_load((const floatx4*)(ep.ad_v + off[u]));
         } else {
           P[u] = *(const floatx4*)(ep.ad_p + off[u]);
           Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
@@ -887,14 +892,19 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         if (!ep.dw_nostore) *(uint4v*)(out + off[u]) = v;
         adam4(P[u], Mm[u], Vv[u], __builtin_bit_cast(floatx4, v), ep.ad_b1, ep.ad_b2, ep.ad_eps,
               ad_step, ad_bc2);
-        *(floatx4*)(ep.ad_p + off[u]) = P[u];
-        *(floatx4*)(ep.ad_m + off[u]) = Mm[u];
-        *(floatx4*)(ep.ad_v + off[u]) = Vv[u];
-        if (ep.ad_shadow) {
-          bf16x4 sh;
+        bf16x4 sh;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) sh[e] = (bf16)P[u][e];
-          *(bf16x4*)((bf16*)ep.ad_shadow + off[u]) = sh;
+        for (int e = 0; e < 4; ++e) sh[e] = (bf16)P[u][e];
+        if (ep.ad_nt) {
+          __builtin_nontemporal_store(P[u], (floatx4*)(ep.ad_p + off[u]));
+          __builtin_nontemporal_store(Mm[u], (floatx4*)(ep.ad_m + off[u]));
+          __builtin_nontemporal_store(Vv[u], (floatx4*)(ep.ad_v + off[u]));
+          if (ep.ad_shadow) __builtin_nontemporal_store(sh, (bf16x4*)((bf16*)ep.ad_shadow + off[u]));
+        } else {
+          *(floatx4*)(ep.ad_p + off[u]) = P[u];
+          *(floatx4*)(ep.ad_m + off[u]) = Mm[u];
+          *(floatx4*)(ep.ad_v + off[u]) = Vv[u];
+          if (ep.ad_shadow) *(bf16x4*)((bf16*)ep.ad_shadow + off[u]) = sh;
         }
       }
     }
@@ -918,7 +928,14 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
       const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
       const int row = m0 + rl;
       const int col = n0 + ch * OEPC;
-      if (out) *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
+      if (EPI == GEMM_EPI_BWD_WEIGHT && ep.tile_flag) {
+        // handed to the streamed Adam (mmad_adam_stream_kernel): write-through
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            out + (size_t)m0 * ep.ldo, 0, BM * ep.ldo * (int)sizeof(TO), 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, (rl * ep.ldo + col) * (int)sizeof(TO), 0, 16 /*sc1*/);
+      } else if (out) {
+        *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
+      }
       if constexpr (EPI == GEMM_EPI_SCORE) {
         const uint4v rv = rvs[it];
         const TO* pv = (const TO*)&v;
@@ -946,6 +963,13 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         for (int o = 1; o < CPR128; o <<= 1) sq += __shfl_xor(sq, o);
         if (ch % CPR128 == 0) ep.rowsq[(size_t)(col / 128) * ep.ldrow + row] = sq;
       }
+    }
+    if (EPI == GEMM_EPI_BWD_WEIGHT && ep.tile_flag) {
+      // every wave's sc1 tile stores landed, then one lane raises this
+      // block's flag (MI355X_MICROARCH.md hand-off table, row 1)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(ep.tile_flag + bid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if constexpr (EPI == GEMM_EPI_FWD) {
@@ -1532,6 +1556,115 @@ __global__ __launch_bounds__(2 * Cfg<CFG>::NT, 1) void mmad_dw_adam_ws_kernel(
 }
 
 // -------------------------------------------------------------------------
+// Streamed Adam for a dW GEMM (tuning knob 16, the tail layers of the fused
+// step).  The Adam-fused dW kernel runs its K loop (L2-fed, latency-bound)
+// and then the tile's Adam stream (26 B per parameter from HBM) one after the
+// other in the same waves, and the co-resident blocks of a CU do the same in
+// lockstep, so HBM idles through the loops and the loops wait for the stream.
+// Here the dW GEMM (mmad_gemm_kernel, no Adam) writes each fp32 tile
+// write-through and raises the flag of its block; this kernel, launched
+// beside it on another stream, walks the producer's blocks f = a, a + grid,
+// ... (a multiple-of-8 grid: f and a share an XCD under round-robin
+// dispatch, a speed bonus only), loads the tile's p / m / v BEFORE polling
+// its flag (they do not depend on the GEMM), then reads the dW tile with sc1
+// loads and applies the same adam4 as the fused epilogue (same bits).  The
+// consumer resets each flag after use.  One 256-thread block per CU, no LDS:
+// the GEMM's blocks always fit beside it, and it is enqueued after the
+// GEMM, so the producer is never starved; a flag that never rises within
+// ~2^20 polls sets the sticky error word and the block exits.
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void mmad_adam_stream_kernel(const float* __restrict__ g, int ld,
+                                                                GemmEpi ep, int ntiles) {
+  constexpr int NT = 256;
+  constexpr int CPR = BN / 4;                  // 16-B chunks per row
+  constexpr int CH = BM * CPR / NT;            // chunks per thread per tile
+  constexpr int AG = CH < 4 ? CH : 4;          // chunks in flight per group
+  static_assert(CH % AG == 0, "chunk groups");
+  __shared__ unsigned okw;
+  const int tid = threadIdx.x;
+  float ad_step = ep.ad_step, ad_bc2 = ep.ad_bc2;
+  if (ep.dyn) {
+    ad_step = ep.dyn->ad_step;
+    ad_bc2 = ep.dyn->ad_bc2;
+  }
+  for (int f = blockIdx.x; f < ntiles; f += gridDim.x) {
+    // producer block f -> output tile (the mapping of mmad_gemm_kernel, S = 1)
+    int tm, tn;
+    {
+      const int q = ntiles >> 3, r = ntiles & 7, xcd = f & 7;
+      const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (f >> 3);
+      const int tiles_m = ntiles / ep.tiles_n;
+      const int per_group = ep.group_m * ep.tiles_n;
+      const int first_m = (tile / per_group) * ep.group_m;
+      const int gsz = min(tiles_m - first_m, ep.group_m);
+      tm = first_m + (tile % per_group) % gsz;
+      tn = (tile % per_group) / gsz;
+    }
+    const size_t base = (size_t)(tm * BM) * ld + tn * BN;
+    floatx4 P[AG], Mm[AG], Vv[AG];
+    size_t off[AG];
+#pragma unroll
+    for (int u = 0; u < AG; ++u) {
+      const int idx = u * NT + tid;
+      off[u] = base + (size_t)(idx / CPR) * ld + (idx % CPR) * 4;
+      P[u] = *(const floatx4*)(ep.ad_p + off[u]);
+      Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
+      Vv[u] = *(const floatx4*)(ep.ad_v + off[u]);
+    }
+    if (tid == 0) {
+      unsigned ok = 0u;
+      for (unsigned spins = 0; spins < (1u << 20); ++spins) {
+        if (__hip_atomic_load(ep.tile_flag + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+          ok = 1u;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (!ok) __hip_atomic_store(ep.bn_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      okw = ok;
+    }
+    __syncthreads();
+    if (!okw) return;   // uniform: the host reports the sticky word
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(g + (size_t)(tm * BM) * ld), 0, BM * ld * 4, 0x00020000);
+#pragma unroll
+    for (int i0 = 0; i0 < CH; i0 += AG) {
+      if (i0 > 0) {
+#pragma unroll
+        for (int u = 0; u < AG; ++u) {
+          const int idx = (i0 + u) * NT + tid;
+          off[u] = base + (size_t)(idx / CPR) * ld + (idx % CPR) * 4;
+          P[u] = *(const floatx4*)(ep.ad_p + off[u]);
+          Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
+          Vv[u] = *(const floatx4*)(ep.ad_v + off[u]);
+        }
+      }
+      floatx4 G[AG];
+#pragma unroll
+      for (int u = 0; u < AG; ++u) {
+        const int idx = (i0 + u) * NT + tid;
+        G[u] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               rs, ((idx / CPR) * ld + tn * BN + (idx % CPR) * 4) * 4, 0, 16 /*sc1*/));
+      }
+#pragma unroll
+      for (int u = 0; u < AG; ++u) {
+        adam4(P[u], Mm[u], Vv[u], G[u], ep.ad_b1, ep.ad_b2, ep.ad_eps, ad_step, ad_bc2);
+        *(floatx4*)(ep.ad_p + off[u]) = P[u];
+        *(floatx4*)(ep.ad_m + off[u]) = Mm[u];
+        *(floatx4*)(ep.ad_v + off[u]) = Vv[u];
+        if (ep.ad_shadow) {
+          bf16x4 sh;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sh[e] = (bf16)P[u][e];
+          *(bf16x4*)((bf16*)ep.ad_shadow + off[u]) = sh;
+        }
+      }
+    }
+    if (tid == 0) __hip_atomic_store(ep.tile_flag + f, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// -------------------------------------------------------------------------
 // host-side planning and launch
 // -------------------------------------------------------------------------
 static bool cfg_fits(int cfg, int Mp, int Np, int epi) {
@@ -1564,6 +1697,16 @@ static int heuristic_cfg(int Mp, int Np, int epi) {
   return heuristic_cfg(Mp, Np, epi, [&](int c) { return cfg_fits(c, Mp, Np, epi); });
 }
 
+// group height balancing the per-XCD A-panel (gm*BM rows) and B-panel
+// ((ntiles/8/gm)*BN cols) footprints
+static int plan_group_m(int ntiles, int tiles_m, int BM, int BN) {
+  const double per_xcd = ntiles / 8.0;
+  int gm = (int)(sqrt(per_xcd * BN / BM) + 0.5);
+  const int env_gm = mmad_group_override();
+  if (env_gm > 0) gm = env_gm;
+  return gm < 1 ? 1 : (gm > tiles_m ? tiles_m : gm);
+}
+
 template <typename T, typename TO, bool AK, bool BK_, int EPI>
 static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np, int K,
                         const GemmEpi& ep_in, int cfg, hipStream_t s) {
@@ -1572,13 +1715,7 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
   GemmEpi ep = ep_in;
   ep.tiles_n = tiles_n;
   const int S = ep.splitk > 1 ? ep.splitk : 1;
-  // group height balancing the per-XCD A-panel (gm*BM rows) and B-panel
-  // ((ntiles/8/gm)*BN cols) footprints
-  const double per_xcd = ntiles * S / 8.0;
-  int gm = (int)(sqrt(per_xcd / S * BN / BM) + 0.5);
-  const int env_gm = mmad_group_override();
-  if (env_gm > 0) gm = env_gm;
-  ep.group_m = gm < 1 ? 1 : (gm > tiles_m ? tiles_m : gm);
+  ep.group_m = plan_group_m(ntiles, tiles_m, BM, BN);
   dim3 grd(ntiles * S), blk(CFG_NT[cfg]);
   const size_t dyn = ep.lds_pad > 0 ? (size_t)ep.lds_pad : 0;
   switch (cfg) {
@@ -1708,6 +1845,7 @@ static int tune_cfg(int dtype, int epi, const void* A, int lda, const void* B, i
   et.sm_p = nullptr;
   et.bn_rmean = nullptr;   // fused BN: no running-statistics update while timing
   et.bn_rvar = nullptr;
+  et.tile_flag = nullptr;   // no hand-off from a trial launch
   hipEvent_t e0, e1;
   MMAD_HIP_CHECK(hipEventCreate(&e0));
   MMAD_HIP_CHECK(hipEventCreate(&e1));
@@ -1855,13 +1993,16 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   GemmEpi ep = ep_in;
   ep.dbg = mmad_dbg_override();
   ep.apf = mmad_adam_prefetch_enabled();
+  ep.ad_nt = mmad_adam_nt_enabled();
   const bool bnf = ep.bn_sync != nullptr;
   MMAD_CHECK_ARG(!bnf || epi == GEMM_EPI_FWD || epi == GEMM_EPI_BWD_DATA,
                  "gemm: fused BN only for the forward / bwd-data epilogues");
   MMAD_CHECK_ARG(!bnf || Np / 64 <= MMAD_BN_EXIT, "gemm: fused BN: Np=%d too wide", Np);
   // the fused BN barrier needs one block per output tile (no split) and the
   // whole grid resident
-  ep.splitk = (ep.sk_slab && ep.sk_ctl && !bnf) ? mmad_gemm_splitk(Mp, Np, K, dtype, epi) : 1;
+  ep.splitk = (ep.sk_slab && ep.sk_ctl && !bnf && !ep.tile_flag) ? mmad_gemm_splitk(Mp, Np, K, dtype, epi) : 1;
+  MMAD_CHECK_ARG(!ep.tile_flag || (epi == GEMM_EPI_BWD_WEIGHT && !ep.ad_p),
+                 "gemm: tile flags only for a dW GEMM without the fused Adam");
   auto allowed = [&](int c) {
     return c >= 0 && c < NCFG && cfg_fits(c, Mp, Np, epi) && (!bnf || coresident(dtype, epi, c, Mp, Np));
   };
@@ -1909,4 +2050,31 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   }
   if (cfg_used) *cfg_used = cfg;
   return launch_cfg(dtype, epi, A, lda, B, ldb, Mp, Np, K, ep, cfg, s);
+}
+
+// the streamed Adam of a flagged dW GEMM launched with tile configuration cfg
+// (ep: ad_* state, tile_flag, bn_err = sticky error word)
+int mmad_adam_stream(int cfg, const float* g, int ld, int Mp, int Np, const GemmEpi& ep_in, int grid,
+                     hipStream_t s) {
+  MMAD_CHECK_ARG(cfg >= 0 && cfg < NCFG && cfg_fits(cfg, Mp, Np, GEMM_EPI_BWD_WEIGHT),
+                 "adam_stream: bad tile configuration %d for %dx%d", cfg, Mp, Np);
+  MMAD_CHECK_ARG(ep_in.tile_flag && ep_in.bn_err && ep_in.ad_p && ep_in.ad_m && ep_in.ad_v,
+                 "adam_stream: missing flags / state");
+  const int BM = CFG_BM[cfg], BN = CFG_BN[cfg];
+  const int tiles_m = Mp / BM, tiles_n = Np / BN, ntiles = tiles_m * tiles_n;
+  GemmEpi ep = ep_in;
+  ep.tiles_n = tiles_n;
+  ep.group_m = plan_group_m(ntiles, tiles_m, BM, BN);
+  grid = grid < 8 ? 8 : grid / 8 * 8;
+  if (grid > (ntiles + 7) / 8 * 8) grid = (ntiles + 7) / 8 * 8;
+  switch (BM * 1000 + BN) {
+    case 64064: mmad_adam_stream_kernel<64, 64><<<grid, 256, 0, s>>>(g, ld, ep, ntiles); break;
+    case 64128: mmad_adam_stream_kernel<64, 128><<<grid, 256, 0, s>>>(g, ld, ep, ntiles); break;
+    case 128128: mmad_adam_stream_kernel<128, 128><<<grid, 256, 0, s>>>(g, ld, ep, ntiles); break;
+    case 256128: mmad_adam_stream_kernel<256, 128><<<grid, 256, 0, s>>>(g, ld, ep, ntiles); break;
+    case 128256: mmad_adam_stream_kernel<128, 256><<<grid, 256, 0, s>>>(g, ld, ep, ntiles); break;
+    default: mmad_set_error("adam_stream: tile %dx%d", BM, BN); return MMAD_EUNSUPPORTED;
+  }
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
 }

@@ -58,6 +58,7 @@ int mmad_pad_granule(void);
  * faster), knob 13 = that kernel's grid cap (256 workgroups), knob 14 = load
  * the Adam state of a 64x64 Adam-fused dW tile under its K loop (1) or after it
  * (0, default: measured faster, 32.9 vs 36.6 us for the largest c2 layer),
+ * knob 15 = non-temporal loads/stores of that Adam state (MMAD_ADAM_NT),
  * knob 5 = tile of the dW GEMMs with the fused Adam epilogue (default 3 =
  * 64x64; -1 = autotuned like the others), knobs 6 / 7 = tile of the bwd-data /
  * forward GEMMs (-1 = autotuned), knob 8 = tile of the Adam-fused dW GEMMs
