@@ -99,16 +99,27 @@ struct mmad_ae {
   // fused step, layers < dw_main (the main-stream tail): the dW GEMM without
   // Adam publishing each fp32 tile (tile flags) and the streamed Adam
   // (mmad_adam_stream_kernel) consuming the tiles as they complete on the tail
-  // stream, so the tile's K loop and the Adam state stream overlap instead of
-  // running one after the other in the same waves (MMAD_ADAM_STREAM; grid
-  // MMAD_ADAM_STREAM_GRID workgroups, at most one per CU)
+  // stream, so the tile's K loop and the Adam state stream could overlap
+  // instead of running one after the other in the same waves (MMAD_ADAM_STREAM;
+  // grid MMAD_ADAM_STREAM_GRID workgroups, at most two per CU).  Off by
+  // default: measured slower at every tile / grid (c2 0.473-0.487 vs 0.448
+  // ms/step, c3 1.03-1.11 vs 0.998; profiles/r02bf_*): beside the Adam stream
+  // the latency-bound dW K loop slows down (layer 0: 39.6 us vs ~20 alone),
+  // so the pair takes longer than the fused kernel (46-50 vs 33 us)
   int adam_stream = [] {
     const char* e = getenv("MMAD_ADAM_STREAM");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   int adam_stream_grid = [] {
     const char* e = getenv("MMAD_ADAM_STREAM_GRID");
-    return e ? atoi(e) : 256;
+    return e ? atoi(e) : 512;
+  }();
+  // tile of the flagged dW GEMM: 64x64 by default, so its 2-3 waves of
+  // blocks hand tiles over progressively (a one-wave grid of large tiles
+  // finishes every tile at once and leaves nothing to overlap); -1 = autotuned
+  int adam_stream_tile = [] {
+    const char* e = getenv("MMAD_ADAM_STREAM_TILE");
+    return e ? atoi(e) : 3;
   }();
   int mse_tiles = 0;   // loss partials written by the last MSE GEMM
   // data parallelism: RCCL communicator (not owned), its stream and events
@@ -934,9 +945,11 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
         // on the main stream, the weight Adam streamed beside it on the tail
         // stream, started when the GEMM is (bwd-data(l), which read W_l, is
         // before it on the main stream)
-        GemmEpi e = dwe;
-        fill_adam(e, l, false);
+        GemmEpi e = dwe;          // (dwe carries the weight tile's Adam terms: drop them)
+        e.ad_p = e.ad_m = e.ad_v = nullptr;
+        e.ad_shadow = nullptr;
         e.tile_flag = s.tflag;
+        e.tile_force = h->adam_stream_tile + 1;
         e.dw_nostore = 0;
         const bool prb = PROBE_DW + l == h->probe_id && !h->capturing &&
                          2 * h->probe_n < (int)h->probe_ev.size();

@@ -2065,7 +2065,9 @@ int mmad_adam_stream(int cfg, const float* g, int ld, int Mp, int Np, const Gemm
   GemmEpi ep = ep_in;
   ep.tiles_n = tiles_n;
   ep.group_m = plan_group_m(ntiles, tiles_m, BM, BN);
-  grid = grid < 8 ? 8 : grid / 8 * 8;
+  // at most two 256-thread workgroups per CU (no LDS): the GEMM's blocks,
+  // which it waits for, must always find room beside it
+  grid = grid < 8 ? 8 : (grid > 512 ? 512 : grid / 8 * 8);
   if (grid > (ntiles + 7) / 8 * 8) grid = (ntiles + 7) / 8 * 8;
   switch (BM * 1000 + BN) {
     case 64064: mmad_adam_stream_kernel<64, 64><<<grid, 256, 0, s>>>(g, ld, ep, ntiles); break;
