@@ -7,6 +7,17 @@
 #include "mmad_ops.h"
 
 #define SLAB_COLS 64
+// launch-shape knobs (measurement only): MMAD_FOLD_RPT = 64-row groups of
+// consumer rows per bn_fold_k block (2 or 4), MMAD_BNB_PU = partial chunks per
+// group loaded at once by bn_bwd_apply_k (8; 16 = the default above 32 chunks)
+static const int g_fold_rpt = [] {
+  const char* e = getenv("MMAD_FOLD_RPT");
+  return e ? atoi(e) : 2;
+}();
+static const int g_bnb_pu = [] {
+  const char* e = getenv("MMAD_BNB_PU");
+  return e ? atoi(e) : 16;
+}();
 #define SLAB_ROWS 128
 
 namespace {
@@ -175,8 +186,7 @@ __global__ __launch_bounds__(64) void bn_finalize_k(int M, int N, int Np, const 
 // Welford merge is recomputed per n-block: 16 KB of L2 reads) and the
 // 64 * FOLD_RPT consumer rows n0.. of W.  Merge order: 4 chunk groups
 // (g, g+4, ...) each sequential, then groups 0..3 in order.
-#define FOLD_RPT 2
-template <typename TW>
+template <typename TW, int FOLD_RPT>
 __global__ __launch_bounds__(256) void bn_fold_k(int M, int N, int Np, const float* __restrict__ stats,
                                                  int nparts, const float* __restrict__ gamma,
                                                  const float* __restrict__ beta, float* rmean,
@@ -346,7 +356,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(int M, int Np, const T* _
 // 64-column x 128-row slab; sums from the bwd-data GEMM epilogue partials.
 // Every global load (dy, a, the column constants, the partials) is issued
 // before the first use, so a block costs one memory round trip, not four.
-template <typename T>
+template <typename T, int PU>
 __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int M, int N, int Np,
                                                       int nparts, const T* __restrict__ dy,
                                                       const T* __restrict__ a,
@@ -360,7 +370,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
   constexpr int CPR = SLAB_COLS / V;      // threads per row
   constexpr int RG = 256 / CPR;           // row groups
   constexpr int RPT = SLAB_ROWS / RG;     // rows per thread
-  constexpr int PU = 8;                   // partial chunks per group loaded at once
+  // PU: partial chunks per group loaded at once (16 from 2048 rows: one round
+  // trip for all of a 4096-row batch's 64 chunks; same summation order)
   __shared__ double s_red[RG][SLAB_COLS];
   __shared__ double s_p1[4][SLAB_COLS], s_p2[4][SLAB_COLS];
   const int n0 = blockIdx.x * SLAB_COLS, r0 = blockIdx.y * SLAB_ROWS, tid = threadIdx.x;
@@ -879,17 +890,22 @@ int mmad_bn_finalize_fold(int dtype, int M, int N, int Mp, int Np, const float* 
                           void* wout, float* cpart, void* stream) {
   MMAD_CHECK_ARG(Mp % 128 == 0 && Np % 128 == 0 && Nc_p % 64 == 0 && M >= 1 && M <= Mp && N <= Np,
                  "bn_finalize_fold: bad sizes");
-  MMAD_CHECK_ARG(Nc_p % (64 * FOLD_RPT) == 0, "bn_finalize_fold: consumer rows not a multiple of 128");
-  dim3 grd(Np / 64, Nc_p / (64 * FOLD_RPT));
+  MMAD_CHECK_ARG(Nc_p % 128 == 0, "bn_finalize_fold: consumer rows not a multiple of 128");
+  // consumer rows per block: 64 * rpt (the Welford merge is recomputed per
+  // block, so fewer, taller blocks read fewer partials)
+  const int rpt = (g_fold_rpt == 4 && Nc_p % 256 == 0) ? 4 : 2;
+  dim3 grd(Np / 64, Nc_p / (64 * rpt));
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == MMAD_BF16)
-    bn_fold_k<bf16><<<grd, 256, 0, s>>>(M, N, Np, stats, Mp / MMAD_PART_ROWS, gamma, beta,
-                                        running_mean, running_var, momentum, eps, save_mean,
-                                        save_rstd, scale, shift, W, (bf16*)wout, cpart, Nc_p);
-  else
-    bn_fold_k<float><<<grd, 256, 0, s>>>(M, N, Np, stats, Mp / MMAD_PART_ROWS, gamma, beta,
-                                         running_mean, running_var, momentum, eps, save_mean,
-                                         save_rstd, scale, shift, W, (float*)wout, cpart, Nc_p);
+#define MMAD_FOLD(TW_, R_)                                                                        \
+  bn_fold_k<TW_, R_><<<grd, 256, 0, s>>>(M, N, Np, stats, Mp / MMAD_PART_ROWS, gamma, beta,       \
+                                         running_mean, running_var, momentum, eps, save_mean,    \
+                                         save_rstd, scale, shift, W, (TW_*)wout, cpart, Nc_p);
+  if (dtype == MMAD_BF16) {
+    if (rpt == 4) { MMAD_FOLD(bf16, 4) } else { MMAD_FOLD(bf16, 2) }
+  } else {
+    if (rpt == 4) { MMAD_FOLD(float, 4) } else { MMAD_FOLD(float, 2) }
+  }
+#undef MMAD_FOLD
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
 }
@@ -920,14 +936,22 @@ int mmad_bn_act_bwd_apply(int dtype, int act, float slope, int M, int N, int Mp,
                           void* stream) {
   dim3 grd(Np / SLAB_COLS, Mp / SLAB_ROWS);
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == MMAD_BF16)
-    bn_bwd_apply_k<bf16><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const bf16*)dy,
-                                             (const bf16*)a, save_mean, save_rstd, gamma, part,
-                                             (bf16*)dz, dgamma, dbeta, db_partials);
-  else
-    bn_bwd_apply_k<float><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const float*)dy,
-                                              (const float*)a, save_mean, save_rstd, gamma, part,
-                                              (float*)dz, dgamma, dbeta, db_partials);
+  const bool wide = nparts > 4 * 8 && g_bnb_pu != 8;
+#define MMAD_BNB(PU_)                                                                              \
+  if (dtype == MMAD_BF16)                                                                          \
+    bn_bwd_apply_k<bf16, PU_><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const bf16*)dy,   \
+                                                  (const bf16*)a, save_mean, save_rstd, gamma, part, \
+                                                  (bf16*)dz, dgamma, dbeta, db_partials);          \
+  else                                                                                             \
+    bn_bwd_apply_k<float, PU_><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const float*)dy, \
+                                                   (const float*)a, save_mean, save_rstd, gamma,   \
+                                                   part, (float*)dz, dgamma, dbeta, db_partials);
+  if (wide) {
+    MMAD_BNB(16)
+  } else {
+    MMAD_BNB(8)
+  }
+#undef MMAD_BNB
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
 }
@@ -947,13 +971,13 @@ int mmad_bn_act_bwd(int dtype, int act, float slope, int M, int N, int Mp, int N
   if (dtype == MMAD_BF16) {
     bn_bwd_reduce_k<bf16><<<grd, 256, 0, s>>>(M, Np, (const bf16*)dy, (const bf16*)a, save_mean,
                                               save_rstd, part);
-    bn_bwd_apply_k<bf16><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const bf16*)dy,
+    bn_bwd_apply_k<bf16, 8><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const bf16*)dy,
                                              (const bf16*)a, save_mean, save_rstd, gamma, part,
                                              (bf16*)dz, dgamma, dbeta, db_partials);
   } else {
     bn_bwd_reduce_k<float><<<grd, 256, 0, s>>>(M, Np, (const float*)dy, (const float*)a, save_mean,
                                                save_rstd, part);
-    bn_bwd_apply_k<float><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const float*)dy,
+    bn_bwd_apply_k<float, 8><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const float*)dy,
                                               (const float*)a, save_mean, save_rstd, gamma, part,
                                               (float*)dz, dgamma, dbeta, db_partials);
   }
