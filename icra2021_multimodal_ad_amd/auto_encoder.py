@@ -332,6 +332,9 @@ class AutoEncoder(AbstractModel):
                 x = x.cuda(engine.config.gpu_id)
             x = x.view(x.size(0), -1)
             _, loss = model._native.forward(x, train_bn=False, want_xhat=False, want_loss=True)
+            if model.dist is not None:
+                # data parallel: the whole batch's sum-MSE = sum of the shards'
+                model.dist.all_reduce_sum(loss)
         loss = float(loss)
         model._native.check_status()
         return (loss,)

@@ -88,23 +88,35 @@ class BatchLoader:
     """torch DataLoader(dataset, batch_size, sampler, num_workers=0) over a
     device-resident dataset: each batch is one gather of the sampler's
     indices, ``(x [B, D] on the data's device, y [B] float32 on the host)``;
-    the last batch may be short (drop_last=False)."""
+    the last batch may be short (drop_last=False).
 
-    def __init__(self, dataset, batch_size, sampler):
+    Data parallel (world > 1): every rank draws the same sampler order (same
+    seed), a global batch is ``batch_size * world`` windows and this rank gets
+    its contiguous rows of it (dist.shard_rows), so the ranks together step
+    through exactly the single-process sequence of windows."""
+
+    def __init__(self, dataset, batch_size, sampler, rank=0, world=1):
         self.dataset = dataset
         self.batch_size = int(batch_size)
         self.sampler = sampler
+        self.rank, self.world = int(rank), int(world)
 
     def __iter__(self):
         order = np.fromiter(iter(self.sampler), dtype=np.int64, count=len(self.sampler))
         dev = self.dataset.data.device
-        for s in range(0, len(order), self.batch_size):
-            idx = order[s:s + self.batch_size]
+        gb = self.batch_size * self.world
+        for s in range(0, len(order), gb):
+            idx = order[s:s + gb]
+            if self.world > 1:
+                q, r = divmod(len(idx), self.world)
+                lo = self.rank * q + min(self.rank, r)
+                idx = idx[lo:lo + q + (1 if self.rank < r else 0)]
             yield (self.dataset.data[torch.from_numpy(idx).to(dev)],
                    self.dataset.targets[torch.from_numpy(idx)])
 
     def __len__(self):
-        return (len(self.sampler) + self.batch_size - 1) // self.batch_size
+        gb = self.batch_size * self.world
+        return (len(self.sampler) + gb - 1) // gb
 
 
 class SyntheticWindowDataset:
@@ -193,16 +205,18 @@ class TabularDatasetManager:
         ds = data_loader.dataset
         return ds.data[torch.from_numpy(idx).to(ds.data.device)], ds.targets[torch.from_numpy(idx)]
 
-    def get_loaders(self, batch_size, ratios=None, indexes_list=None, use_gpu=False):
-        """utils/data_loaders.py:554-598."""
+    def get_loaders(self, batch_size, ratios=None, indexes_list=None, use_gpu=False, rank=0, world=1):
+        """utils/data_loaders.py:554-598 (rank / world: data-parallel shards
+        of every batch, BatchLoader)."""
         if ratios and indexes_list:
             raise Exception("Only either `ratios` or `indexes_list` is allowed")
         elif ratios:
             indexes_list = self.get_indexes(ratios=ratios)
         loaders = [BatchLoader(self.train_dataset, batch_size,
-                               SubsetRandomSampler(indexes_list[0], seed=self.sampler_seed))]
+                               SubsetRandomSampler(indexes_list[0], seed=self.sampler_seed), rank, world)]
         for ix in indexes_list[1:3]:
-            loaders.append(BatchLoader(self.train_dataset, batch_size, SequentialIndicesSampler(ix)))
+            loaders.append(BatchLoader(self.train_dataset, batch_size, SequentialIndicesSampler(ix),
+                                       rank, world))
         return loaders
 
 
@@ -223,8 +237,8 @@ def split_labels(config, use_full_class=False):
     return seen, unseen
 
 
-def get_loaders(config, use_full_class=False, device=None):
-    """utils/data_loaders.py:50-138."""
+def get_loaders(config, use_full_class=False, device=None, rank=0, world=1):
+    """utils/data_loaders.py:50-138 (rank / world: data-parallel batch shards)."""
     if config.data not in DATA_CONFIG:
         raise ValueError("no dataset config for" + config.data)
     if device is None:
@@ -246,5 +260,5 @@ def get_loaders(config, use_full_class=False, device=None):
                                            len(u[0]) / max(len(u[0]) + len(s[2]), 1)))
         indexes_list = [s[0], s[1], list(s[2]) + list(u[0])]
     train, valid, test = dset_manager.get_loaders(batch_size=config.batch_size,
-                                                  indexes_list=indexes_list)
+                                                  indexes_list=indexes_list, rank=rank, world=world)
     return dset_manager, train, valid, test

@@ -15,11 +15,43 @@ Two exchange paths:
   the backward -- then Adam-updated there; biases/gamma/beta + the loss follow
   in one small bucket.  One host call per step, no host sync.
 * torch (gloo / fallback): train_fwd_bwd, then one torch.distributed
-  all-reduce of the flat gradient buffer, then the flat Adam."""
+  all-reduce of the flat gradient buffer, then the flat Adam.
+
+Around the step (NoveltyDetecter under data parallelism): each
+rank trains on its rows of every global batch (data_loaders.BatchLoader with
+rank / world), validation losses are summed over the ranks so every rank
+keeps the same best-on-valid state, BatchNorm running statistics are averaged
+at every epoch end, and scoring is sharded by rows with the per-window scores
+all-gathered (shard_rows / gather_rows) before AUROC."""
 import os
 
 import torch
 import torch.distributed as dist
+
+
+def shard_rows(n, rank, world):
+    """Contiguous row range [lo, hi) of `rank`'s shard of n rows: the first
+    n % world ranks take one row more (rank order = row order)."""
+    q, r = divmod(int(n), int(world))
+    lo = rank * q + min(rank, r)
+    return lo, lo + q + (1 if rank < r else 0)
+
+
+def gather_rows(local, n, group=None):
+    """All-gather row shards cut by shard_rows back into the [n, ...] tensor
+    (rank order), on every rank.  Shards are padded to the largest for the
+    collective (all_gather needs equal sizes) and trimmed after."""
+    world = dist.get_world_size(group)
+    m = -(-int(n) // world)
+    pad = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[:local.shape[0]] = local
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad, group=group)
+    out = []
+    for r in range(world):
+        lo, hi = shard_rows(n, r, world)
+        out.append(parts[r][:hi - lo])
+    return torch.cat(out, dim=0)
 
 
 def init_from_env(backend=None):
@@ -113,6 +145,30 @@ class DataParallel:
     def all_reduce_loss(self, loss):
         if self.world > 1:
             dist.all_reduce(loss, op=dist.ReduceOp.SUM, group=self.group)
+
+    def all_reduce_sum(self, t):
+        """In-place sum over ranks (validation losses: the reference's
+        sum-MSE of the whole batch is the sum of the shard losses)."""
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def average_running_stats(self, model):
+        """BatchNorm running mean / var averaged over the ranks (SURVEY
+        §8(e): statistics are per shard while training, averaged for eval;
+        called at every epoch end before validation)."""
+        if self.world > 1:
+            run = model._native.running
+            dist.all_reduce(run, op=dist.ReduceOp.SUM, group=self.group)
+            run.div_(self.world)
+
+    def shard(self, x):
+        """This rank's contiguous row shard of x (shard_rows)."""
+        lo, hi = shard_rows(x.shape[0], dist.get_rank(self.group), self.world)
+        return x[lo:hi]
+
+    def gather(self, local, n):
+        return gather_rows(local, n, self.group) if self.world > 1 else local
 
     def broadcast_params(self, model, src=0):
         if self.world > 1:

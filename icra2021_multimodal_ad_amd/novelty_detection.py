@@ -16,6 +16,14 @@ per-window squared-diff sums, the diffs never materialised), NAP from the
 device diffs (mmad_ae_score) through the native NAP run; the metrics by the
 native rank/threshold kernels (metric.py).  Train diffs are scored in batches
 of ``config.batch_size`` and valid/test in 698 (:36-38, get_diffs' default).
+
+Data parallel (model.dist set by dist.attach_data_parallel):
+the loaders hand each rank its rows of every global batch, validation losses
+are summed over the ranks (every rank keeps the same best-on-valid state),
+BatchNorm running statistics are averaged over the ranks at every epoch end
+before validation, and scoring is sharded by rows with the per-window scores
+(and the NAP fit's train diffs) all-gathered, so every rank reports the
+single-process metrics.
 """
 from copy import deepcopy
 
@@ -57,24 +65,32 @@ class NoveltyDetecter:
         n = len(widths)
         start = getattr(cfg, "start_layer_index", 0)
         end = cfg.n_layers + 1 - getattr(cfg, "end_layer_index", -1)   # novelty_detection.py:57
+        dp = model.dist if getattr(model, "dist", None) is not None and model.dist.world > 1 else None
+
+        def rows(fn, x):
+            # per-window rows of fn(x): this rank's shard, all-gathered (DP)
+            if dp is None:
+                return fn(x)
+            return dp.gather(fn(dp.shard(x)), x.shape[0])
+
         out = {}
         with torch.no_grad():
-            lv = _layer_sq(model, valid_x, 698)
-            lt = _layer_sq(model, test_x, 698)
+            # [n_layers+1, N] per-layer sums, gathered along the windows
+            lv = rows(lambda v: _layer_sq(model, v, 698).t().contiguous(), valid_x).t()
+            lt = rows(lambda v: _layer_sq(model, v, 698).t().contiguous(), test_x).t()
             out["base"] = (base_from_layer_sq(lv, widths), base_from_layer_sq(lt, widths))
             out["sap"] = (sap_from_layer_sq(lv, widths, start, end), sap_from_layer_sq(lt, widths, start, end))
             nap = NapScorer(model, start_layer_index=start, end_layer_index=end)
-            dtr = _device_diffs(model, train_x, cfg.batch_size)
             cuts = np.cumsum([0] + widths)
             sel = slice(int(cuts[nap.sel.start]), int(cuts[min(nap.sel.stop, n)]))
-            nap_train = dtr[:, sel]
+            nap_train = rows(lambda v: _device_diffs(model, v, cfg.batch_size)[:, sel].contiguous(), train_x)
             path = getattr(cfg, "train_diffs", None)
-            if path:
+            if path and (dp is None or torch.distributed.get_rank(dp.group) == 0):
                 torch.save(nap_train.cpu(), path)           # utils/metric.py:205
             nap = NapScorer.standalone(nap_train.shape[1], device=nat.device).fit(train_diffs=nap_train)
-            del dtr
-            out["nap"] = (nap.score(_device_diffs(model, valid_x, 698)[:, sel]),
-                          nap.score(_device_diffs(model, test_x, 698)[:, sel]))
+            del nap_train
+            out["nap"] = (rows(lambda v: nap.score(_device_diffs(model, v, 698)[:, sel]), valid_x),
+                          rows(lambda v: nap.score(_device_diffs(model, v, 698)[:, sel]), test_x))
         return out
 
     def test(self, model, dset_manager, train_loader, valid_loader, test_loader, df_test=None):
@@ -128,6 +144,10 @@ class NoveltyDetecter:
         def run_validation(engine, evaluator, valid_loader):
             evaluator.run(valid_loader, max_epochs=1)
 
+        if getattr(model, "dist", None) is not None:
+            # data parallel: per-shard BN running statistics averaged for eval
+            trainer.add_event_handler(Events.EPOCH_COMPLETED,
+                                      lambda engine: model.dist.average_running_stats(model))
         trainer.add_event_handler(Events.EPOCH_COMPLETED, run_validation, evaluator, valid_loader)
 
         @trainer.on(Events.EPOCH_COMPLETED)
@@ -151,15 +171,20 @@ class NoveltyDetecter:
 
 
 def main(config):
-    """novelty_detection.py:177-211 on the synthetic dataset."""
+    """novelty_detection.py:177-211 on the synthetic dataset (one process per
+    GPU under torchrun: data parallel, dist.attach_data_parallel)."""
+    from . import dist as mdist
     from .data_loaders import get_input_size, get_loaders
     from .model_builder import get_model
     if getattr(config, "input_size", None) is None:
         config.input_size = get_input_size(config)
+    rank, world, _ = mdist.init_from_env()
     model = get_model(config)
+    if world > 1:
+        mdist.attach_data_parallel(model)
     detecter = NoveltyDetecter(config)
-    dset_manager, train_loader, valid_loader, test_loader = get_loaders(config)
+    dset_manager, train_loader, valid_loader, test_loader = get_loaders(config, rank=rank, world=world)
     _, _, _, model = detecter.train(model, train_loader, valid_loader)
-    if getattr(config, "saved_name", None):
+    if getattr(config, "saved_name", None) and rank == 0:
         torch.save(model.state_dict(), config.saved_name)
     return detecter.test(model, dset_manager, train_loader, valid_loader, test_loader)[:3]

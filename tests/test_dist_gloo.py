@@ -71,3 +71,59 @@ def test_two_rank_gradient_allreduce():
         np.testing.assert_allclose(flat, shard_sum, rtol=1e-5, atol=1e-5)
         assert loss == 3.0
         assert np.all(params == 0.0)
+
+
+def _shard_worker(rank, world, port, out):
+    """Row sharding + all-gather of per-window scores, BatchLoader rank
+    shards, running-statistics averaging: the pieces of the data-parallel
+    NoveltyDetecter (dist.py, data_loaders.BatchLoader) on CPU tensors."""
+    import types
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from icra2021_multimodal_ad_amd import dist as mdist
+    from icra2021_multimodal_ad_amd.data_loaders import get_loaders
+    mdist.init_from_env(backend="gloo")
+    dp = mdist.DataParallel(native=False)
+    res = {}
+    for n in (7, 8, 1001):
+        x = torch.arange(n * 3, dtype=torch.float32).view(n, 3)
+        res[f"gather{n}"] = dp.gather(dp.shard(x) * 2.0, n).numpy()
+    # running statistics: rank r holds r + 1 everywhere -> mean over ranks
+    stub = types.SimpleNamespace(_native=types.SimpleNamespace(running=torch.full((6,), float(rank + 1))))
+    dp.average_running_stats(stub)
+    res["running"] = stub._native.running.numpy()
+    cfg = types.SimpleNamespace(data="hsr_objectdrop", target_class=1, unimodal_normal=False,
+                                novelty_ratio=0.0, batch_size=64, input_size=16, n_normal=500,
+                                n_novelty=100, data_seed=3, gpu_id=-1)
+    _, tr, va, _ = get_loaders(cfg, device="cpu", rank=rank, world=world)
+    res["train"] = [xb.numpy() for xb, _ in tr]
+    res["valid"] = [xb.numpy() for xb, _ in va]
+    out[rank] = res
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharding_gather_and_loaders():
+    import types
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_shard_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for n in (7, 8, 1001):
+        ref = np.arange(n * 3, dtype=np.float32).reshape(n, 3) * 2.0
+        for r in range(world):
+            np.testing.assert_array_equal(out[r][f"gather{n}"], ref)
+    for r in range(world):
+        np.testing.assert_array_equal(out[r]["running"], np.full(6, 1.5, np.float32))
+    # the ranks' batches together are the single-process batches of 2 x 64
+    # windows, in order (same sampler permutation on every rank)
+    from icra2021_multimodal_ad_amd.data_loaders import get_loaders
+    cfg = types.SimpleNamespace(data="hsr_objectdrop", target_class=1, unimodal_normal=False,
+                                novelty_ratio=0.0, batch_size=128, input_size=16, n_normal=500,
+                                n_novelty=100, data_seed=3, gpu_id=-1)
+    _, tr, va, _ = get_loaders(cfg, device="cpu")
+    for name, loader in (("train", tr), ("valid", va)):
+        single = [xb.numpy() for xb, _ in loader]
+        assert len(single) == len(out[0][name]) == len(out[1][name])
+        for i, xb in enumerate(single):
+            np.testing.assert_array_equal(np.concatenate([out[0][name][i], out[1][name][i]]), xb)

@@ -157,3 +157,67 @@ def test_native_exchange_schedule_loopback(dtype):
         ma._native.set_comm(None)
     finally:
         lib.mmad_comm_destroy(h)
+
+
+def _nd_cfg():
+    return types.SimpleNamespace(input_size=192, btl_size=16, n_layers=5, gpu_id=0, dtype="f32",
+                                 models="ae", batch_size=64, n_epochs=2, n_normal=700, n_novelty=140,
+                                 anomaly_strength=0.7, data="hsr_objectdrop", target_class=1,
+                                 unimodal_normal=False, novelty_ratio=0.0, start_layer_index=0,
+                                 end_layer_index=-1, data_seed=5, sampler_seed=6, verbose=0)
+
+
+def _nd_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    import torch.distributed as dist
+    from icra2021_multimodal_ad_amd import dist as mdist
+    from icra2021_multimodal_ad_amd.data_loaders import get_loaders
+    from icra2021_multimodal_ad_amd.novelty_detection import NoveltyDetecter
+    mdist.init_from_env(backend="gloo")
+    torch.cuda.set_device(0)
+    m = _model()
+    mdist.attach_data_parallel(m)
+    cfg = _nd_cfg()
+    det = NoveltyDetecter(cfg)
+    dset, tr, va, te = get_loaders(cfg, rank=rank, world=world)
+    th, vh, _, m = det.train(m, tr, va)
+    res = det.test(m, dset, tr, va, te)
+    out[rank] = dict(params=m._native.params.cpu().numpy(), running=m._native.running.cpu().numpy(),
+                     vh=list(vh), best=det.best_epoch, res=[list(r) for r in res[:3]],
+                     scores={k: (v.copy(), t.copy()) for k, (v, t) in det.last_scores.items()},
+                     sd={k: v.cpu().numpy() for k, v in m.state_dict().items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_novelty_detecter_two_ranks():
+    """NoveltyDetecter.train / test under data parallelism (2 ranks sharing
+    cuda:0 over gloo): each rank trains on its rows of every global batch,
+    validation losses are summed over the ranks, BN running statistics
+    averaged at every epoch end, scoring sharded by rows and all-gathered.
+    Both ranks must end with the same parameters, running statistics,
+    best-on-valid epoch and metrics, and the gathered per-window BASE / SAP /
+    NAP scores must equal a single process scoring the final model."""
+    world = 2
+    mgr = mp.get_context("spawn").Manager()
+    out = mgr.dict()
+    mp.start_processes(_nd_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+                       start_method="spawn")
+    a, b = out[0], out[1]
+    assert np.array_equal(a["params"], b["params"])
+    assert np.array_equal(a["running"], b["running"])
+    assert a["best"] == b["best"] and a["vh"] == b["vh"] and a["res"] == b["res"]
+    from icra2021_multimodal_ad_amd.data_loaders import get_loaders
+    from icra2021_multimodal_ad_amd.novelty_detection import NoveltyDetecter
+    m = _model()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in a["sd"].items()})
+    cfg = _nd_cfg()
+    det = NoveltyDetecter(cfg)
+    dset, tr, va, te = get_loaders(cfg)
+    for _ in range(cfg.n_epochs):       # the train sampler's state after training (same train_x order)
+        list(iter(tr.sampler))
+    det.test(m, dset, tr, va, te)
+    for k, (v, t) in det.last_scores.items():
+        np.testing.assert_allclose(a["scores"][k][0], v, rtol=1e-5, atol=1e-7, err_msg=k)
+        np.testing.assert_allclose(a["scores"][k][1], t, rtol=1e-5, atol=1e-7, err_msg=k)
