@@ -190,6 +190,23 @@ __device__ __forceinline__ floatx4 frag_f32(const char* img, int rbase, int kc, 
   }
 }
 
+// main-loop schedule variants (build-time, measurement): 0 = every phase
+// pinned by sched_barrier(0) (default); 1 = compiler-scheduled phases; 2 = 1
+// + s_setprio(1) around each MFMA half; 3 = 0 + s_setprio
+#ifndef MMAD_LOOP_VARIANT
+#define MMAD_LOOP_VARIANT 0
+#endif
+#if MMAD_LOOP_VARIANT == 1 || MMAD_LOOP_VARIANT == 2
+#define MMAD_SB() do { } while (0)
+#else
+#define MMAD_SB() __builtin_amdgcn_sched_barrier(0)
+#endif
+#if MMAD_LOOP_VARIANT >= 2
+#define MMAD_PRIO(x) __builtin_amdgcn_s_setprio(x)
+#else
+#define MMAD_PRIO(x) do { } while (0)
+#endif
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -518,12 +535,16 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
     auto step = [&](int t, auto issue_c, auto last_c) {
       constexpr bool ISSUE = decltype(issue_c)::value, LAST = decltype(last_c)::value;
       const char* sa = smem + (t % NS) * SLOT;
+      MMAD_PRIO(1);
       mma_half<T, TM, TN, 0>(acc, f0a, f0b);
-      __builtin_amdgcn_sched_barrier(0);
+      MMAD_PRIO(0);
+      MMAD_SB();
       read_sub<T, AK, BK_, NAT, BM, BN, TM, TN>(sa, sa + IA::BYTES, ra, rb, 1, lane, f1a, f1b);
-      __builtin_amdgcn_sched_barrier(0);
+      MMAD_SB();
+      MMAD_PRIO(1);
       mma_half<T, TM, TN, 1>(acc, f0a, f0b);
-      __builtin_amdgcn_sched_barrier(0);
+      MMAD_PRIO(0);
+      MMAD_SB();
       if constexpr (!LAST) {
         if constexpr (ISSUE) {
           if (APF_OK && apf && t <= NS - 2) wait_vmcnt<(NS - 2) * NL + APF>();
@@ -534,17 +555,21 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
         wait_lgkm0();
         block_barrier();                     // stage t+1 visible; slot t free
         if constexpr (ISSUE) issue(t + NS);
-        __builtin_amdgcn_sched_barrier(0);
+        MMAD_SB();
       }
+      MMAD_PRIO(1);
       mma_half<T, TM, TN, 0>(acc, f1a, f1b);
-      __builtin_amdgcn_sched_barrier(0);
+      MMAD_PRIO(0);
+      MMAD_SB();
       if constexpr (!LAST) {
         const char* sn = smem + ((t + 1) % NS) * SLOT;
         read_sub<T, AK, BK_, NAT, BM, BN, TM, TN>(sn, sn + IA::BYTES, ra, rb, 0, lane, f0a, f0b);
       }
-      __builtin_amdgcn_sched_barrier(0);
+      MMAD_SB();
+      MMAD_PRIO(1);
       mma_half<T, TM, TN, 1>(acc, f1a, f1b);
-      __builtin_amdgcn_sched_barrier(0);
+      MMAD_PRIO(0);
+      MMAD_SB();
     };
     using T_ = std::true_type;
     using F_ = std::false_type;
