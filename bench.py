@@ -178,18 +178,26 @@ def gemm_roofline(model, batch, iters=50):
             "timing": f"{iters} back-to-back launches between one HIP event pair"}
 
 
-def dw_roofline(nat, layer, durations_ms, batch, steps_timed, fused_adam=True):
-    """roofline of the dominant dW GEMM from the in-situ probe durations."""
+def dw_roofline(nat, layer, durations_ms, batch, steps_timed, fused_adam=True, layers=None):
+    """roofline of the dominant dW GEMM launch from the in-situ probe durations.
+    layers: the layers that launch covered (mmad_ae_probe_layers: the
+    main-stream tail runs layers 1 and 0 as one pair launch)."""
     import statistics
-    L = nat.layers[layer]
+    layers = sorted(layers or [layer], reverse=True)
     rows = batch                      # k = 1: decoder rows = encoder rows
     es = 2 if nat.dtype_name == "bf16" else 4
+    nbytes, flops = 0, 0.0
+    for l in layers:
+        L = nat.layers[l]
+        if fused_adam:
+            nbytes += dw_adam_bytes(L["N"], L["K"], rows, es)
+        else:
+            nbytes += 4 * L["N"] * L["K"] + es * rows * (L["N"] + L["K"])
+        flops += 2.0 * rows * L["N"] * L["K"]
     if fused_adam:
-        nbytes = dw_adam_bytes(L["N"], L["K"], rows, es)
         what = "bwd-weight + fused Adam"
         body = "p/m/v fp32 + bf16 shadow updated in the epilogue"
     else:
-        nbytes = 4 * L["N"] * L["K"] + es * rows * (L["N"] + L["K"])
         what = "bwd-weight"
         body = "fp32 dW written for the all-reduce; Adam runs after the exchange"
     avg_s = statistics.fmean(durations_ms) / 1e3
@@ -197,15 +205,20 @@ def dw_roofline(nat, layer, durations_ms, batch, steps_timed, fused_adam=True):
     wl = {"dim": nat.enc_widths[0], "batch": batch, "dtype": nat.dtype_name,
           "model": "vib_ae" if nat.vib else "ae", "layer": layer}
     pmc, src = _pmc_file("dw", wl)
-    return {"kernel": f"mmad_gemm_kernel {what} (layer {layer}: dW[{L['N']}x{L['K']}] = "
-                      f"dz^T a over {rows} windows; {body})",
+    if len(layers) > 1:
+        wl["layers"] = layers
+        pmc, src = _pmc_file("dw", wl)
+    shapes = ", ".join(f"layer {l}: dW[{nat.layers[l]['N']}x{nat.layers[l]['K']}]" for l in layers)
+    kern = "mmad_gemm_pair_kernel" if len(layers) > 1 else "mmad_gemm_kernel"
+    return {"kernel": f"{kern} {what} ({shapes} = dz^T a over {rows} windows"
+                      f"{'; both layers in one launch' if len(layers) > 1 else ''}; {body})",
             "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4),
             "traffic": pmc["traffic_bytes_per_launch"] if pmc else None,
             "traffic_source": src,
             "avg_us": round(avg_s * 1e6, 2), "launches_timed": len(durations_ms),
             "algorithmic_bytes_per_launch": nbytes,
-            "flops_per_launch": 2.0 * rows * L["N"] * L["K"],
+            "flops_per_launch": flops,
             "timing": f"executor probe: HIP event pair around this launch on its stream, in "
                       f"{steps_timed} eager steps right after the timed region"}
 
@@ -337,7 +350,7 @@ def run(args):
                                    "ms_per_step": round(e1 / n1 * 1e3, 4), "steps": n1,
                                    "how": "same ranks, exchange off, after the timed region (max over ranks)"}
         model.dist = mdl_dist
-    durs, n_probe = [], 0
+    durs, n_probe, probe_layers = [], 0, None
     if not args.no_probe and rank == 0:
         # the timed steps replay one captured hipGraph each, so the dominant
         # kernel is timed by the executor's probe on EAGER steps of the same
@@ -356,6 +369,8 @@ def run(args):
         if n < 0:
             _native.check(n, "mmad_ae_probe_read")
         durs = list(buf[:n])
+        mask = lib.mmad_ae_probe_layers(nat._h)
+        probe_layers = [l for l in range(len(nat.layers)) if mask > 0 and (mask >> l) & 1] or [probe_layer]
         _native.check(lib.mmad_ae_probe(nat._h, 1, -1, 0), "mmad_ae_probe")
         nat.use_graph = graph_mode
     res["train_step"] = ("one captured hipGraph replay per step (mmad_ae_train_step_graph)"
@@ -364,7 +379,8 @@ def run(args):
     if rank == 0:
         if durs:
             fused = model.dist is None or not model.dist.native
-            res["roofline"] = dw_roofline(nat, probe_layer, durs, batch, n_probe, fused_adam=fused)
+            res["roofline"] = dw_roofline(nat, probe_layer, durs, batch, n_probe, fused_adam=fused,
+                                          layers=probe_layers)
         res["roofline_encoder_gemm"] = gemm_roofline(model, batch)
         if not args.no_cpu_baseline and world == 1:   # host baseline: rank 0 at N=1 only
             res["cpu_baseline"] = cpu_baseline(dim, batch, vib, budget_s=args.cpu_budget)

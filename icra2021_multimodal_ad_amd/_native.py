@@ -78,6 +78,7 @@ SIGNATURES = {
     "mmad_ae_status": (_I, [_P, _P, _I64, _P]),
     "mmad_ae_probe": (_I, [_P, _I, _I, _I]),
     "mmad_ae_probe_read": (_I, [_P, ctypes.POINTER(_F), _I]),
+    "mmad_ae_probe_layers": (_I, [_P]),
     "mmad_ae_graph_count": (_I, [_P]),
     "mmad_ae_clear_graphs": (_I, [_P]),
     "mmad_comm_unique_id_bytes": (_I, []),

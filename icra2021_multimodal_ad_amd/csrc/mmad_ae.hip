@@ -121,6 +121,17 @@ struct mmad_ae {
     const char* e = getenv("MMAD_ADAM_STREAM_TILE");
     return e ? atoi(e) : 3;
   }();
+  // fused step, dw_main == 2: the Adam-fused dW GEMMs of layers 1 and 0 (the
+  // main-stream tail) as ONE launch of two problems (mmad_gemm_pair_kernel)
+  // when both use the same tile, so the second problem's blocks fill the
+  // first one's last partial wave (MMAD_DW_PAIR=1).  Bit-identical, but
+  // neutral as measured (c2 58 us for the pair vs 33 + 25 separately, c3 110
+  // vs 60 + 52; profiles/r02bp_*): the blocks already backfill freed slots
+  // across the two launches, so off by default
+  int dw_pair = [] {
+    const char* e = getenv("MMAD_DW_PAIR");
+    return e ? atoi(e) : 0;
+  }();
   int mse_tiles = 0;   // loss partials written by the last MSE GEMM
   // data parallelism: RCCL communicator (not owned), its stream and events
   mmad_comm* comm = nullptr;
@@ -179,6 +190,7 @@ struct mmad_ae {
   // the step, on the stream it is launched on (bench roofline, in situ)
   mutable int probe_id = -1;
   mutable int probe_n = 0;
+  mutable unsigned probe_mask = 0;    // layers the last probed launch covered (bit l)
   std::vector<hipEvent_t> probe_ev;   // [2 * capacity]: start, end pairs
   // hipGraph-captured fused train steps (mmad_ae_train_step_graph): one per
   // call signature, replayed after a host->device copy of the per-call values
@@ -588,6 +600,7 @@ static int ae_gemm(const mmad_ae* h, const AeWS& w, int dt, int epi, const void*
   if (rec) {
     MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n + 1], s));
     ++h->probe_n;
+    h->probe_mask = 1u << (probe % 64);
   }
   return MMAD_OK;
 }
@@ -747,6 +760,8 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
   hipStream_t side = h->side;
   std::vector<PendingDW> pending;   // side-stream dW GEMMs waiting for a recorded event
   bool used_tail = false;
+  PendingDW pair_first{};           // main-tail dW of layer 1, launched with layer 0's
+  bool pair_pending = false;
   // layer l's Adam terms for a dW epilogue: the weight tile's (ad_*, unless
   // weights_too is false) and the small segment [bias | gamma | beta]'s
   auto fill_adam = [&](GemmEpi& e, int l, bool weights_too) {
@@ -972,8 +987,39 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
         used_tail = true;
       } else if (on_main) {
         dwe.tile_force = mmad_tile_adam_main_override() + 1;
-        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st,
-                       nullptr, PROBE_DW + l));
+        // the tile each of the two tail problems would get on its own
+        auto tail_cfg = [&](int M_, int N_, int K_) {
+          return mmad_gemm_adam_dw_cfg(M_, N_, K_, dwe.tile_force);
+        };
+        if (h->dw_pair && h->dw_main == 2 && l == 1 && !h->capturing) {
+          pair_first = PendingDW{dz, in, a.Np, a.Kp, a.Np, a.Kp, Mp, dwe, l};
+          pair_pending = true;
+        } else if (pair_pending && l == 0 &&
+                   tail_cfg(pair_first.M, pair_first.N, pair_first.K) == tail_cfg(a.Np, a.Kp, Mp) &&
+                   tail_cfg(a.Np, a.Kp, Mp) >= 0) {
+          const int cfg = tail_cfg(a.Np, a.Kp, Mp);
+          const bool prb = (PROBE_DW + 0 == h->probe_id || PROBE_DW + 1 == h->probe_id) &&
+                           !h->capturing && 2 * h->probe_n < (int)h->probe_ev.size();
+          if (prb) MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n], st));
+          RET_IF(mmad_gemm_dispatch_pair(dt, cfg, pair_first.dz, pair_first.lda, pair_first.in,
+                                         pair_first.ldb, pair_first.M, pair_first.N, pair_first.K,
+                                         pair_first.ep, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st));
+          if (prb) {
+            MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n + 1], st));
+            ++h->probe_n;
+            h->probe_mask = 3u;
+          }
+          pair_pending = false;
+        } else {
+          if (pair_pending) {
+            RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, pair_first.dz, pair_first.lda, pair_first.in,
+                           pair_first.ldb, pair_first.M, pair_first.N, pair_first.K, pair_first.ep, st,
+                           nullptr, PROBE_DW + pair_first.layer));
+            pair_pending = false;
+          }
+          RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st,
+                         nullptr, PROBE_DW + l));
+        }
       } else if (ping) {
         MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
@@ -991,7 +1037,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       }
     }
   }
-  MMAD_CHECK_ARG(pending.empty(), "ae backward: deferred dW GEMMs left unissued");
+  MMAD_CHECK_ARG(pending.empty() && !pair_pending, "ae backward: deferred dW GEMMs left unissued");
   // join the side (and tail) streams back into the main stream
   MMAD_HIP_CHECK(hipEventRecord(h->ev_join, side));
   MMAD_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
@@ -1423,12 +1469,15 @@ int mmad_ae_probe(mmad_ae* h, int kind, int layer, int capacity) {
   h->probe_ev.clear();
   h->probe_n = 0;
   h->probe_id = -1;
+  h->probe_mask = 0;
   if (layer < 0 || capacity == 0) return MMAD_OK;
   h->probe_ev.resize(2 * (size_t)capacity, nullptr);
   for (auto& e : h->probe_ev) MMAD_HIP_CHECK(hipEventCreate(&e));
   h->probe_id = (kind == 0 ? PROBE_FWD : PROBE_DW) + layer;
   return MMAD_OK;
 }
+
+int mmad_ae_probe_layers(const mmad_ae* h) { return h ? (int)h->probe_mask : -1; }
 
 int mmad_ae_probe_read(mmad_ae* h, float* ms, int max_n) {
   if (!h || !ms || max_n < 0) {

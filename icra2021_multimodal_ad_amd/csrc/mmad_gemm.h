@@ -174,5 +174,12 @@ bool mmad_gemm_bn_fusable(int dtype, int epi, int Mp, int Np);
 // stream AFTER the GEMM; grid rounded to a multiple of 8, <= one block per CU)
 int mmad_adam_stream(int cfg, const float* g, int ld, int Mp, int Np, const GemmEpi& ep, int grid,
                      hipStream_t s);
+// tile configuration of an Adam-fused dW GEMM under the static rules (-1: autotuned)
+int mmad_gemm_adam_dw_cfg(int Mp, int Np, int K, int tile_force);
+// two Adam-fused / plain dW GEMMs (EPI_BWD_WEIGHT) in one launch, tile configuration cfg
+int mmad_gemm_dispatch_pair(int dtype, int cfg, const void* A0, int lda0, const void* B0, int ldb0,
+                            int Mp0, int Np0, int K0, const GemmEpi& e0, const void* A1, int lda1,
+                            const void* B1, int ldb1, int Mp1, int Np1, int K1, const GemmEpi& e1,
+                            hipStream_t s);
 int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,
                        int Np, int K, const GemmEpi& ep, hipStream_t s, int* cfg_used = nullptr);

@@ -359,10 +359,12 @@ __device__ __forceinline__ bool mmad_apf_on(const GemmEpi& ep) { return ep.apf &
 // dW GEMM contracts the raw activation and fixes up in the epilogue
 // (dW = scale[k] * acc + shift[k] * db[n]).  Every GEMM is a plain MFMA
 // contraction.
+// The body of one output tile; `bid` / `nblk` = this problem's block index /
+// block count (mmad_gemm_kernel: the grid; mmad_gemm_pair_kernel: its share).
 template <typename T, typename TO, bool AK, bool BK_, int CFG, int EPI>
-__global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __restrict__ A, int lda,
-                                                           const T* __restrict__ B, int ldb, int K,
-                                                           GemmEpi ep) {
+__device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, const T* __restrict__ B,
+                                          int ldb, int K, const GemmEpi& ep, const int bid,
+                                          const int nblk) {
   using C = Cfg<CFG>;
   constexpr int BM = C::BM, BN = C::BN, WM = C::WM, WN = C::WN, NS = C::NS, NT = C::NT;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;   // 16x16 MFMA tiles per wave
@@ -399,7 +401,6 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   // at a time so every XCD works on a compact rectangle whose A/B panels stay
   // in its L2.
   const int S = ep.splitk > 1 ? ep.splitk : 1;
-  const int nblk = gridDim.x, bid = blockIdx.x;
   const int ntl = nblk / S;                 // output tiles
   int tm, tn, tile, sk;
   {
@@ -1297,6 +1298,34 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   }
 }
 
+template <typename T, typename TO, bool AK, bool BK_, int CFG, int EPI>
+__global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __restrict__ A, int lda,
+                                                           const T* __restrict__ B, int ldb, int K,
+                                                           GemmEpi ep) {
+  gemm_body<T, TO, AK, BK_, CFG, EPI>(A, lda, B, ldb, K, ep, blockIdx.x, gridDim.x);
+}
+
+// Two independent problems of one epilogue and tile configuration in ONE
+// launch: blocks [0, n0) run problem 0, the rest problem 1 (the main-stream
+// tail's two Adam-fused dW GEMMs: one grid, so the second problem's blocks
+// fill the first one's last partial wave, and one launch less).  Each
+// problem keeps its own XCD-aware tile order and partial-sum orders, so the
+// results are those of two separate launches bit for bit.
+struct GemmPairArgs {
+  const void *A0, *B0, *A1, *B1;
+  int lda0, ldb0, K0, lda1, ldb1, K1, n0;
+  GemmEpi ep0, ep1;
+};
+template <typename T, typename TO, bool AK, bool BK_, int CFG, int EPI>
+__global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_pair_kernel(GemmPairArgs p) {
+  if ((int)blockIdx.x < p.n0)
+    gemm_body<T, TO, AK, BK_, CFG, EPI>((const T*)p.A0, p.lda0, (const T*)p.B0, p.ldb0, p.K0, p.ep0,
+                                        blockIdx.x, p.n0);
+  else
+    gemm_body<T, TO, AK, BK_, CFG, EPI>((const T*)p.A1, p.lda1, (const T*)p.B1, p.ldb1, p.K1, p.ep1,
+                                        blockIdx.x - p.n0, gridDim.x - p.n0);
+}
+
 // -------------------------------------------------------------------------
 // dW GEMM + fused Adam, warp-specialised and persistent (bf16 operands).
 //
@@ -2104,4 +2133,69 @@ int mmad_adam_stream(int cfg, const float* g, int ld, int Mp, int Np, const Gemm
   }
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
+}
+
+// Two dW GEMMs (EPI_BWD_WEIGHT, no split, no tile flags) in one launch with
+// tile configuration cfg: mmad_gemm_pair_kernel
+int mmad_gemm_dispatch_pair(int dtype, int cfg, const void* A0, int lda0, const void* B0, int ldb0,
+                            int Mp0, int Np0, int K0, const GemmEpi& e0, const void* A1, int lda1,
+                            const void* B1, int ldb1, int Mp1, int Np1, int K1, const GemmEpi& e1,
+                            hipStream_t s) {
+  MMAD_CHECK_ARG(dtype == MMAD_BF16 || dtype == MMAD_F32, "gemm_pair: bad dtype %d", dtype);
+  MMAD_CHECK_ARG(cfg >= 0 && cfg < NCFG && cfg_fits(cfg, Mp0, Np0, GEMM_EPI_BWD_WEIGHT) &&
+                     cfg_fits(cfg, Mp1, Np1, GEMM_EPI_BWD_WEIGHT),
+                 "gemm_pair: tile configuration %d does not fit both problems", cfg);
+  MMAD_CHECK_ARG(K0 % 128 == 0 && K1 % 128 == 0 && K0 > 0 && K1 > 0, "gemm_pair: bad K");
+  MMAD_CHECK_ARG(!e0.tile_flag && !e1.tile_flag && !e0.bn_sync && !e1.bn_sync,
+                 "gemm_pair: plain dW epilogues only");
+  GemmPairArgs p{};
+  p.A0 = A0; p.B0 = B0; p.lda0 = lda0; p.ldb0 = ldb0; p.K0 = K0;
+  p.A1 = A1; p.B1 = B1; p.lda1 = lda1; p.ldb1 = ldb1; p.K1 = K1;
+  const int BM = CFG_BM[cfg], BN = CFG_BN[cfg];
+  auto prep = [&](GemmEpi& ep, const GemmEpi& in, int Mp, int Np) {
+    ep = in;
+    ep.dbg = mmad_dbg_override();
+    ep.apf = mmad_adam_prefetch_enabled();
+    ep.ad_nt = mmad_adam_nt_enabled();
+    ep.splitk = 1;
+    const int tm = Mp / BM, tn = Np / BN;
+    ep.tiles_n = tn;
+    ep.group_m = plan_group_m(tm * tn, tm, BM, BN);
+    return tm * tn;
+  };
+  const int n0 = prep(p.ep0, e0, Mp0, Np0);
+  const int n1 = prep(p.ep1, e1, Mp1, Np1);
+  p.n0 = n0;
+  dim3 grd(n0 + n1), blk(CFG_NT[cfg]);
+#define MMAD_PAIR(T_, C_) \
+  mmad_gemm_pair_kernel<T_, float, false, false, C_, GEMM_EPI_BWD_WEIGHT><<<grd, blk, 0, s>>>(p); break;
+#define MMAD_PAIR_T(T_)        \
+  switch (cfg) {               \
+    case 0: MMAD_PAIR(T_, 0)   \
+    case 1: MMAD_PAIR(T_, 1)   \
+    case 2: MMAD_PAIR(T_, 2)   \
+    case 3: MMAD_PAIR(T_, 3)   \
+    case 4: MMAD_PAIR(T_, 4)   \
+    default: MMAD_PAIR(T_, 5)  \
+  }
+  if (dtype == MMAD_BF16) {
+    MMAD_PAIR_T(bf16)
+  } else {
+    MMAD_PAIR_T(float)
+  }
+#undef MMAD_PAIR_T
+#undef MMAD_PAIR
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+// the tile configuration mmad_gemm_dispatch gives an Adam-fused dW GEMM of
+// this shape with this tile_force (-1: not decided by the static rules --
+// autotuned or the warp-specialised kernel -- so not predictable here)
+int mmad_gemm_adam_dw_cfg(int Mp, int Np, int K, int tile_force) {
+  if (mmad_dw_ws_enabled()) return -1;
+  auto fits = [&](int c) { return c >= 0 && c < NCFG && cfg_fits(c, Mp, Np, GEMM_EPI_BWD_WEIGHT); };
+  if (fits(tile_force - 1)) return tile_force - 1;
+  const int e = mmad_tile_adam_for(Mp, Np, K);
+  return fits(e) ? e : -1;
 }

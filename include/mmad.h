@@ -411,6 +411,10 @@ int mmad_ae_status(mmad_ae* h, void* ws, int64_t ws_bytes, void* stream);
  * max_n durations (ms) in call order; returns how many (or < 0). */
 int mmad_ae_probe(mmad_ae* h, int kind, int layer, int capacity);
 int mmad_ae_probe_read(mmad_ae* h, float* ms, int max_n);
+/* Layers (bit l) the last probed launch covered: one layer, or layers 0 and 1
+ * when the main-stream tail ran its two Adam-fused dW GEMMs as one launch
+ * (mmad_gemm_pair_kernel, MMAD_DW_PAIR). */
+int mmad_ae_probe_layers(const mmad_ae* h);
 
 /* number of cached score graphs (-1 for a null handle); drop them all */
 int mmad_ae_graph_count(const mmad_ae* h);

@@ -54,3 +54,36 @@ def test_streamed_adam_matches_fused_epilogue(monkeypatch, rows, dtype, models):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
     if dtype == "bf16":
         assert torch.equal(a.shadow, b.shadow)
+
+
+@pytest.mark.parametrize("rows,dtype,models", [(1024, "bf16", "ae"), (4096, "bf16", "vib_ae"),
+                                               (256, "f32", "ae")])
+def test_tail_pair_launch_matches_two_launches(monkeypatch, rows, dtype, models):
+    """The main-stream tail's two Adam-fused dW GEMMs as one launch
+    (mmad_gemm_pair_kernel, MMAD_DW_PAIR=1) against two launches
+    (MMAD_DW_PAIR=0): each problem keeps its own tile order and partial-sum
+    orders, so everything must agree bit for bit over several steps."""
+    import types
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    ms = []
+    for pair in ("1", "0"):
+        monkeypatch.setenv("MMAD_DW_PAIR", pair)
+        cfg = types.SimpleNamespace(input_size=2048, btl_size=100, n_layers=5, gpu_id=0, dtype=dtype,
+                                    models=models, vib_k=1, beta_kl=1.0)
+        torch.manual_seed(4)
+        ms.append(get_model(cfg))
+    ms[1].load_state_dict(ms[0].state_dict())
+    for m in ms:
+        m._native.sync_shadow(force=True)
+    for s in range(3):
+        x = torch.from_numpy(synth_windows(rows, 2048, seed=70 + s)).cuda()
+        eps = torch.randn(rows, 100, device="cuda") if models == "vib_ae" else None
+        la, lb = (float(m._native.train_step_fused(x, eps=eps)) for m in ms)
+        assert la == lb, (s, la, lb)
+    for m in ms:
+        m._native.check_status()
+    a, b = ms[0]._native, ms[1]._native
+    for name in ("params", "exp_avg", "exp_avg_sq", "running"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    if dtype == "bf16":
+        assert torch.equal(a.shadow, b.shadow)
