@@ -67,6 +67,11 @@ struct mmad_ae {
   hipStream_t side = nullptr;
   std::vector<hipEvent_t> ev_fork, ev_data;
   hipEvent_t ev_join = nullptr;
+  hipEvent_t ev_loss = nullptr;   // fused step: forward done -> the loss reduction on the side stream
+  int loss_side = [] {            // MMAD_LOSS_SIDE=0: reduce the loss at the end of the main stream
+    const char* e = getenv("MMAD_LOSS_SIDE");
+    return e ? atoi(e) : 1;
+  }();
   // tail stream (MMAD_DW_TAIL=1): the main-stream dW GEMMs of layers
   // 1 .. dw_main-1 run here instead, concurrently with the end of the chain
   int dw_tail = [] {
@@ -226,6 +231,7 @@ struct mmad_ae {
     for (auto e : ev_fork) (void)hipEventDestroy(e);
     for (auto e : ev_data) (void)hipEventDestroy(e);
     if (ev_join) (void)hipEventDestroy(ev_join);
+    if (ev_loss) (void)hipEventDestroy(ev_loss);
     for (auto e : ev_dw) (void)hipEventDestroy(e);
     if (ev_small) (void)hipEventDestroy(ev_small);
     if (ev_cdone) (void)hipEventDestroy(ev_cdone);
@@ -496,6 +502,7 @@ int mmad_ae_bind(mmad_ae* h, float* params, float* grads, float* adam_m, float* 
       MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_data[i], kEvFlags));
     }
     MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_join, kEvFlags));
+    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_loss, kEvFlags));
     MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_tail, kEvFlags));
   }
   return MMAD_OK;
@@ -1123,12 +1130,24 @@ int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const
   hipStream_t st = (hipStream_t)stream;
   const AdamHyper ah = adam_hyper(lr, beta1, beta2, adam_eps, step);
   RET_IF(run_forward(h, w, x, ld_x, 0, eps, seed, offset, st));
-  RET_IF(run_backward(h, w, true, beta_kl, &ah, st));
-  if (!h->comm) {
+  if (!h->comm && !h->loss_side) {
+    RET_IF(run_backward(h, w, true, beta_kl, &ah, st));
     RET_IF(finish_reductions(h, w, false, true, beta_kl, loss_out, st));
     if (h->shadow_alt) std::swap(h->shadow, h->shadow_alt);
     return MMAD_OK;
   }
+  if (!h->comm) {
+    // the loss needs only the forward's MSE (and KL) partials: reduce it on
+    // the side stream now, off the main stream's tail (the backward joins the
+    // side stream back into the caller's before the step ends)
+    MMAD_HIP_CHECK(hipEventRecord(h->ev_loss, st));
+    MMAD_HIP_CHECK(hipStreamWaitEvent(h->side, h->ev_loss, 0));
+    RET_IF(finish_reductions(h, w, false, true, beta_kl, loss_out, h->side));
+    RET_IF(run_backward(h, w, true, beta_kl, &ah, st));
+    if (h->shadow_alt) std::swap(h->shadow, h->shadow_alt);
+    return MMAD_OK;
+  }
+  RET_IF(run_backward(h, w, true, beta_kl, &ah, st));
   // data parallel tail: bias grads + loss, then one small bucket
   // [all bias | gamma | beta grads] + the loss, its Adam, join
   RET_IF(finish_reductions(h, w, true, true, beta_kl, loss_out, st));
