@@ -149,6 +149,18 @@ struct mmad_ae {
     const char* e = getenv("MMAD_DW_MAIN");
     return e ? atoi(e) : 2;   // tools/sched_sweep.py: 0.499 ms (2) vs 0.512 (1) vs 0.523 (3)
   }();
+  // ping-pong schedule per call from this many padded rows (bf16 with a
+  // shadow pair; MMAD_SHADOW_PAIR_ROWS), with dw_main_ping main-stream dW
+  // GEMMs (MMAD_DW_MAIN_PING): VIB B=4096 0.941-0.945 vs 0.995-0.999 ms/step,
+  // B=1024 0.450-0.455 vs 0.442-0.449 (profiles/r02bu_*, r02bv_*)
+  int pair_rows = [] {
+    const char* e = getenv("MMAD_SHADOW_PAIR_ROWS");
+    return e ? atoi(e) : 4096;
+  }();
+  int dw_main_ping = [] {
+    const char* e = getenv("MMAD_DW_MAIN_PING");
+    return e ? atoi(e) : 1;
+  }();
   int keep_grads = [] {
     const char* e = getenv("MMAD_KEEP_GRADS");
     return e ? atoi(e) : 0;
@@ -180,7 +192,7 @@ struct mmad_ae {
   // GEMMs of the layers in between wait for the next recorded one
   int ev_every = [] {
     const char* e = getenv("MMAD_EV_EVERY");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 2;   // c2 0.435-0.440 vs 0.442-0.444 with 1 (profiles/r02bv_*)
   }();
   // hipGraph cache for mmad_ae_score_stream: one captured graph per
   // (input, output, workspace, N, batch) pass, replayed with one launch
@@ -203,6 +215,7 @@ struct mmad_ae {
   struct TrainGraph {
     int B, k, ld_x, xvec, has_eps, dw_main, ev_every, keep_grads;
     const void* ws;
+    const void* shadow;   // the bf16 shadow the captured kernels read / write
     float beta_kl, b1, b2, aeps;
     hipGraphExec_t exec;
   };
@@ -271,6 +284,11 @@ struct AeWS {
   size_t sk_ctl_bytes;   // both split-K control blocks + the fused-BN counters
   unsigned* bn_err;      // fused-BN barrier timeout word
   int bn_mode;           // this call's train-mode BN schedule (0 apply, 1 fold, 2 fused)
+  // this call's fused-step schedule: ping-pong the bf16 weight shadows (the
+  // Adam of layer l writes the shadow the NEXT step reads, so dW_l waits only
+  // for dz_l) and how many of the last dW GEMMs run on the main stream
+  bool ping = false;
+  int dw_main = 2;
   std::vector<LayerWS> l;
   int64_t bytes;
 };
@@ -526,9 +544,9 @@ int mmad_ae_sync_shadow(mmad_ae* h, void* stream) {
 }
 
 // the shadow the fused step's Adam writes (bf16 only)
-static void* adam_shadow(const mmad_ae* h, const AeLayer& a) {
+static void* adam_shadow(const mmad_ae* h, const AeLayer& a, bool ping) {
   if (h->dtype != MMAD_BF16) return nullptr;
-  return (char*)(h->shadow_alt ? h->shadow_alt : h->shadow) + a.w_off * 2;
+  return (char*)(ping && h->shadow_alt ? h->shadow_alt : h->shadow) + a.w_off * 2;
 }
 
 // ---------------------------------------------------------------------------
@@ -574,6 +592,8 @@ static int prepare_ws(const mmad_ae* h, int B, int k, void* ws, int64_t ws_bytes
   // when this handle first sees it (and mmad_ae_status re-zeroes after a
   // timed-out combine); only when a split can be chosen at all
   w.bn_mode = h->bn_mode;
+  w.ping = false;
+  w.dw_main = h->dw_main;
   if (w.bn_mode == 2 && w.Mpd > h->bn_fused_rows) w.bn_mode = h->fold ? 1 : 0;
   if (w.bn_mode == 1 && !h->fold) w.bn_mode = 0;
   if ((splitk_possible(h->dtype) || h->bn_mode == 2 || h->adam_stream) && ws != h->ws_zeroed) {
@@ -778,7 +798,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       e.ad_p = h->params + a.w_off;
       e.ad_m = h->m + a.w_off;
       e.ad_v = h->v + a.w_off;
-      e.ad_shadow = adam_shadow(h, a);
+      e.ad_shadow = adam_shadow(h, a, w.ping);
       // the gradient is consumed by the fused Adam in registers; materialise
       // it only when asked (h->keep_grads)
       e.dw_nostore = h->keep_grads ? 0 : 1;
@@ -806,7 +826,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     const int64_t n = (int64_t)a.Np * a.Kp;
     return mmad_adam_dyn(n, h->params + a.w_off, h->grads + a.w_off, h->m + a.w_off, h->v + a.w_off,
                          adam->b1, adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt,
-                         adam_shadow(h, a), h->dtype == MMAD_BF16 ? n : 0, w.dyn, s_);
+                         adam_shadow(h, a, w.ping), h->dtype == MMAD_BF16 ? n : 0, w.dyn, s_);
   };
   for (int l = nL - 1; l >= 0; --l) {
     const AeLayer& a = h->L[l];
@@ -832,21 +852,21 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     const bool dp = adam && h->comm;
     // ping-pong shadows (bf16): the fused Adam of dW_l writes the other
     // shadow, so dW_l may start as soon as dz_l is complete
-    const bool ping = adam && !dp && h->shadow_alt && l >= h->dw_main;
+    const bool ping = adam && !dp && w.ping && l >= w.dw_main;
     if (ping) {
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
     }
     // does the main stream record ev_data[l] (bwd-data of l done)?  Needed by
     // the DP exchange and by side-stream dW GEMMs (every ev_every-th layer;
     // the lowest side layer always records, flushing the deferred ones)
-    const bool side_dw = adam && !dp && !ping && l >= h->dw_main;
-    const bool split = adam && !dp && !ping && h->tail && l < h->dw_main &&
+    const bool side_dw = adam && !dp && !ping && l >= w.dw_main;
+    const bool split = adam && !dp && !ping && h->tail && l < w.dw_main &&
                        (h->dw_split > 0 || (h->dw_split < 0 && w.Mpe >= 4096));
     const bool tail_dw = adam && !dp && !ping && !split && h->tail && h->dw_tail && l > 0 &&
-                         l < h->dw_main;
+                         l < w.dw_main;
     const bool rec = dp || tail_dw || split ||
-                     (side_dw && (h->ev_every <= 1 || l == h->dw_main ||
-                                  (l - h->dw_main) % h->ev_every == 0));
+                     (side_dw && (h->ev_every <= 1 || l == w.dw_main ||
+                                  (l - w.dw_main) % h->ev_every == 0));
     if (!adam || dp) {
       // fork: dz_l is complete on the main stream; dW_l overlaps the chain below
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
@@ -930,7 +950,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       RET_IF(mmad_allreduce_bucket(h->comm, h->grads + a.w_off, n, h->cstream));
       RET_IF(mmad_adam(n, h->params + a.w_off, h->grads + a.w_off, h->m + a.w_off, h->v + a.w_off,
                        adam->b1, adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt,
-                       adam_shadow(h, a), h->dtype == MMAD_BF16 ? n : 0, h->cstream));
+                       adam_shadow(h, a, w.ping), h->dtype == MMAD_BF16 ? n : 0, h->cstream));
     } else if (adam) {
       // dW_l with this layer's Adam update fused into its epilogue.  It rewrites
       // W_l, so it starts only once the main stream has finished reading W_l
@@ -955,7 +975,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       fill_adam(dwe, l, true);
       // the last dW GEMMs of the chain go to the main stream, which is idle
       // by then, instead of queueing behind the side stream's backlog
-      const bool on_main = l < h->dw_main;
+      const bool on_main = l < w.dw_main;
       if (tail_dw) {
         dwe.tile_force = mmad_tile_adam_main_override() + 1;
         MMAD_HIP_CHECK(hipStreamWaitEvent(h->tail, h->ev_data[l], 0));
@@ -998,7 +1018,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
         auto tail_cfg = [&](int M_, int N_, int K_) {
           return mmad_gemm_adam_dw_cfg(M_, N_, K_, dwe.tile_force);
         };
-        if (h->dw_pair && h->dw_main == 2 && l == 1 && !h->capturing) {
+        if (h->dw_pair && w.dw_main == 2 && l == 1 && !h->capturing) {
           pair_first = PendingDW{dz, in, a.Np, a.Kp, a.Np, a.Kp, Mp, dwe, l};
           pair_pending = true;
         } else if (pair_pending && l == 0 &&
@@ -1129,11 +1149,14 @@ int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const
   RET_IF(prepare_ws(h, B, k, ws, ws_bytes, w, (hipStream_t)stream));
   hipStream_t st = (hipStream_t)stream;
   const AdamHyper ah = adam_hyper(lr, beta1, beta2, adam_eps, step);
+  // ping-pong schedule (bf16 with a shadow pair, large calls, single process)
+  w.ping = h->shadow_alt && !h->comm && !h->capturing && w.Mpe >= h->pair_rows;
+  if (w.ping) w.dw_main = h->dw_main_ping;
   RET_IF(run_forward(h, w, x, ld_x, 0, eps, seed, offset, st));
   if (!h->comm && !h->loss_side) {
     RET_IF(run_backward(h, w, true, beta_kl, &ah, st));
     RET_IF(finish_reductions(h, w, false, true, beta_kl, loss_out, st));
-    if (h->shadow_alt) std::swap(h->shadow, h->shadow_alt);
+    if (w.ping) std::swap(h->shadow, h->shadow_alt);
     return MMAD_OK;
   }
   if (!h->comm) {
@@ -1144,7 +1167,7 @@ int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const
     MMAD_HIP_CHECK(hipStreamWaitEvent(h->side, h->ev_loss, 0));
     RET_IF(finish_reductions(h, w, false, true, beta_kl, loss_out, h->side));
     RET_IF(run_backward(h, w, true, beta_kl, &ah, st));
-    if (h->shadow_alt) std::swap(h->shadow, h->shadow_alt);
+    if (w.ping) std::swap(h->shadow, h->shadow_alt);
     return MMAD_OK;
   }
   RET_IF(run_backward(h, w, true, beta_kl, &ah, st));
@@ -1161,7 +1184,6 @@ int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const
                    h->cstream));
   MMAD_HIP_CHECK(hipEventRecord(h->ev_cdone, h->cstream));
   MMAD_HIP_CHECK(hipStreamWaitEvent(st, h->ev_cdone, 0));
-  if (h->shadow_alt) std::swap(h->shadow, h->shadow_alt);
   return MMAD_OK;
 }
 
@@ -1173,7 +1195,7 @@ int mmad_ae_train_step_graph(mmad_ae* h, const float* x, int ld_x, int B, int k,
                  "ae_train_step_graph: unbound handle");
   MMAD_CHECK_ARG(x && ld_x >= h->L[0].K && loss_out, "ae_train_step_graph: bad input");
   MMAD_CHECK_ARG(step >= 1, "ae_train_step_graph: step must be >= 1");
-  if (h->comm || h->shadow_alt || h->graph_broken)   // eager schedule for these
+  if (h->comm || h->graph_broken)   // eager schedule for these
     return mmad_ae_train_step(h, x, ld_x, B, k, eps, seed, offset, beta_kl, lr, beta1, beta2,
                               adam_eps, step, loss_out, ws, ws_bytes, stream);
   AeWS w;
@@ -1203,7 +1225,7 @@ int mmad_ae_train_step_graph(mmad_ae* h, const float* x, int ld_x, int B, int k,
   const int xvec = ((uintptr_t)x % 16 == 0 && ld_x % 4 == 0) ? 1 : 0;
   for (auto& g : h->tgraphs) {
     if (g.B == B && g.k == k && g.ld_x == ld_x && g.xvec == xvec && g.has_eps == (eps != nullptr) &&
-        g.ws == ws && g.dw_main == h->dw_main && g.ev_every == h->ev_every &&
+        g.ws == ws && g.shadow == h->shadow && g.dw_main == h->dw_main && g.ev_every == h->ev_every &&
         g.keep_grads == h->keep_grads && g.beta_kl == beta_kl && g.b1 == beta1 && g.b2 == beta2 &&
         g.aeps == adam_eps) {
       MMAD_HIP_CHECK(hipGraphLaunch(g.exec, st));
@@ -1245,7 +1267,7 @@ int mmad_ae_train_step_graph(mmad_ae* h, const float* x, int ld_x, int B, int k,
     h->tgraphs.erase(h->tgraphs.begin());
   }
   h->tgraphs.push_back({B, k, ld_x, xvec, eps != nullptr, h->dw_main, h->ev_every, h->keep_grads, ws,
-                        beta_kl, beta1, beta2, adam_eps, exec});
+                        h->shadow, beta_kl, beta1, beta2, adam_eps, exec});
   return MMAD_OK;
 }
 

@@ -77,10 +77,10 @@ class NativeAE:
         self.exp_avg_sq = torch.zeros(self.n_params, **kw)
         self.running = torch.zeros(2 * self.n_bn, **kw)
         self.running[self.n_bn:] = 1.0
-        # bf16: MMAD_SHADOW_PAIR=1 keeps two weight shadows, ping-ponged by
-        # the fused step (mmad_ae_set_shadow_pair); off by default: the
-        # earlier dW starts steal CUs from the critical bwd-data chain
-        self._pair = self.dt == _native.BF16 and os.environ.get("MMAD_SHADOW_PAIR", "0") == "1"
+        # bf16: two weight shadows (mmad_ae_set_shadow_pair), ping-ponged by
+        # the fused step on large calls (the executor picks per call:
+        # MMAD_SHADOW_PAIR_ROWS); MMAD_SHADOW_PAIR=0 keeps one
+        self._pair = self.dt == _native.BF16 and os.environ.get("MMAD_SHADOW_PAIR", "1") == "1"
         self._shadow_buf = (torch.zeros((2 if self._pair else 1) * self.n_weight, device=device,
                                         dtype=torch.bfloat16)
                             if self.dt == _native.BF16 else None)

@@ -136,16 +136,20 @@ def test_train_step_split_factors_agree(dtype):
         assert cos > (1 - 1e-6 if dtype == "f32" else 0.99), (split, cos)
 
 
-def test_shadow_pair_matches_single_shadow(monkeypatch):
+@pytest.mark.parametrize("pair_rows", ["0", "1000"])
+def test_shadow_pair_matches_single_shadow(monkeypatch, pair_rows):
     """bf16 fused steps with the ping-pong weight shadows (dW+Adam of a layer
     overlapping its bwd-data GEMM) give the same bits as the single-shadow
-    schedule; the current shadow is always bf16(params)."""
+    schedule; the current shadow is always bf16(params).  pair_rows 0: every
+    call ping-pongs; 1000: the executor alternates between the ping-pong
+    schedule (1024-row calls) and the single-shadow one (512-row calls)."""
     import types
     from icra2021_multimodal_ad_amd.model_builder import get_model
     from icra2021_multimodal_ad_amd.common_utils import init_state_dict
     from icra2021_multimodal_ad_amd.data import synth_windows
     sd = init_state_dict(1728, 100, 5, seed=5)
-    xs = [torch.from_numpy(synth_windows(512, 1728, seed=10 + i)).cuda() for i in range(3)]
+    xs = [torch.from_numpy(synth_windows(512 * (1 + i % 2), 1728, seed=10 + i)).cuda() for i in range(4)]
+    monkeypatch.setenv("MMAD_SHADOW_PAIR_ROWS", pair_rows)
     res = {}
     for pair in ("1", "0"):
         monkeypatch.setenv("MMAD_SHADOW_PAIR", pair)
