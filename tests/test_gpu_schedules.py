@@ -1,4 +1,6 @@
-"""Streamed Adam on the main-stream tail of the fused step (MMAD_ADAM_STREAM=1:
+"""Fused-step schedule variants give the same bits as the default schedule.
+
+Streamed Adam on the main-stream tail of the fused step (MMAD_ADAM_STREAM=1:
 layers < MMAD_DW_MAIN run a dW GEMM that publishes each fp32 tile through a
 per-tile flag, and mmad_adam_stream_kernel applies Adam to the tiles as they
 complete, on the tail stream) against the Adam fused into the dW GEMM's
@@ -87,3 +89,43 @@ def test_tail_pair_launch_matches_two_launches(monkeypatch, rows, dtype, models)
         assert torch.equal(getattr(a, name), getattr(b, name)), name
     if dtype == "bf16":
         assert torch.equal(a.shadow, b.shadow)
+
+
+@pytest.mark.parametrize("env", [
+    {"MMAD_EV_EVERY": "1"}, {"MMAD_EV_EVERY": "3"}, {"MMAD_LOSS_SIDE": "0"},
+    {"MMAD_DW_MAIN": "1"}, {"MMAD_DW_MAIN": "3"}, {"MMAD_SHADOW_PAIR_ROWS": "0"},
+    {"MMAD_SHADOW_PAIR_ROWS": "0", "MMAD_DW_MAIN_PING": "0"}, {"MMAD_SHADOW_PAIR": "0"},
+    {"MMAD_SIDE_PRIO": "1"}, {"MMAD_DW_TAIL": "1"}])
+def test_schedule_knobs_match_default(monkeypatch, env):
+    """Every schedule knob of the fused step only reorders independent work
+    across streams (event coalescing, where the loss is reduced, how many dW
+    GEMMs run on the main stream, ping-pong shadows, stream priority, the tail
+    stream): parameters, Adam moments, BN statistics, the current bf16 shadow
+    and the losses equal the default schedule's bit for bit."""
+    import types
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    ms = []
+    for variant in (True, False):
+        for k in env:
+            monkeypatch.delenv(k, raising=False)
+        if variant:
+            for k, v in env.items():
+                monkeypatch.setenv(k, v)
+        cfg = types.SimpleNamespace(input_size=2048, btl_size=100, n_layers=5, gpu_id=0, dtype="bf16",
+                                    models="ae")
+        torch.manual_seed(8)
+        ms.append(get_model(cfg))
+    ms[1].load_state_dict(ms[0].state_dict())
+    for m in ms:
+        m._native.sync_shadow(force=True)
+    for s in range(3):
+        x = torch.from_numpy(synth_windows(1024, 2048, seed=40 + s)).cuda()
+        la, lb = (float(m._native.train_step_fused(x)) for m in ms)
+        assert la == lb, (s, la, lb)
+    for m in ms:
+        m._native.check_status()
+    a, b = ms[0]._native, ms[1]._native
+    for name in ("params", "exp_avg", "exp_avg_sq", "running"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert torch.equal(a.shadow, b.shadow)
+    assert torch.equal(a.shadow, a.params[: a.n_weight].bfloat16())
