@@ -61,7 +61,7 @@ def cpu_baseline(d, budget_s=10.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--windows", type=int, default=1 << 20)
-    ap.add_argument("--batch", type=int, default=16384)
+    ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--dim", type=int, default=2048)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=3)

@@ -35,7 +35,7 @@ def get_diffs(x, model, batch_size=698):
     return [np.concatenate(o, axis=0) for o in out]
 
 
-def score_windows(x, model, batch_size=16384, out=None, graph=True):
+def score_windows(x, model, batch_size=65536, out=None, graph=True):
     """Per-window sum of squared diffs per layer, [n_enc+1, N] fp32 on the
     device.  x: [N, D] tensor.  Resident on the model's device: ONE native call
     for the whole pass (mmad_ae_score_stream), replayed as a captured hipGraph
