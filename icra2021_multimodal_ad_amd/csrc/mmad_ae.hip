@@ -183,6 +183,14 @@ struct mmad_ae {
   // vs 1.32 apply vs 1.27 fold -- more tiles per column, longer barrier
   // waits), fold above; fp32 0 (the parity path).
   int bn_mode = 0;
+  // backward BN schedule override for the bf16 path (MMAD_BN_MODE_BWD: -1 =
+  // the forward's; 2 = fused into the bwd-data GEMMs whatever the forward did:
+  // the fused backward needs only a, the saved mean / rstd and gamma, which
+  // every forward schedule leaves)
+  int bn_mode_bwd = [] {
+    const char* e = getenv("MMAD_BN_MODE_BWD");
+    return e ? atoi(e) : -1;
+  }();
   int bn_fused_rows = [] {
     const char* e = getenv("MMAD_BN_FUSED_MAX_ROWS");
     return e ? atoi(e) : 2048;
@@ -284,6 +292,7 @@ struct AeWS {
   size_t sk_ctl_bytes;   // both split-K control blocks + the fused-BN counters
   unsigned* bn_err;      // fused-BN barrier timeout word
   int bn_mode;           // this call's train-mode BN schedule (0 apply, 1 fold, 2 fused)
+  int bn_mode_bwd;       // ... of the backward (2: fused into the bwd-data GEMMs; else the apply kernel)
   // this call's fused-step schedule: ping-pong the bf16 weight shadows (the
   // Adam of layer l writes the shadow the NEXT step reads, so dW_l waits only
   // for dz_l) and how many of the last dW GEMMs run on the main stream
@@ -596,7 +605,9 @@ static int prepare_ws(const mmad_ae* h, int B, int k, void* ws, int64_t ws_bytes
   w.dw_main = h->dw_main;
   if (w.bn_mode == 2 && w.Mpd > h->bn_fused_rows) w.bn_mode = h->fold ? 1 : 0;
   if (w.bn_mode == 1 && !h->fold) w.bn_mode = 0;
-  if ((splitk_possible(h->dtype) || h->bn_mode == 2 || h->adam_stream) && ws != h->ws_zeroed) {
+  w.bn_mode_bwd = (h->bn_mode_bwd >= 0 && h->fold) ? h->bn_mode_bwd : w.bn_mode;
+  if ((splitk_possible(h->dtype) || h->bn_mode == 2 || h->bn_mode_bwd == 2 || h->adam_stream) &&
+      ws != h->ws_zeroed) {
     MMAD_HIP_CHECK(hipMemsetAsync(w.sk_ctl[0], 0, w.sk_ctl_bytes, st));
     const_cast<mmad_ae*>(h)->ws_zeroed = ws;
   }
@@ -909,7 +920,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
         ep.bn_mean = ps.mean;
         ep.bn_rstd = ps.rstd;
         ep.bn_part = ps.bnpart;
-        ps.bwd_fused = w.bn_mode == 2 && mmad_gemm_bn_fusable(dt, GEMM_EPI_BWD_DATA, Mp, a.Kp);
+        ps.bwd_fused = w.bn_mode_bwd == 2 && mmad_gemm_bn_fusable(dt, GEMM_EPI_BWD_DATA, Mp, a.Kp);
         if (ps.bwd_fused) {
           // BN + activation backward of layer l-1 inside this GEMM: dz directly
           ep.out = nullptr;
@@ -1478,13 +1489,14 @@ int mmad_ae_status(mmad_ae* h, void* ws, int64_t ws_bytes, void* stream) {
   MMAD_CHECK_ARG(h, "ae_status: null handle");
   // no split-K GEMM / fused-BN barrier can have run unless the dtype /
   // override / BN mode allows one
-  if ((!splitk_possible(h->dtype) && h->bn_mode != 2 && !h->adam_stream) || !ws) return MMAD_OK;
+  if ((!splitk_possible(h->dtype) && h->bn_mode != 2 && h->bn_mode_bwd != 2 && !h->adam_stream) || !ws)
+    return MMAD_OK;
   AeWS w;
   carve(h, 1, 1, (char*)ws, w);
   MMAD_CHECK_ARG(ws_bytes >= w.bytes, "ae_status: workspace too small");
   for (int r = 0; r < 2; ++r)
     RET_IF(mmad_gemm_read_status(w.sk_ctl[r], (hipStream_t)stream, "ae_status"));
-  if ((h->bn_mode == 2 || h->adam_stream) && w.bn_err) {
+  if ((h->bn_mode == 2 || h->bn_mode_bwd == 2 || h->adam_stream) && w.bn_err) {
     unsigned word = 0;
     MMAD_HIP_CHECK(hipMemcpyAsync(&word, w.bn_err, sizeof(word), hipMemcpyDeviceToHost, (hipStream_t)stream));
     MMAD_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));

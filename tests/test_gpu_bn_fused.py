@@ -160,3 +160,27 @@ def test_split_tail_matches_fused_tail(monkeypatch, rows):
     for m in ms:
         m._native.check_status()
     assert torch.equal(ms[0]._native.params, ms[1]._native.params)
+
+
+def test_fold_forward_fused_backward_c3_vib(monkeypatch):
+    """MMAD_BN_MODE_BWD=2: the BatchNorm backward fused into the bwd-data
+    GEMMs after a FOLD forward (the fused backward needs only a, the saved
+    mean / rstd and gamma, which bn_fold_k leaves), at the C3 shape through
+    the fused step: finite, within 1 % of the default schedule's loss over 3
+    steps, no barrier timeout."""
+    sd = init_state_dict(2048, 100, 5, seed=16, enc_out=200)
+    monkeypatch.setenv("MMAD_BN_MODE_BWD", "2")
+    ma, _ = _model(2048, 100, 5, sd, dtype="bf16", models="vib_ae", k=1)
+    monkeypatch.delenv("MMAD_BN_MODE_BWD")
+    mb, _ = _model(2048, 100, 5, sd, dtype="bf16", models="vib_ae", k=1)
+    ma._native.sync_shadow(force=True)
+    mb._native.sync_shadow(force=True)
+    eps = torch.randn(1, 4096, 100, device="cuda")
+    for s in range(3):
+        x = torch.from_numpy(synth_windows(4096, 2048, seed=90 + s)).cuda()
+        la = float(ma._native.train_step_fused(x, eps=eps, beta_kl=1.0))
+        lb = float(mb._native.train_step_fused(x, eps=eps, beta_kl=1.0))
+        assert np.isfinite(la)
+        assert abs(la - lb) <= 1e-2 * abs(lb), (s, la, lb)
+    ma._native.check_status()
+    mb._native.check_status()
