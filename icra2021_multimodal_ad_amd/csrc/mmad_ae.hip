@@ -791,8 +791,14 @@ struct PendingDW {
   int layer;
 };
 
+static int finish_reductions(mmad_ae* h, AeWS& w, bool biases, bool from_mse, float beta_kl,
+                             float* loss_out, hipStream_t st);
+
+// dp_loss (data-parallel fused step): the loss output; the bias / gamma / beta
+// bucket and the loss are reduced and exchanged as soon as the backward chain
+// has produced the last bias partials, ahead of layer 0's weight bucket
 static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const AdamHyper* adam,
-                        hipStream_t st) {
+                        hipStream_t st, float* dp_loss = nullptr) {
   const int dt = h->dtype;
   const int nL = (int)h->L.size();
   hipStream_t side = h->side;
@@ -843,6 +849,21 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     const AeLayer& a = h->L[l];
     LayerWS& s = w.l[l];
     const int Mp = prows_of(w, a);
+    if (l == 0 && dp_loss && adam && h->comm) {
+      // data parallel: the last bwd-data (l = 1) has produced every bias
+      // partial, and the loss partials are the forward's: reduce them on the
+      // main stream now and queue the small bucket's exchange + Adam on the
+      // comm stream ahead of layer 0's weight bucket, under its dW GEMM
+      RET_IF(finish_reductions(h, w, true, true, beta_kl, dp_loss, st));
+      MMAD_HIP_CHECK(hipEventRecord(h->ev_small, st));
+      MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_small, 0));
+      const int64_t ns = h->n_params - h->n_weight;
+      RET_IF(mmad_allreduce_bucket(h->comm, h->grads + h->n_weight, ns, h->cstream));
+      RET_IF(mmad_allreduce_bucket(h->comm, dp_loss, 1, h->cstream));
+      RET_IF(mmad_adam(ns, h->params + h->n_weight, h->grads + h->n_weight, h->m + h->n_weight,
+                       h->v + h->n_weight, adam->b1, adam->b2, adam->eps, adam->step_size,
+                       adam->bc2_sqrt, nullptr, 0, h->cstream));
+    }
     const void* dz = (l == nL - 1) ? (from_mse ? s.out : s.dy) : (a.bn ? s.dz : s.dy);
     const float *isc, *ish;
     const void* in = input_of(h, w, l, true, &isc, &ish);
@@ -1181,18 +1202,10 @@ int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const
     if (w.ping) std::swap(h->shadow, h->shadow_alt);
     return MMAD_OK;
   }
-  RET_IF(run_backward(h, w, true, beta_kl, &ah, st));
-  // data parallel tail: bias grads + loss, then one small bucket
-  // [all bias | gamma | beta grads] + the loss, its Adam, join
-  RET_IF(finish_reductions(h, w, true, true, beta_kl, loss_out, st));
-  MMAD_HIP_CHECK(hipEventRecord(h->ev_small, st));
-  MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_small, 0));
-  const int64_t ns = h->n_params - h->n_weight;
-  RET_IF(mmad_allreduce_bucket(h->comm, h->grads + h->n_weight, ns, h->cstream));
-  RET_IF(mmad_allreduce_bucket(h->comm, loss_out, 1, h->cstream));
-  RET_IF(mmad_adam(ns, h->params + h->n_weight, h->grads + h->n_weight, h->m + h->n_weight,
-                   h->v + h->n_weight, ah.b1, ah.b2, ah.eps, ah.step_size, ah.bc2_sqrt, nullptr, 0,
-                   h->cstream));
+  // data parallel: per-layer weight buckets and (ahead of layer 0's) the
+  // small bucket [all bias | gamma | beta grads] + the loss, each with its
+  // Adam, on the comm stream (run_backward); then join
+  RET_IF(run_backward(h, w, true, beta_kl, &ah, st, loss_out));
   MMAD_HIP_CHECK(hipEventRecord(h->ev_cdone, h->cstream));
   MMAD_HIP_CHECK(hipStreamWaitEvent(st, h->ev_cdone, 0));
   return MMAD_OK;

@@ -1,4 +1,4 @@
-# Bias-partial reduction with 32 loads in flight: DP tests (loopback bit-exactness), DP overhead at c2/c4, DP timeline.
+# Small DP bucket queued ahead of layer 0 on the comm stream: DP tests (loopback bit-exactness), DP overhead at c2/c4, DP timeline.
 set -o pipefail
 T=${1:-r02cl}
 mkdir -p gpurun_out && export TMPDIR=/tmp
