@@ -137,6 +137,14 @@ struct mmad_ae {
     const char* e = getenv("MMAD_DW_PAIR");
     return e ? atoi(e) : 0;
   }();
+  // data-parallel step: the small bucket (bias / gamma / beta grads + loss)
+  // goes on the comm stream right after the bwd-data GEMM of this layer
+  // (ahead of this layer's and the lower layers' weight buckets);
+  // MMAD_DP_SMALL_AT, 0 or 1
+  int dp_small_at = [] {
+    const char* e = getenv("MMAD_DP_SMALL_AT");
+    return e ? atoi(e) : 1;
+  }();
   int mse_tiles = 0;   // loss partials written by the last MSE GEMM
   // data parallelism: RCCL communicator (not owned), its stream and events
   mmad_comm* comm = nullptr;
@@ -849,21 +857,6 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     const AeLayer& a = h->L[l];
     LayerWS& s = w.l[l];
     const int Mp = prows_of(w, a);
-    if (l == 0 && dp_loss && adam && h->comm) {
-      // data parallel: the last bwd-data (l = 1) has produced every bias
-      // partial, and the loss partials are the forward's: reduce them on the
-      // main stream now and queue the small bucket's exchange + Adam on the
-      // comm stream ahead of layer 0's weight bucket, under its dW GEMM
-      RET_IF(finish_reductions(h, w, true, true, beta_kl, dp_loss, st));
-      MMAD_HIP_CHECK(hipEventRecord(h->ev_small, st));
-      MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_small, 0));
-      const int64_t ns = h->n_params - h->n_weight;
-      RET_IF(mmad_allreduce_bucket(h->comm, h->grads + h->n_weight, ns, h->cstream));
-      RET_IF(mmad_allreduce_bucket(h->comm, dp_loss, 1, h->cstream));
-      RET_IF(mmad_adam(ns, h->params + h->n_weight, h->grads + h->n_weight, h->m + h->n_weight,
-                       h->v + h->n_weight, adam->b1, adam->b2, adam->eps, adam->step_size,
-                       adam->bc2_sqrt, nullptr, 0, h->cstream));
-    }
     const void* dz = (l == nL - 1) ? (from_mse ? s.out : s.dy) : (a.bn ? s.dz : s.dy);
     const float *isc, *ish;
     const void* in = input_of(h, w, l, true, &isc, &ish);
@@ -969,6 +962,22 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
                                   a.Np, ep, st));
       }
+    }
+    if (dp && dp_loss && l == (nL > h->dp_small_at ? h->dp_small_at : 0)) {
+      // the last bwd-data (l = 1, just enqueued) has produced every bias
+      // partial and the loss partials are the forward's: reduce them on the
+      // main stream now and queue the small bucket's exchange + Adam on the
+      // comm stream ahead of layer 1's and layer 0's weight buckets, so it
+      // runs while their dW GEMMs still compute instead of after them
+      RET_IF(finish_reductions(h, w, true, true, beta_kl, dp_loss, st));
+      MMAD_HIP_CHECK(hipEventRecord(h->ev_small, st));
+      MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_small, 0));
+      const int64_t ns = h->n_params - h->n_weight;
+      RET_IF(mmad_allreduce_bucket(h->comm, h->grads + h->n_weight, ns, h->cstream));
+      RET_IF(mmad_allreduce_bucket(h->comm, dp_loss, 1, h->cstream));
+      RET_IF(mmad_adam(ns, h->params + h->n_weight, h->grads + h->n_weight, h->m + h->n_weight,
+                       h->v + h->n_weight, adam->b1, adam->b2, adam->eps, adam->step_size,
+                       adam->bc2_sqrt, nullptr, 0, h->cstream));
     }
     if (dp) {
       // data parallel: all-reduce dW_l on the comm stream as soon as it is
