@@ -10,6 +10,7 @@ import statistics
 import sys
 
 tag, B, N, K, layer, model = sys.argv[1], *map(int, sys.argv[2:6]), sys.argv[6]
+tile = sys.argv[7] if len(sys.argv) > 7 else "64x64"   # label of the tile dw_one.py ran
 med = {}
 dur = []
 for p in ("fetch", "write", "hit", "mfma"):
@@ -24,7 +25,7 @@ for p in ("fetch", "write", "hit", "mfma"):
         med[n] = statistics.median(v[3:] if len(v) > 6 else v)   # skip the autotune / warm launches
 
 alg = 26 * N * K + 2 * B * (N + K)
-d = {"kernel": f"mmad_gemm_kernel bwd-weight + fused Adam (dW[{N}x{K}] over {B} windows, bf16, tile 64x64)",
+d = {"kernel": f"mmad_gemm_kernel bwd-weight + fused Adam (dW[{N}x{K}] over {B} windows, bf16, tile {tile})",
      "workload": {"dim": 2048, "batch": B, "dtype": "bf16", "model": model, "layer": layer},
      "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | TCC_HIT_sum TCC_MISS_sum | "
                 "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE (separate passes) -- python3 tools/dw_one.py "
