@@ -254,8 +254,14 @@ def run(args):
     from icra2021_multimodal_ad_amd.model_builder import get_model
     from icra2021_multimodal_ad_amd.data import synth_windows_device
 
-    torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-    rank, world, local = mdist.init_from_env()
+    # MMAD_BENCH_SHARED_GPU=1 (harness test only): every rank on cuda:0 over
+    # gloo, so the N>1 launch / rendezvous / max-over-ranks / report path can be
+    # exercised on a one-GPU box (RCCL refuses two ranks on one device)
+    shared = os.environ.get("MMAD_BENCH_SHARED_GPU", "0") == "1"
+    torch.cuda.set_device(0 if shared else int(os.environ.get("LOCAL_RANK", "0")))
+    rank, world, local = mdist.init_from_env(backend="gloo" if shared else None)
+    if shared:
+        local = 0
     cname = args.config if args.config != "auto" else ("c2" if world == 1 else "c4")
     cfgd = dict(CONFIGS[cname])
     for k in ("model", "dim", "batch"):
@@ -361,8 +367,14 @@ def run(args):
         graph_mode = nat.use_graph
         nat.use_graph = False
         _native.check(lib.mmad_ae_probe(nat._h, 1, probe_layer, n_probe), "mmad_ae_probe")
+        # rank 0 alone: single-process fused steps (no collective the other
+        # ranks would have to join; at N > 1 the exchange is already detached
+        # from the executor by the n1_same_workload run above)
+        probe_dist = model.dist
+        model.dist = None
         for i in range(n_probe):
             model.train_step_async(pool[i % len(pool)], opt)
+        model.dist = probe_dist
         torch.cuda.synchronize()
         buf = (ctypes.c_float * n_probe)()
         n = lib.mmad_ae_probe_read(nat._h, buf, n_probe)
@@ -378,8 +390,8 @@ def run(args):
                          else "eager executor step (mmad_ae_train_step)")
     if rank == 0:
         if durs:
-            fused = model.dist is None or not model.dist.native
-            res["roofline"] = dw_roofline(nat, probe_layer, durs, batch, n_probe, fused_adam=fused,
+            # the probe steps are single-process fused steps (Adam in the dW epilogue)
+            res["roofline"] = dw_roofline(nat, probe_layer, durs, batch, n_probe, fused_adam=True,
                                           layers=probe_layers)
         res["roofline_encoder_gemm"] = gemm_roofline(model, batch)
         if not args.no_cpu_baseline and world == 1:   # host baseline: rank 0 at N=1 only
