@@ -89,6 +89,20 @@ class NativeComm:
                       "mmad_comm_create")
         self.handle = h
 
+    def self_test(self, n=4096):
+        """One sum all-reduce through the library's communicator on a fresh
+        stream-ordered buffer (rank r contributes r + 1), checked on the host:
+        a communicator that builds but cannot exchange fails here, before any
+        train step depends on it (the ranks then fall back together)."""
+        from . import _native
+        from ._native import ptr, stream_ptr
+        buf = torch.full((n,), float(self.rank + 1), device="cuda", dtype=torch.float32)
+        _native.check(self._lib.mmad_allreduce_bucket(self.handle, ptr(buf), n, stream_ptr()),
+                      "mmad_allreduce_bucket")
+        want = self.world * (self.world + 1) / 2.0
+        if not bool(torch.all(buf == want)):
+            raise RuntimeError(f"native all-reduce self-test: got {float(buf[0])}, want {want}")
+
     def close(self):
         if self.handle is not None and self.handle.value:
             self._lib.mmad_comm_destroy(self.handle)
@@ -116,8 +130,12 @@ class DataParallel:
             comm, err = None, None
             try:
                 comm = NativeComm(group)
+                comm.self_test()
             except Exception as e:  # noqa: BLE001 -- reported below, then fallback
                 err = e
+                if comm is not None:
+                    comm.close()
+                    comm = None
             ok = torch.tensor([0.0 if comm is None else 1.0], device="cuda")
             dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
             if float(ok.item()) == 1.0:

@@ -221,3 +221,30 @@ def test_dp_novelty_detecter_two_ranks():
     for k, (v, t) in det.last_scores.items():
         np.testing.assert_allclose(a["scores"][k][0], v, rtol=1e-5, atol=1e-7, err_msg=k)
         np.testing.assert_allclose(a["scores"][k][1], t, rtol=1e-5, atol=1e-7, err_msg=k)
+
+
+def test_native_comm_self_test_passes_and_catches_a_broken_exchange():
+    """dist.NativeComm.self_test (run before the native exchange is used, the
+    ranks fall back to torch.distributed together if it fails): a one-rank
+    RCCL communicator sums correctly; a loopback communicator that doubles
+    its buffer (a wrong exchange) is rejected."""
+    import ctypes
+    import types as _t
+    from icra2021_multimodal_ad_amd import _native
+    from icra2021_multimodal_ad_amd.dist import NativeComm
+    lib = _native.load()
+    torch.cuda.set_device(0)
+    n = lib.mmad_comm_unique_id_bytes()
+    uid = (ctypes.c_char * n)()
+    assert lib.mmad_comm_get_unique_id(uid) == 0, lib.mmad_last_error_string()
+    h = ctypes.c_void_p()
+    assert lib.mmad_comm_create(ctypes.byref(h), uid, 1, 0) == 0, lib.mmad_last_error_string()
+    good = _t.SimpleNamespace(_lib=lib, handle=h, rank=0, world=1)
+    NativeComm.self_test(good)
+    lib.mmad_comm_destroy(h)
+    hb = ctypes.c_void_p()
+    assert lib.mmad_comm_create_loopback(ctypes.byref(hb), 2.0) == 0
+    bad = _t.SimpleNamespace(_lib=lib, handle=hb, rank=0, world=1)
+    with pytest.raises(RuntimeError, match="self-test"):
+        NativeComm.self_test(bad)
+    lib.mmad_comm_destroy(hb)
