@@ -7,6 +7,9 @@ Workloads (``--config``; ``auto`` = c2 on one GPU, c4 on several):
   c4  BASELINE configs[3]: the c3 model, 4096 windows PER GPU (global 4096*N),
       one process per GPU, per-layer RCCL all-reduce of the gradients over xGMI
       overlapped with the backward (weak scaling)
+  c5  BASELINE configs[4]: RaPP scoring (get_diffs + BASE + SAP) over 1,048,576
+      windows resident in HBM, D=2048, one hipGraph-captured pass per step
+      (bench_score.run_c5; metric: scored windows/s)
 ``--model/--dim/--batch`` override the chosen config's fields.
 
 ``python bench.py --gpus N`` without torchrun env vars spawns the N ranks itself
@@ -14,15 +17,17 @@ Workloads (``--config``; ``auto`` = c2 on one GPU, c4 on several):
 RANK/WORLD_SIZE/LOCAL_RANK.  W untimed steps, then K timed steps between
 barrier + synchronize pairs, the max over ranks; rank 0 prints ONE JSON line:
 
-* the timed steps each replay ONE captured hipGraph of the whole step
-  (mmad_ae_train_step_graph; ``train_step`` says which schedule ran).
+* the timed steps are eager executor steps (mmad_ae_train_step: one host
+  call enqueues the whole step on the main + side streams, no host sync);
+  ``train_step`` says which schedule ran.  ``step_spread`` = per-step GPU
+  times from HIP events between consecutive steps of a separate run of the
+  same length right after the timed region (median / p10 / p90 / max).
 * ``roofline``: the kernel that dominates the step -- the dW GEMM with the
   fused Adam epilogue of the largest layer, HBM-bound (26 B of Adam state per
   parameter + its two bf16 operands).  Its duration comes from the executor's
   probe (mmad_ae_probe: a HIP event pair around that one launch, on the stream
   it runs on) over eager steps of the same state right after the timed region
-  (a graph replay has no per-kernel events); the rocprofv3 kernel trace of the
-  graph-mode run under profiles/ gives the in-graph average;  ``traffic`` =
+  (the same state and inputs);  ``traffic`` =
   PMC HBM bytes per launch from the newest matching profiles/*_pmc_dw.json.
 * ``roofline_encoder_gemm``: the encoder's first forward GEMM (the north-star
   MFMA target), launched back to back between one event pair.
@@ -50,6 +55,7 @@ CONFIGS = {
     "c2": dict(model="ae", dim=2048, batch=1024, name="BASELINE configs[1]"),
     "c3": dict(model="vib_ae", dim=2048, batch=4096, name="BASELINE configs[2]"),
     "c4": dict(model="vib_ae", dim=2048, batch=4096, name="BASELINE configs[3]"),
+    "c5": dict(model="ae", dim=2048, batch=65536, name="BASELINE configs[4]"),
 }
 
 
@@ -77,7 +83,9 @@ def cpu_baseline(d, batch, vib, budget_s=12.0):
     from oracle import torch_ref
     from icra2021_multimodal_ad_amd.common_utils import init_state_dict, ae_widths
     from icra2021_multimodal_ad_amd.data import synth_windows
-    threads = torch.get_num_threads()
+    # every host core this process may run on (the lease's affinity)
+    threads = len(os.sched_getaffinity(0))
+    torch.set_num_threads(threads)
     enc_out = 200 if vib else None
     enc, dec = ae_widths(d, 100, 5, enc_out=enc_out)
     sd = init_state_dict(d, 100, 5, seed=0, enc_out=enc_out)
@@ -97,7 +105,7 @@ def cpu_baseline(d, batch, vib, budget_s=12.0):
             "sample": f"{n} train steps of the reference's modules in torch-CPU fp32 "
                       f"(nn.Linear/LeakyReLU/BatchNorm1d, MSELoss(sum), optim.Adam; "
                       f"oracle/torch_ref.py{', VIB-AE' if vib else ''}) at D={d}, batch={batch}, "
-                      f"{el:.1f} s, torch threads={threads}"}
+                      f"{el:.1f} s, torch threads={threads} = len(os.sched_getaffinity(0))"}
 
 
 def dw_adam_bytes(N, K, B, es=2):
@@ -108,17 +116,10 @@ def dw_adam_bytes(N, K, B, es=2):
 
 
 def pick_dominant_layer(nat, batch):
-    """Largest parameter count among the layers whose dW GEMM carries the
-    fused Adam epilogue.  Below 4096 windows every layer does (ties: the
-    first, encoder layer 1, on the main stream at the end of the chain); with
-    the split tail (MMAD_DW_SPLIT=1, or -1 from 4096 windows) layers 0 and 1
-    (l < MMAD_DW_MAIN = 2) run as a dW GEMM + flat Adam pass instead (ties:
-    the last, the decoder's output layer on the side stream)."""
-    sp = os.environ.get("MMAD_DW_SPLIT", "0")
-    split = sp not in ("-1", "0") or (sp == "-1" and batch >= 4096)
-    if not split:
-        return max(range(len(nat.layers)), key=lambda l: (nat.layers[l]["N"] * nat.layers[l]["K"], -l))
-    return max(range(2, len(nat.layers)), key=lambda l: (nat.layers[l]["N"] * nat.layers[l]["K"], l))
+    """Largest parameter count among the layers (every dW GEMM carries the
+    fused Adam epilogue; ties: the first, encoder layer 1, on the main stream
+    at the end of the chain)."""
+    return max(range(len(nat.layers)), key=lambda l: (nat.layers[l]["N"] * nat.layers[l]["K"], -l))
 
 
 def _pmc_file(kind, workload):
@@ -180,8 +181,7 @@ def gemm_roofline(model, batch, iters=50):
 
 def dw_roofline(nat, layer, durations_ms, batch, steps_timed, fused_adam=True, layers=None):
     """roofline of the dominant dW GEMM launch from the in-situ probe durations.
-    layers: the layers that launch covered (mmad_ae_probe_layers: the
-    main-stream tail runs layers 1 and 0 as one pair launch)."""
+    layers: the layers that launch covered (mmad_ae_probe_layers)."""
     import statistics
     layers = sorted(layers or [layer], reverse=True)
     rows = batch                      # k = 1: decoder rows = encoder rows
@@ -209,7 +209,7 @@ def dw_roofline(nat, layer, durations_ms, batch, steps_timed, fused_adam=True, l
         wl["layers"] = layers
         pmc, src = _pmc_file("dw", wl)
     shapes = ", ".join(f"layer {l}: dW[{nat.layers[l]['N']}x{nat.layers[l]['K']}]" for l in layers)
-    kern = "mmad_gemm_pair_kernel" if len(layers) > 1 else "mmad_gemm_kernel"
+    kern = "mmad_gemm_kernel"
     return {"kernel": f"{kern} {what} ({shapes} = dz^T a over {rows} windows"
                       f"{'; both layers in one launch' if len(layers) > 1 else ''}; {body})",
             "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -263,6 +263,12 @@ def run(args):
     if shared:
         local = 0
     cname = args.config if args.config != "auto" else ("c2" if world == 1 else "c4")
+    if cname == "c5":
+        import bench_score
+        if world > 1:
+            raise SystemExit("c5 (scoring) is a one-GPU configuration")
+        bench_score.run_c5(args)
+        return
     cfgd = dict(CONFIGS[cname])
     for k in ("model", "dim", "batch"):
         if getattr(args, k) is not None:
@@ -299,10 +305,21 @@ def run(args):
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    # a fused-BN barrier or split-K combine that timed out leaves its launch's
+    # outputs unwritten (sticky error word): such steps are not a measurement.
+    # Every rank checks; the flag is all-reduced so all ranks stop together.
+    bad = 0
+    try:
+        nat.check_status()
+    except Exception as e:   # noqa: BLE001 -- reported below, on every rank
+        print(f"[bench] rank {rank}: {e}", file=sys.stderr, flush=True)
+        bad = 1
     if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        t = torch.tensor([el, float(bad)], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el, bad = float(t[0].item()), int(t[1].item())
+    if bad:
+        raise SystemExit("bench: a kernel barrier timed out in the timed steps; no valid measurement")
     loss_v = float(loss.item())
 
     fpw, _ = ae_flops_per_window(nat.enc_widths, nat.dec_widths)
@@ -334,6 +351,20 @@ def run(args):
         "host_enqueue_ms_per_step": round(t_host / args.steps * 1e3, 4),
         "final_loss": loss_v,
     }
+    # per-step spread: the same number of steps again, a HIP event after each
+    # (on the caller's stream, which joins the side streams at every step end)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    evs[0].record()
+    for i in range(args.steps):
+        model.train_step_async(pool[i % len(pool)], opt)
+        evs[i + 1].record()
+    torch.cuda.synchronize()
+    per = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    q = lambda f: per[min(len(per) - 1, int(f * len(per)))]   # noqa: E731
+    res["step_spread"] = {"median_ms": round(q(0.5), 4), "p10_ms": round(q(0.1), 4),
+                          "p90_ms": round(q(0.9), 4), "max_ms": round(per[-1], 4),
+                          "steps": args.steps,
+                          "how": "HIP event after every step, separate run right after the timed one"}
     if world > 1:
         # same workload without the exchange, same ranks (read scaling against it)
         mdl_dist = model.dist
@@ -385,6 +416,7 @@ def run(args):
         probe_layers = [l for l in range(len(nat.layers)) if mask > 0 and (mask >> l) & 1] or [probe_layer]
         _native.check(lib.mmad_ae_probe(nat._h, 1, -1, 0), "mmad_ae_probe")
         nat.use_graph = graph_mode
+        nat.check_status()
     res["train_step"] = ("one captured hipGraph replay per step (mmad_ae_train_step_graph)"
                          if nat.use_graph and (model.dist is None or not model.dist.native)
                          else "eager executor step (mmad_ae_train_step)")

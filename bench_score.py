@@ -42,7 +42,7 @@ def cpu_baseline(d, budget_s=10.0):
     from oracle.model_io import model_from_state_dict
     from icra2021_multimodal_ad_amd.common_utils import init_state_dict
     from icra2021_multimodal_ad_amd.data import synth_windows
-    threads = min(16, os.cpu_count() or 1)
+    threads = len(os.sched_getaffinity(0))   # every host core of this process
     m = model_from_state_dict(init_state_dict(d, 100, 5, seed=0))
     x = synth_windows(4096, d, seed=3)
     n, t0 = 0, time.perf_counter()
@@ -55,7 +55,123 @@ def cpu_baseline(d, budget_s=10.0):
     el = time.perf_counter() - t0
     return {"value": n / el, "unit": "windows/sec", "cores": threads, "kind": "port",
             "sample": f"{n} windows of oracle get_diffs+BASE+SAP (numpy fp32, batch 698) at D={d}, "
-                      f"{el:.1f} s, BLAS threads={threads}"}
+                      f"{el:.1f} s, BLAS threads={threads} = len(os.sched_getaffinity(0))"}
+
+
+def _setup(dim, dtype, N, batch):
+    """Model after 20 train steps (real BN statistics), eval mode; N windows
+    resident in HBM; one warm / tuning scoring batch."""
+    import torch
+    import types
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    from icra2021_multimodal_ad_amd.data import synth_windows_device
+    from icra2021_multimodal_ad_amd import reconstruction_aggregation as ra
+    dev = torch.device("cuda", 0)
+    cfg = types.SimpleNamespace(input_size=dim, btl_size=100, n_layers=5, gpu_id=0, dtype=dtype)
+    torch.manual_seed(0)
+    model = get_model(cfg)
+    for i in range(20):
+        model.train_step_async(synth_windows_device(1024, dim, dev, seed=500 + i))
+    model.eval()
+    nat = model._native
+    nat.sync_shadow(force=True)
+    x = torch.empty((N, dim), device=dev)
+    for s0 in range(0, N, 65536):
+        n = min(65536, N - s0)
+        x[s0:s0 + n] = synth_windows_device(n, dim, dev, seed=7 + s0)
+    layer_sq = torch.empty((nat.n_enc + 1, N), device=dev)
+    ra.score_windows(x[:batch], model, batch, out=layer_sq[:, :batch])   # warm / tile tuning
+    torch.cuda.synchronize()
+    return model, nat, x, layer_sq
+
+
+def score_gemm_roofline(nat, B, iters=30):
+    """The largest score GEMM (last decoder layer, score epilogue vs x) at B
+    rows, per-launch HIP event pairs on the launch stream."""
+    import torch
+    from icra2021_multimodal_ad_amd import _native
+    from icra2021_multimodal_ad_amd._native import call, ptr, stream_ptr
+    dev = nat.device
+    L = nat.layers[-1]
+    Mp = _native.pad(B)
+    tdt = torch.bfloat16 if nat.dt == _native.BF16 else torch.float32
+    xin = torch.randn((Mp, L["Kp"]), device=dev).to(tdt)
+    ref = torch.randn((Mp, L["Np"]), device=dev).to(tdt)
+    out = torch.empty((Mp, L["Np"]), device=dev, dtype=tdt)
+    rowsq = torch.empty((L["Np"] // 128, Mp), device=dev)
+    w = nat.shadow[L["w_off"]:] if nat.shadow is not None else nat.params[L["w_off"]:]
+    bb = nat.params[L["b_off"]:]
+    s = stream_ptr()
+
+    def launch():
+        call("mmad_fc_fwd_score", nat.dt, B, L["N"], L["K"], Mp, L["Np"], L["Kp"], ptr(xin), ptr(w),
+             ptr(bb), 0, 0.2, None, None, ptr(out), ptr(ref), ptr(rowsq), None, 0, s)
+    for _ in range(5):
+        launch()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    for e0, e1 in ev:
+        e0.record()
+        launch()
+        e1.record()
+    torch.cuda.synchronize()
+    avg = sum(e0.elapsed_time(e1) for e0, e1 in ev) / 1e3 / len(ev)
+    fl = 2.0 * B * L["K"] * L["N"]
+    peak = BF16_PEAK_TFLOPS if nat.dt == _native.BF16 else F32_PEAK_TFLOPS
+    return {"kernel": f"mmad_gemm_kernel score (decoder last layer {B}x{L['K']} . "
+                      f"{L['N']}x{L['K']}^T + sum (y-x)^2 epilogue)",
+            "bound": "mfma", "achieved": round(fl / avg / 1e12, 2), "peak": peak,
+            "unit": "TFLOP/s", "frac": round(fl / avg / 1e12 / peak, 4), "traffic": None,
+            "avg_us": round(avg * 1e6, 2), "flops_per_launch": fl,
+            "timing": f"{iters} launches, a HIP event pair around each"}
+
+
+def run_c5(args):
+    """bench.py --config c5: BASELINE configs[4].  One step = one whole RaPP
+    scoring pass (BASE + SAP per window) over 1,048,576 windows resident in
+    HBM, replayed as one captured hipGraph (mmad_ae_score_stream) plus the
+    on-device BASE / SAP reductions; W untimed passes, then K timed passes
+    between synchronize pairs."""
+    import torch
+    from icra2021_multimodal_ad_amd import reconstruction_aggregation as ra
+    dim = args.dim or 2048
+    batch = args.batch or 65536
+    N = 1 << 20
+    model, nat, x, layer_sq = _setup(dim, args.dtype, N, batch)
+    widths = nat.diff_widths()
+
+    def one_pass():
+        ra.score_windows(x, model, batch, out=layer_sq, graph=True)
+        return ra.base_from_layer_sq(layer_sq, widths), ra.sap_from_layer_sq(layer_sq, widths)
+    for _ in range(max(1, args.warmup)):        # the first call captures the graph
+        one_pass()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        base, sap = one_pass()
+    t_host = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    nat.check_status()
+    value = args.steps * N / el
+    fpw = score_flops_per_window(nat.enc_widths, nat.dec_widths)
+    res = {
+        "metric": "sensor-windows/sec (RaPP scoring: BASE+SAP)",
+        "value": round(value, 1), "unit": "sensor-windows/sec", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic (seeded 4-modal windows resident in HBM, AE after 20 train steps)",
+        "config": {"workload": f"c5 (BASELINE configs[4]): RaPP scoring (get_diffs + BASE + SAP), "
+                               f"D={dim}, btl=100, n_layers=5, {N} windows per step in batches of "
+                               f"{batch}, one hipGraph replay per step", "global_batch": N,
+                   "input_dim": dim, "parallelism": "dp1"},
+        "model_tflops": round(value * fpw / 1e12, 2),
+        "host_enqueue_ms_per_step": round(t_host / args.steps * 1e3, 4),
+        "score_checksum": {"base_mean": float(base.mean()), "sap_mean": float(sap.mean())},
+        "roofline": score_gemm_roofline(nat, batch),
+    }
+    if not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(dim, budget_s=min(args.cpu_budget, 12.0))
+    print(json.dumps(res), flush=True)
 
 
 def main():

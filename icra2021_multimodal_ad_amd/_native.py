@@ -4,6 +4,7 @@ There is no fallback: if the library is missing or no GPU is visible, calls
 raise ``NativeUnavailable``.  Loading the library itself needs no GPU (the CPU
 test-suite checks the exported symbols).
 """
+import contextlib
 import ctypes
 import os
 
@@ -27,6 +28,7 @@ SIGNATURES = {
     "mmad_abi_version": (_I, []),
     "mmad_pad_granule": (_I, []),
     "mmad_tune_set": (_I, [_I, _I]),
+    "mmad_tune_get": (_I, [_I, ctypes.POINTER(_I)]),
     "mmad_gemm_splitk_for": (_I, [_I, _I, _I, _I, _I]),
     "mmad_gemm_ws_bytes": (ctypes.c_size_t, []),
     "mmad_gemm_set_workspace": (_I, [_P, ctypes.c_size_t]),
@@ -99,6 +101,48 @@ SIGNATURES = {
     "mmad_hsr_weight_count": (_I, []),
     "mmad_hsr_fuse": (_I, [_I, _P, _P, _P, _P, _P, _I, _P, _I, _P]),
 }
+
+
+# the library's tune table (include/mmad.h, mmad_tune_set): GEMM knobs are read
+# per dispatch, the schedule knobs (16-27) when a model handle is created
+KNOB = dict(tile=0, group_m=1, autotune=2, dbg=3, splitk=4, tile_adam=5, tile_bwd_data=6,
+            tile_fwd=7, tile_adam_main=8, splitk_dw=9, splitk_dw_blocks=10, splitk_dw_min_stages=11,
+            bn_mode=16, bn_mode_bwd=17, bn_fused_rows=18, dw_main=19, pair_rows=20, dw_main_ping=21,
+            ev_every=22, loss_side=23, dp_small_at=24, keep_grads=25, side_prio=26,
+            event_sysfence=27)
+# host-side schedule choices of the Python executor wrapper (engine.py), read
+# when a model is built: a second bf16 weight shadow (ping-pong), and whether
+# train_step replays one captured hipGraph per step instead of the eager enqueue
+SCHEDULE = {"shadow_pair": True, "train_graph": False}
+
+
+def tune_get(name):
+    if name in SCHEDULE:
+        return SCHEDULE[name]
+    v = ctypes.c_int(0)
+    check(load().mmad_tune_get(KNOB[name], ctypes.byref(v)), f"tune_get({name})")
+    return v.value
+
+
+def tune_set(name, value):
+    if name in SCHEDULE:
+        SCHEDULE[name] = value
+        return
+    check(load().mmad_tune_set(KNOB[name], int(value)), f"tune_set({name})")
+
+
+@contextlib.contextmanager
+def tune(**knobs):
+    """Set tune-table knobs / host schedule options for the duration of a
+    ``with`` block (models created inside keep their schedule), then restore."""
+    old = {k: tune_get(k) for k in knobs}
+    try:
+        for k, v in knobs.items():
+            tune_set(k, v)
+        yield
+    finally:
+        for k, v in old.items():
+            tune_set(k, v)
 
 
 class NativeUnavailable(RuntimeError):

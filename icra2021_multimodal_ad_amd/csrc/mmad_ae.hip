@@ -37,14 +37,12 @@
 // skip the system-scope fence (L2 writeback for host visibility) that a
 // default event adds at record time.  Each record still leaves a ~5 us bubble
 // on the main stream (~6 us with the fence; 0.513 vs 0.521 ms/step).
-// Device-scope release/acquire (the same as a
-// kernel boundary on one stream) still orders the data.  MMAD_EVENT_SYSFENCE=1
-// restores the default.
-static const unsigned kEvFlags = [] {
-  const char* e = getenv("MMAD_EVENT_SYSFENCE");
-  return (e && atoi(e)) ? (unsigned)hipEventDisableTiming
-                        : (unsigned)(hipEventDisableTiming | hipEventDisableSystemFence);
-}();
+// Device-scope release/acquire (the same as a kernel boundary on one stream)
+// still orders the data.  Knob 27 restores the default.
+static unsigned ev_flags(int sysfence) {
+  return sysfence ? (unsigned)hipEventDisableTiming
+                  : (unsigned)(hipEventDisableTiming | hipEventDisableSystemFence);
+}
 
 struct AeLayer {
   int K, N, Kp, Np;
@@ -68,148 +66,61 @@ struct mmad_ae {
   std::vector<hipEvent_t> ev_fork, ev_data;
   hipEvent_t ev_join = nullptr;
   hipEvent_t ev_loss = nullptr;   // fused step: forward done -> the loss reduction on the side stream
-  int loss_side = [] {            // MMAD_LOSS_SIDE=0: reduce the loss at the end of the main stream
-    const char* e = getenv("MMAD_LOSS_SIDE");
-    return e ? atoi(e) : 1;
-  }();
-  // tail stream (MMAD_DW_TAIL=1): the main-stream dW GEMMs of layers
-  // 1 .. dw_main-1 run here instead, concurrently with the end of the chain
-  int dw_tail = [] {
-    const char* e = getenv("MMAD_DW_TAIL");
-    return e ? atoi(e) : 0;
-  }();
-  hipStream_t tail = nullptr;
-  hipEvent_t ev_tail = nullptr;
-  // side-stream GEMM launches reserve this much extra LDS per workgroup
-  // (MMAD_SIDE_LDS_PAD bytes): fewer side workgroups per CU, so the main
-  // stream's chain always finds room next to them
-  int side_lds_pad = [] {
-    const char* e = getenv("MMAD_SIDE_LDS_PAD");
-    return e ? atoi(e) : 0;
-  }();
-  // fused step, layers < dw_main (the end of the backward chain): the dW
-  // GEMM (with the small-segment Adam in its epilogue) and a flat Adam pass
-  // over the weights instead of one Adam-fused dW GEMM: layer l >= 1's GEMM
-  // starts on the tail stream as soon as dz_l exists, its Adam once
-  // bwd-data(l) has read W_l, both overlapping the end of the chain
-  // (MMAD_DW_SPLIT=0: the fused form on the main stream; -1: split from 4096
-  // rows per call).  Default 0: since the dW GEMM loop stopped draining its
-  // LDS ring every K stage (asm LDS-DMA) the fused form wins at both sizes
-  // (VIB D=2048 B=4096: 0.991-0.996 vs 1.013 ms/step; D=2048 B=1024: 0.455 vs
-  // 0.468; profiles/r02ad_*, r02ae_*; before: split 1.217 vs 1.244 at 4096)
-  int dw_split = [] {
-    const char* e = getenv("MMAD_DW_SPLIT");
-    return e ? atoi(e) : 0;
-  }();
-  // fused step, layers < dw_main (the main-stream tail): the dW GEMM without
-  // Adam publishing each fp32 tile (tile flags) and the streamed Adam
-  // (mmad_adam_stream_kernel) consuming the tiles as they complete on the tail
-  // stream, so the tile's K loop and the Adam state stream could overlap
-  // instead of running one after the other in the same waves (MMAD_ADAM_STREAM;
-  // grid MMAD_ADAM_STREAM_GRID workgroups, at most two per CU).  Off by
-  // default: measured slower at every tile / grid (c2 0.473-0.487 vs 0.448
-  // ms/step, c3 1.03-1.11 vs 0.998; profiles/r02bf_*): beside the Adam stream
-  // the latency-bound dW K loop slows down (layer 0: 39.6 us vs ~20 alone),
-  // so the pair takes longer than the fused kernel (46-50 vs 33 us)
-  int adam_stream = [] {
-    const char* e = getenv("MMAD_ADAM_STREAM");
-    return e ? atoi(e) : 0;
-  }();
-  int adam_stream_grid = [] {
-    const char* e = getenv("MMAD_ADAM_STREAM_GRID");
-    return e ? atoi(e) : 512;
-  }();
-  // tile of the flagged dW GEMM: 64x64 by default, so its 2-3 waves of
-  // blocks hand tiles over progressively (a one-wave grid of large tiles
-  // finishes every tile at once and leaves nothing to overlap); -1 = autotuned
-  int adam_stream_tile = [] {
-    const char* e = getenv("MMAD_ADAM_STREAM_TILE");
-    return e ? atoi(e) : 3;
-  }();
-  // fused step, dw_main == 2: the Adam-fused dW GEMMs of layers 1 and 0 (the
-  // main-stream tail) as ONE launch of two problems (mmad_gemm_pair_kernel)
-  // when both use the same tile, so the second problem's blocks fill the
-  // first one's last partial wave (MMAD_DW_PAIR=1).  Bit-identical, but
-  // neutral as measured (c2 58 us for the pair vs 33 + 25 separately, c3 110
-  // vs 60 + 52; profiles/r02bp_*): the blocks already backfill freed slots
-  // across the two launches, so off by default
-  int dw_pair = [] {
-    const char* e = getenv("MMAD_DW_PAIR");
-    return e ? atoi(e) : 0;
-  }();
+  // the schedule, copied from the tune table at create (include/mmad.h knobs
+  // 16-27): one schedule per handle, whatever the table says later
+  unsigned ev_flags_ = 0;
+  int loss_side = 1;      // knob 23: reduce the loss on the side stream after the forward
+  int side_prio_hi = 0;   // knob 26
   // data-parallel step: the small bucket (bias / gamma / beta grads + loss)
   // goes on the comm stream right after the bwd-data GEMM of this layer
-  // (ahead of this layer's and the lower layers' weight buckets);
-  // MMAD_DP_SMALL_AT, 0 or 1
-  int dp_small_at = [] {
-    const char* e = getenv("MMAD_DP_SMALL_AT");
-    return e ? atoi(e) : 1;
-  }();
+  // (ahead of this layer's and the lower layers' weight buckets); knob 24
+  int dp_small_at = 1;
   int mse_tiles = 0;   // loss partials written by the last MSE GEMM
   // data parallelism: RCCL communicator (not owned), its stream and events
   mmad_comm* comm = nullptr;
   hipStream_t cstream = nullptr;
   std::vector<hipEvent_t> ev_dw;
   hipEvent_t ev_small = nullptr, ev_cdone = nullptr;
-  // fused step: dW GEMMs of layers < dw_main run on the caller's stream;
-  // keep_grads: also write dW to the grads buffer
-  int dw_main = [] {
-    const char* e = getenv("MMAD_DW_MAIN");
-    return e ? atoi(e) : 2;   // tools/sched_sweep.py: 0.499 ms (2) vs 0.512 (1) vs 0.523 (3)
-  }();
+  // fused step: dW GEMMs of layers < dw_main run on the caller's stream
+  // (knob 19; tools/sched_sweep.py: 0.499 ms (2) vs 0.512 (1) vs 0.523 (3));
+  // keep_grads (knob 25): also write dW to the grads buffer
+  int dw_main = 2;
   // ping-pong schedule per call from this many padded rows (bf16 with a
-  // shadow pair; MMAD_SHADOW_PAIR_ROWS), with dw_main_ping main-stream dW
-  // GEMMs (MMAD_DW_MAIN_PING): VIB B=4096 0.941-0.945 vs 0.995-0.999 ms/step,
-  // B=1024 0.450-0.455 vs 0.442-0.449 (profiles/r02bu_*, r02bv_*)
-  int pair_rows = [] {
-    const char* e = getenv("MMAD_SHADOW_PAIR_ROWS");
-    return e ? atoi(e) : 4096;
-  }();
-  int dw_main_ping = [] {
-    const char* e = getenv("MMAD_DW_MAIN_PING");
-    return e ? atoi(e) : 1;
-  }();
-  int keep_grads = [] {
-    const char* e = getenv("MMAD_KEEP_GRADS");
-    return e ? atoi(e) : 0;
-  }();
+  // shadow pair; knob 20), with dw_main_ping main-stream dW GEMMs (knob 21):
+  // VIB B=4096 0.941-0.945 vs 0.995-0.999 ms/step, B=1024 0.450-0.455 vs
+  // 0.442-0.449 (profiles/r02bu_*, r02bv_*)
+  int pair_rows = 4096;
+  int dw_main_ping = 1;
+  int keep_grads = 0;
   // train-mode BN: fold the batch statistics into the consumer's weights
   // (bn_fold_k; the bf16 throughput path) or normalise the activations into y
   // (bn_train_apply_k; the exact-fp32 parity path: folding contracts the raw,
   // un-centred activations and cancels the mean back out, which costs the
   // fp32 path ~10x the reference's rounding error on BN-producer layers).
-  // Set at create from the dtype; MMAD_BN_FOLD=0/1 overrides.
+  // Set at create from the dtype and knob 16.
   int fold = 1;
   // train-mode BN inside the producing GEMM (bn_mode 2, MMAD_BN_MODE): the
   // forward GEMM's epilogue finishes the batch statistics and writes y, the
   // bwd-data GEMM's epilogue writes dz (a per-column-tile barrier between the
   // blocks of one column, mmad_gemm_mfma.hip) -- no finalize / fold / apply
   // launches.  Layers whose grid cannot be co-resident fall back to mode 0
-  // (apply kernels).  0 = apply kernels, 1 = fold, 2 = fused.  Default: bf16
+  // (apply kernels).  0 = apply kernels, 1 = fold, 2 = fused (knob 16).  Default: bf16
   // 2 up to bn_fused_rows padded rows per call (measured: D=2048 B=1024
   // 0.495 ms/step fused vs 0.531 apply vs 0.536 fold; B=4096 VIB 1.33 fused
   // vs 1.32 apply vs 1.27 fold -- more tiles per column, longer barrier
   // waits), fold above; fp32 0 (the parity path).
   int bn_mode = 0;
-  // backward BN schedule override for the bf16 path (MMAD_BN_MODE_BWD: -1 =
+  // backward BN schedule override for the bf16 path (knob 17: -1 =
   // the forward's; 2 = fused into the bwd-data GEMMs whatever the forward did:
   // the fused backward needs only a, the saved mean / rstd and gamma, which
   // every forward schedule leaves)
-  int bn_mode_bwd = [] {
-    const char* e = getenv("MMAD_BN_MODE_BWD");
-    return e ? atoi(e) : -1;
-  }();
-  int bn_fused_rows = [] {
-    const char* e = getenv("MMAD_BN_FUSED_MAX_ROWS");
-    return e ? atoi(e) : 2048;
-  }();
+  int bn_mode_bwd = -1;
+  int bn_fused_rows = 2048;   // knob 18
   // fused step: record the "bwd-data of l done" event only every ev_every-th
   // side-stream layer (each record costs a bubble on the main stream); the dW
-  // GEMMs of the layers in between wait for the next recorded one
-  int ev_every = [] {
-    const char* e = getenv("MMAD_EV_EVERY");
-    return e ? atoi(e) : 2;   // c2 0.435-0.440 vs 0.442-0.444 with 1 (profiles/r02bv_*)
-  }();
+  // GEMMs of the layers in between wait for the next recorded one (knob 22;
+  // c2 0.435-0.440 vs 0.442-0.444 with 1, profiles/r02bv_*)
+  int ev_every = 2;
   // hipGraph cache for mmad_ae_score_stream: one captured graph per
   // (input, output, workspace, N, batch) pass, replayed with one launch
   struct ScoreGraph {
@@ -266,8 +177,6 @@ struct mmad_ae {
     if (ev_cdone) (void)hipEventDestroy(ev_cdone);
     if (cstream) (void)hipStreamDestroy(cstream);
     if (side) (void)hipStreamDestroy(side);
-    if (ev_tail) (void)hipEventDestroy(ev_tail);
-    if (tail) (void)hipStreamDestroy(tail);
   }
 };
 
@@ -284,7 +193,6 @@ struct LayerWS {
   bool fwd_fused, bwd_fused;
   unsigned* sync_f;   // fused-BN barrier counters (MMAD_BN_SYNC_WORDS each)
   unsigned* sync_b;
-  unsigned* tflag;    // streamed-Adam tile flags of this layer's dW GEMM ((Np/64)*(Kp/64))
 };
 struct AeWS {
   int B, k, Mpe, Mpd;
@@ -328,11 +236,7 @@ static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
     mmad_gemm_splitk_bytes(0, 0, &slab, &ctl);
     ctl = (ctl + 255) / 256 * 256;
     // + fused-BN barrier counters: 2 blocks per layer, then the error word
-    // + the streamed-Adam tile flags, one word per 64x64 dW tile of every layer
-    size_t tf_words = 0;
-    for (const AeLayer& a : h->L) tf_words += (size_t)(a.Np / 64) * (a.Kp / 64);
-    const size_t bn_ctl =
-        ((size_t)(2 * h->L.size() * MMAD_BN_SYNC_WORDS + 64 + tf_words) * 4 + 255) / 256 * 256;
+    const size_t bn_ctl = ((size_t)(2 * h->L.size() * MMAD_BN_SYNC_WORDS + 64) * 4 + 255) / 256 * 256;
     w.sk_ctl_bytes = 2 * ctl + bn_ctl;
     char* c = take((int64_t)w.sk_ctl_bytes);
     w.sk_ctl[0] = (unsigned*)c;
@@ -340,13 +244,10 @@ static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
     unsigned* bc = c ? (unsigned*)(c + 2 * ctl) : nullptr;
     w.bn_err = bc ? bc + 2 * h->L.size() * MMAD_BN_SYNC_WORDS : nullptr;
     w.l.resize(h->L.size());
-    unsigned* tf = bc ? bc + 2 * h->L.size() * MMAD_BN_SYNC_WORDS + 64 : nullptr;
     for (size_t i = 0; i < h->L.size(); ++i) {
       w.l[i].sync_f = bc ? bc + (2 * i) * MMAD_BN_SYNC_WORDS : nullptr;
       w.l[i].sync_b = bc ? bc + (2 * i + 1) * MMAD_BN_SYNC_WORDS : nullptr;
       w.l[i].fwd_fused = w.l[i].bwd_fused = false;
-      w.l[i].tflag = tf;
-      if (tf) tf += (size_t)(h->L[i].Np / 64) * (h->L[i].Kp / 64);
     }
   }
   w.B = B;
@@ -428,14 +329,25 @@ int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, i
   h->bn_eps = bn_eps;
   h->bn_mom = bn_momentum;
   {
-    const char* e = getenv("MMAD_BN_FOLD");
-    h->fold = e ? (atoi(e) != 0) : (dtype == MMAD_BF16);
-    h->bn_mode = e ? (h->fold ? 1 : 0) : (dtype == MMAD_BF16 ? 2 : 0);
-    const char* m = getenv("MMAD_BN_MODE");
-    if (m && atoi(m) >= 0 && atoi(m) <= 2) {
-      h->bn_mode = atoi(m);
-      h->fold = h->bn_mode != 0 && dtype == MMAD_BF16;   // fold: mode 1, mode 2's fallback
+    // the schedule knobs (include/mmad.h 16-27), read once for this handle
+    const int m = mmad_knob(16);
+    h->fold = dtype == MMAD_BF16;
+    h->bn_mode = dtype == MMAD_BF16 ? 2 : 0;
+    if (m >= 0 && m <= 2) {
+      h->bn_mode = m;
+      h->fold = m != 0 && dtype == MMAD_BF16;   // fold: mode 1, mode 2's fallback
     }
+    h->bn_mode_bwd = mmad_knob(17);
+    h->bn_fused_rows = mmad_knob(18);
+    h->dw_main = mmad_knob(19);
+    h->pair_rows = mmad_knob(20);
+    h->dw_main_ping = mmad_knob(21);
+    h->ev_every = mmad_knob(22);
+    h->loss_side = mmad_knob(23);
+    h->dp_small_at = mmad_knob(24);
+    h->keep_grads = mmad_knob(25);
+    h->side_prio_hi = mmad_knob(26);
+    h->ev_flags_ = ev_flags(mmad_knob(27));
   }
   for (int side = 0; side < 2; ++side) {
     const int n = side == 0 ? n_enc : n_dec;
@@ -510,35 +422,18 @@ int mmad_ae_bind(mmad_ae* h, float* params, float* grads, float* adam_m, float* 
     // lowest priority: the side stream fills CUs the critical chain leaves idle
     int least = 0, greatest = 0;
     MMAD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    // (MMAD_SIDE_PRIO=1: the highest priority instead, for schedule sweeps)
-    const char* sp = getenv("MMAD_SIDE_PRIO");
-    const char* sc = getenv("MMAD_SIDE_CUS");
-    const int side_cus = sc ? atoi(sc) : 0;
-    if (side_cus > 0 && side_cus < 256) {
-      // (schedule experiments) the side stream confined to side_cus CUs, the
-      // same number on each XCD whether the mask bits enumerate CUs XCD-major
-      // or round-robin over XCDs: bit i set iff i % 32 < side_cus / 8
-      uint32_t mask[8] = {};
-      const int per = side_cus / 8 > 0 ? side_cus / 8 : 1;
-      for (int i = 0; i < 256; ++i)
-        if (i % 32 < per) mask[i / 32] |= 1u << (i % 32);
-      MMAD_HIP_CHECK(hipExtStreamCreateWithCUMask(&h->side, 8, mask));
-    } else {
-      MMAD_HIP_CHECK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking,
-                                                 (sp && atoi(sp) == 1) ? greatest : least));
-    }
-    if (h->dw_tail || h->dw_split || h->adam_stream)
-      MMAD_HIP_CHECK(hipStreamCreateWithFlags(&h->tail, hipStreamNonBlocking));
+    // (knob 26: the highest priority instead, for schedule sweeps)
+    MMAD_HIP_CHECK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking,
+                                               h->side_prio_hi ? greatest : least));
     const size_t n = h->L.size();
     h->ev_fork.resize(n);
     h->ev_data.resize(n);
     for (size_t i = 0; i < n; ++i) {
-      MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_fork[i], kEvFlags));
-      MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_data[i], kEvFlags));
+      MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_fork[i], h->ev_flags_));
+      MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_data[i], h->ev_flags_));
     }
-    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_join, kEvFlags));
-    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_loss, kEvFlags));
-    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_tail, kEvFlags));
+    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_join, h->ev_flags_));
+    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_loss, h->ev_flags_));
   }
   return MMAD_OK;
 }
@@ -614,7 +509,7 @@ static int prepare_ws(const mmad_ae* h, int B, int k, void* ws, int64_t ws_bytes
   if (w.bn_mode == 2 && w.Mpd > h->bn_fused_rows) w.bn_mode = h->fold ? 1 : 0;
   if (w.bn_mode == 1 && !h->fold) w.bn_mode = 0;
   w.bn_mode_bwd = (h->bn_mode_bwd >= 0 && h->fold) ? h->bn_mode_bwd : w.bn_mode;
-  if ((splitk_possible(h->dtype) || h->bn_mode == 2 || h->bn_mode_bwd == 2 || h->adam_stream) &&
+  if ((splitk_possible(h->dtype) || h->bn_mode == 2 || h->bn_mode_bwd == 2) &&
       ws != h->ws_zeroed) {
     MMAD_HIP_CHECK(hipMemsetAsync(w.sk_ctl[0], 0, w.sk_ctl_bytes, st));
     const_cast<mmad_ae*>(h)->ws_zeroed = ws;
@@ -633,11 +528,6 @@ static int ae_gemm(const mmad_ae* h, const AeWS& w, int dt, int epi, const void*
   const int r = (h->side && s == h->side) ? 1 : 0;
   ep.sk_slab = w.sk_slab[r];
   ep.sk_ctl = w.sk_ctl[r];
-  if (r == 1) ep.lds_pad = h->side_lds_pad;
-  if (h->tail && s == h->tail) {   // no split-K workspace of its own: never split
-    ep.sk_slab = nullptr;
-    ep.sk_ctl = nullptr;
-  }
   const bool rec = probe >= 0 && probe == h->probe_id && !h->capturing &&
                    2 * h->probe_n < (int)h->probe_ev.size();
   if (rec) MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n], s));
@@ -811,9 +701,6 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
   const int nL = (int)h->L.size();
   hipStream_t side = h->side;
   std::vector<PendingDW> pending;   // side-stream dW GEMMs waiting for a recorded event
-  bool used_tail = false;
-  PendingDW pair_first{};           // main-tail dW of layer 1, launched with layer 0's
-  bool pair_pending = false;
   // layer l's Adam terms for a dW epilogue: the weight tile's (ad_*, unless
   // weights_too is false) and the small segment [bias | gamma | beta]'s
   auto fill_adam = [&](GemmEpi& e, int l, bool weights_too) {
@@ -844,14 +731,6 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     e.gb_stride = bs.stride;
     e.sm_bN = a.N;
     e.sm_bNp = a.Np;
-  };
-  // the flat Adam pass over layer l's weight tile (split layers)
-  auto weight_adam = [&](int l, hipStream_t s_) -> int {
-    const AeLayer& a = h->L[l];
-    const int64_t n = (int64_t)a.Np * a.Kp;
-    return mmad_adam_dyn(n, h->params + a.w_off, h->grads + a.w_off, h->m + a.w_off, h->v + a.w_off,
-                         adam->b1, adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt,
-                         adam_shadow(h, a, w.ping), h->dtype == MMAD_BF16 ? n : 0, w.dyn, s_);
   };
   for (int l = nL - 1; l >= 0; --l) {
     const AeLayer& a = h->L[l];
@@ -885,13 +764,8 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     // the DP exchange and by side-stream dW GEMMs (every ev_every-th layer;
     // the lowest side layer always records, flushing the deferred ones)
     const bool side_dw = adam && !dp && !ping && l >= w.dw_main;
-    const bool split = adam && !dp && !ping && h->tail && l < w.dw_main &&
-                       (h->dw_split > 0 || (h->dw_split < 0 && w.Mpe >= 4096));
-    const bool tail_dw = adam && !dp && !ping && !split && h->tail && h->dw_tail && l > 0 &&
-                         l < w.dw_main;
-    const bool rec = dp || tail_dw || split ||
-                     (side_dw && (h->ev_every <= 1 || l == w.dw_main ||
-                                  (l - w.dw_main) % h->ev_every == 0));
+    const bool rec = dp || (side_dw && (h->ev_every <= 1 || l == w.dw_main ||
+                                        (l - w.dw_main) % h->ev_every == 0));
     if (!adam || dp) {
       // fork: dz_l is complete on the main stream; dW_l overlaps the chain below
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
@@ -899,18 +773,6 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
                      nullptr, PROBE_DW + l));
       if (dp) MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l], side));
-    }
-    if (split && l > 0) {
-      // dz_l is complete on the main stream: dW_l (+ the small-segment Adam)
-      // on the tail stream now, overlapping bwd-data(l)
-      GemmEpi e = dwe;
-      fill_adam(e, l, false);
-      e.tile_force = mmad_tile_adam_main_override() + 1;
-      MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
-      MMAD_HIP_CHECK(hipStreamWaitEvent(h->tail, h->ev_fork[l], 0));
-      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, e, h->tail,
-                     nullptr, PROBE_DW + l));
-      used_tail = true;
     }
     if (l > 0) {
       const AeLayer& p = h->L[l - 1];
@@ -998,96 +860,14 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       // (bwd-data of l); the rest of the chain keeps overlapping it.
       if (rec && (l == 0 || !(h->L[l - 1].bn) || (h->vib && l == h->n_enc)))
         MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
-      if (split) {
-        if (l > 0) {
-          // W_l has been read by bwd-data(l): its Adam on the tail stream
-          MMAD_HIP_CHECK(hipStreamWaitEvent(h->tail, h->ev_data[l], 0));
-          RET_IF(weight_adam(l, h->tail));
-        } else {
-          GemmEpi e = dwe;
-          fill_adam(e, l, false);
-          e.tile_force = mmad_tile_adam_main_override() + 1;
-          RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, e, st,
-                         nullptr, PROBE_DW + l));
-          RET_IF(weight_adam(l, st));
-        }
-        continue;
-      }
       fill_adam(dwe, l, true);
       // the last dW GEMMs of the chain go to the main stream, which is idle
       // by then, instead of queueing behind the side stream's backlog
       const bool on_main = l < w.dw_main;
-      if (tail_dw) {
+      if (on_main) {
         dwe.tile_force = mmad_tile_adam_main_override() + 1;
-        MMAD_HIP_CHECK(hipStreamWaitEvent(h->tail, h->ev_data[l], 0));
-        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, h->tail,
+        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st,
                        nullptr, PROBE_DW + l));
-        used_tail = true;
-      } else if (on_main && h->adam_stream && h->tail) {
-        // dW GEMM (small-segment Adam in its epilogue) publishing its tiles
-        // on the main stream, the weight Adam streamed beside it on the tail
-        // stream, started when the GEMM is (bwd-data(l), which read W_l, is
-        // before it on the main stream)
-        GemmEpi e = dwe;          // (dwe carries the weight tile's Adam terms: drop them)
-        e.ad_p = e.ad_m = e.ad_v = nullptr;
-        e.ad_shadow = nullptr;
-        e.tile_flag = s.tflag;
-        e.tile_force = h->adam_stream_tile + 1;
-        e.dw_nostore = 0;
-        const bool prb = PROBE_DW + l == h->probe_id && !h->capturing &&
-                         2 * h->probe_n < (int)h->probe_ev.size();
-        MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
-        MMAD_HIP_CHECK(hipStreamWaitEvent(h->tail, h->ev_fork[l], 0));
-        if (prb) MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n], st));
-        int cfg = -1;
-        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, e, st, &cfg));
-        GemmEpi c{};
-        fill_adam(c, l, true);
-        c.sm_p = nullptr;                  // the GEMM's epilogue did the small segment
-        c.tile_flag = s.tflag;
-        c.bn_err = w.bn_err;
-        RET_IF(mmad_adam_stream(cfg, h->grads + a.w_off, a.Kp, a.Np, a.Kp, c, h->adam_stream_grid,
-                                h->tail));
-        if (prb) {
-          MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n + 1], h->tail));
-          ++h->probe_n;
-        }
-        used_tail = true;
-      } else if (on_main) {
-        dwe.tile_force = mmad_tile_adam_main_override() + 1;
-        // the tile each of the two tail problems would get on its own
-        auto tail_cfg = [&](int M_, int N_, int K_) {
-          return mmad_gemm_adam_dw_cfg(M_, N_, K_, dwe.tile_force);
-        };
-        if (h->dw_pair && w.dw_main == 2 && l == 1 && !h->capturing) {
-          pair_first = PendingDW{dz, in, a.Np, a.Kp, a.Np, a.Kp, Mp, dwe, l};
-          pair_pending = true;
-        } else if (pair_pending && l == 0 &&
-                   tail_cfg(pair_first.M, pair_first.N, pair_first.K) == tail_cfg(a.Np, a.Kp, Mp) &&
-                   tail_cfg(a.Np, a.Kp, Mp) >= 0) {
-          const int cfg = tail_cfg(a.Np, a.Kp, Mp);
-          const bool prb = (PROBE_DW + 0 == h->probe_id || PROBE_DW + 1 == h->probe_id) &&
-                           !h->capturing && 2 * h->probe_n < (int)h->probe_ev.size();
-          if (prb) MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n], st));
-          RET_IF(mmad_gemm_dispatch_pair(dt, cfg, pair_first.dz, pair_first.lda, pair_first.in,
-                                         pair_first.ldb, pair_first.M, pair_first.N, pair_first.K,
-                                         pair_first.ep, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st));
-          if (prb) {
-            MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n + 1], st));
-            ++h->probe_n;
-            h->probe_mask = 3u;
-          }
-          pair_pending = false;
-        } else {
-          if (pair_pending) {
-            RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, pair_first.dz, pair_first.lda, pair_first.in,
-                           pair_first.ldb, pair_first.M, pair_first.N, pair_first.K, pair_first.ep, st,
-                           nullptr, PROBE_DW + pair_first.layer));
-            pair_pending = false;
-          }
-          RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st,
-                         nullptr, PROBE_DW + l));
-        }
       } else if (ping) {
         MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
@@ -1105,14 +885,10 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       }
     }
   }
-  MMAD_CHECK_ARG(pending.empty() && !pair_pending, "ae backward: deferred dW GEMMs left unissued");
-  // join the side (and tail) streams back into the main stream
+  MMAD_CHECK_ARG(pending.empty(), "ae backward: deferred dW GEMMs left unissued");
+  // join the side stream back into the main stream
   MMAD_HIP_CHECK(hipEventRecord(h->ev_join, side));
   MMAD_HIP_CHECK(hipStreamWaitEvent(st, h->ev_join, 0));
-  if (used_tail) {
-    MMAD_HIP_CHECK(hipEventRecord(h->ev_tail, h->tail));
-    MMAD_HIP_CHECK(hipStreamWaitEvent(st, h->ev_tail, 0));
-  }
   return MMAD_OK;
 }
 
@@ -1239,7 +1015,7 @@ int mmad_ae_train_step_graph(mmad_ae* h, const float* x, int ld_x, int B, int k,
   if (!h->dyn_host) {
     MMAD_HIP_CHECK(hipHostMalloc((void**)&h->dyn_host, sizeof(MmadDyn) * mmad_ae::kDynSlots,
                                  hipHostMallocDefault));
-    for (auto& e : h->dyn_ev) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, kEvFlags));
+    for (auto& e : h->dyn_ev) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, h->ev_flags_));
   }
   const int slot = h->dyn_next;
   h->dyn_next = (slot + 1) % mmad_ae::kDynSlots;
@@ -1315,9 +1091,9 @@ int mmad_ae_set_comm(mmad_ae* h, mmad_comm* c) {
     MMAD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     MMAD_HIP_CHECK(hipStreamCreateWithPriority(&h->cstream, hipStreamNonBlocking, greatest));
     h->ev_dw.resize(h->L.size());
-    for (auto& e : h->ev_dw) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, kEvFlags));
-    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_small, kEvFlags));
-    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_cdone, kEvFlags));
+    for (auto& e : h->ev_dw) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, h->ev_flags_));
+    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_small, h->ev_flags_));
+    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_cdone, h->ev_flags_));
   }
   h->comm = c;
   return MMAD_OK;
@@ -1511,14 +1287,14 @@ int mmad_ae_status(mmad_ae* h, void* ws, int64_t ws_bytes, void* stream) {
   MMAD_CHECK_ARG(h, "ae_status: null handle");
   // no split-K GEMM / fused-BN barrier can have run unless the dtype /
   // override / BN mode allows one
-  if ((!splitk_possible(h->dtype) && h->bn_mode != 2 && h->bn_mode_bwd != 2 && !h->adam_stream) || !ws)
+  if ((!splitk_possible(h->dtype) && h->bn_mode != 2 && h->bn_mode_bwd != 2) || !ws)
     return MMAD_OK;
   AeWS w;
   carve(h, 1, 1, (char*)ws, w);
   MMAD_CHECK_ARG(ws_bytes >= w.bytes, "ae_status: workspace too small");
   for (int r = 0; r < 2; ++r)
     RET_IF(mmad_gemm_read_status(w.sk_ctl[r], (hipStream_t)stream, "ae_status"));
-  if ((h->bn_mode == 2 || h->bn_mode_bwd == 2 || h->adam_stream) && w.bn_err) {
+  if ((h->bn_mode == 2 || h->bn_mode_bwd == 2) && w.bn_err) {
     unsigned word = 0;
     MMAD_HIP_CHECK(hipMemcpyAsync(&word, w.bn_err, sizeof(word), hipMemcpyDeviceToHost, (hipStream_t)stream));
     MMAD_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
@@ -1527,8 +1303,8 @@ int mmad_ae_status(mmad_ae* h, void* ws, int64_t ws_bytes, void* stream) {
       // counters raised) for the next call
       MMAD_HIP_CHECK(hipMemsetAsync(w.sk_ctl[0], 0, w.sk_ctl_bytes, (hipStream_t)stream));
       MMAD_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
-      mmad_set_error("ae_status: a fused BatchNorm column barrier or a streamed-Adam tile wait timed "
-                     "out; the outputs of that call are invalid");
+      mmad_set_error("ae_status: a fused BatchNorm column barrier timed out; the outputs of that "
+                     "call are invalid");
       return MMAD_EHIP;
     }
   }

@@ -29,50 +29,52 @@ const char* mmad_last_error_string(void) { return g_err; }
 int mmad_abi_version(void) { return MMAD_ABI_VERSION; }
 int mmad_pad_granule(void) { return MMAD_PAD; }
 
-// tuning knobs (env defaults, overridable at run time through mmad_tune_set)
-static int g_tile = [] {
-  const char* e = getenv("MMAD_GEMM_TILE");
-  return e ? atoi(e) : -1;
-}();
-static int g_group = [] {
-  const char* e = getenv("MMAD_GEMM_GROUP_M");
-  return e ? atoi(e) : -1;
-}();
-static int g_autotune = [] {
-  const char* e = getenv("MMAD_GEMM_AUTOTUNE");
-  return e ? atoi(e) : 1;
-}();
-int mmad_tile_override() { return g_tile; }
-int mmad_group_override() { return g_group; }
-int mmad_autotune_enabled() { return g_autotune; }
-static int g_dbg = 0;
-int mmad_dbg_override() { return g_dbg; }
-static int g_splitk = [] {
-  const char* e = getenv("MMAD_GEMM_SPLITK");
-  return e ? atoi(e) : 0;
-}();
-int mmad_splitk_override() { return g_splitk; }
-static int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-static int g_splitk_dw = env_int("MMAD_GEMM_SPLITK_DW", 0);
+// Tuning knobs: ONE table, set only through mmad_tune_set (the library reads
+// no environment variables, so every rank of a job runs the same schedule
+// unless its code says otherwise).  GEMM knobs (0-11) are read per dispatch;
+// the executor's schedule knobs (16-27) are copied into a handle when it is
+// created (mmad_ae_create), so a handle keeps one schedule for its lifetime.
+namespace {
+int g_knob[MMAD_KNOB_COUNT] = {
+    -1,    // 0  GEMM tile override (-1 = autotuned)
+    -1,    // 1  XCD tile-group height (-1 = rule)
+    1,     // 2  per-shape autotune on first dispatch
+    0,     // 3  diagnostics bits (tools/gemm_phase; tests)
+    0,     // 4  split-K override (0 = shape rule)
+    -2,    // 5  tile of the Adam-fused dW GEMMs (-2 = shape rule, -1 = autotuned)
+    -1,    // 6  tile of the bwd-data GEMMs
+    -1,    // 7  tile of the forward GEMMs
+    -1,    // 8  tile of the main-stream Adam-fused dW GEMMs (-1 = knob 5)
+    0,     // 9  split-K override of the dW GEMMs
+    0,     // 10 dW split rule: target 64x64-tile blocks (0 = no split)
+    8,     // 11 dW split rule: minimum K stages per slice
+    0, 0, 0, 0,   // 12-15 retired (measured-slower experiments, removed in round 3)
+    -1,    // 16 train-mode BN schedule (-1 = dtype default: bf16 fused, fp32 apply; 0 apply, 1 fold, 2 fused)
+    -1,    // 17 backward BN schedule (-1 = the forward's; 2 = fused into the bwd-data GEMMs)
+    2048,  // 18 fused BN up to this many padded rows (fold above)
+    2,     // 19 dW GEMMs of the last layers run on the main stream
+    4096,  // 20 ping-pong weight shadows from this many padded rows
+    1,     // 21 main-stream dW GEMMs when ping-ponging
+    2,     // 22 record the bwd-data event every n-th side-stream layer
+    1,     // 23 reduce the loss on the side stream after the forward
+    1,     // 24 DP: exchange the small bucket after the bwd-data GEMM of this layer
+    0,     // 25 also materialise dW in the fused step (grads buffer)
+    0,     // 26 side stream at the highest priority (schedule sweeps)
+    0,     // 27 executor events with the system-scope fence
+};
+}  // namespace
+int mmad_knob(int k) { return g_knob[k]; }
+int mmad_tile_override() { return g_knob[0]; }
+int mmad_group_override() { return g_knob[1]; }
+int mmad_autotune_enabled() { return g_knob[2]; }
+int mmad_dbg_override() { return g_knob[3]; }
+int mmad_splitk_override() { return g_knob[4]; }
+int mmad_splitk_dw_override() { return g_knob[9]; }
 // dW split-K target blocks (0 = no split): 512 paid before the dW loop stopped
 // draining its LDS ring every K stage; since then no split measures faster
 // (VIB B=4096 0.991-0.996 vs 1.013 ms/step with the split tail off; r02ae_*)
-static int g_splitk_dw_blocks = env_int("MMAD_SPLITK_DW_BLOCKS", 0);
-static int g_splitk_dw_min_stages = env_int("MMAD_SPLITK_DW_MIN_STAGES", 8);
-static int g_dw_ws = env_int("MMAD_DW_WS", 0);
-static int g_dw_ws_blocks = env_int("MMAD_DW_WS_BLOCKS", 256);
-static int g_adam_prefetch = env_int("MMAD_ADAM_PREFETCH", 0);
-static int g_adam_nt = env_int("MMAD_ADAM_NT", 0);
-int mmad_adam_nt_enabled() { return g_adam_nt; }
-int mmad_dw_ws_enabled() { return g_dw_ws; }
-int mmad_dw_ws_blocks() { return g_dw_ws_blocks; }
-int mmad_adam_prefetch_enabled() { return g_adam_prefetch; }
-int mmad_splitk_dw_override() { return g_splitk_dw; }
-int mmad_splitk_dw_blocks() { return g_splitk_dw_blocks; }
-int mmad_splitk_dw_min_stages() { return g_splitk_dw_min_stages; }
+int mmad_splitk_dw_blocks() { return g_knob[10]; }
+int mmad_splitk_dw_min_stages() { return g_knob[11]; }
 // tile for the dW GEMMs with the fused Adam epilogue (the autotuner times
 // them without Adam, which under-weights the epilogue's HBM traffic: it picks
 // 128x128 for the large layers, 208 blocks for 256 CUs).  Default (-2) = a
@@ -81,57 +83,39 @@ int mmad_splitk_dw_min_stages() { return g_splitk_dw_min_stages; }
 // everywhere (0.522 vs 0.529 ms/step, tools/tile_adam_sweep.py); B=4096:
 // 67 vs 87 us at 1658x2048, 63 vs 78 at 1268x1658, 64x64 better below
 // (profiles/r02j_splitk_dw4096_vib.log).
-static int g_tile_adam = [] {
-  const char* e = getenv("MMAD_GEMM_TILE_ADAM");
-  return e ? atoi(e) : -2;
-}();
-int mmad_tile_adam_override() { return g_tile_adam; }
+int mmad_tile_adam_override() { return g_knob[5]; }
 int mmad_tile_adam_for(int Mp, int Np, int K) {
-  if (g_tile_adam != -2) return g_tile_adam;
+  if (g_knob[5] != -2) return g_knob[5];
   return (K >= 2048 && (long)Mp * Np >= 1500000L) ? 0 : 3;
 }
 // tile of the Adam-fused dW GEMMs that run on the main stream at the end of
 // the backward (nothing else on the GPU then; -1 = same as knob 5)
-static int g_tile_adam_main = [] {
-  const char* e = getenv("MMAD_GEMM_TILE_ADAM_MAIN");
-  return e ? atoi(e) : -1;
-}();
-int mmad_tile_adam_main_override() { return g_tile_adam_main; }
+int mmad_tile_adam_main_override() { return g_knob[8]; }
 // per-epilogue tile overrides (-1 = autotuned): bwd-data GEMMs, forward GEMMs
-static int g_tile_bwd_data = [] {
-  const char* e = getenv("MMAD_GEMM_TILE_BWD_DATA");
-  return e ? atoi(e) : -1;
-}();
-static int g_tile_fwd = [] {
-  const char* e = getenv("MMAD_GEMM_TILE_FWD");
-  return e ? atoi(e) : -1;
-}();
 int mmad_tile_epi_override(int epi) {
-  if (epi == GEMM_EPI_BWD_DATA) return g_tile_bwd_data;
-  if (epi == GEMM_EPI_FWD || epi == GEMM_EPI_MSE) return g_tile_fwd;
+  if (epi == GEMM_EPI_BWD_DATA) return g_knob[6];
+  if (epi == GEMM_EPI_FWD || epi == GEMM_EPI_MSE) return g_knob[7];
   return -1;
 }
 
+static bool knob_valid(int knob) {
+  return knob >= 0 && knob < MMAD_KNOB_COUNT && !(knob >= 12 && knob <= 15);
+}
 int mmad_tune_set(int knob, int value) {
-  switch (knob) {
-    case 0: g_tile = value; return MMAD_OK;
-    case 1: g_group = value; return MMAD_OK;
-    case 2: g_autotune = value; return MMAD_OK;
-    case 3: g_dbg = value; return MMAD_OK;
-    case 4: g_splitk = value; return MMAD_OK;
-    case 5: g_tile_adam = value; return MMAD_OK;
-    case 6: g_tile_bwd_data = value; return MMAD_OK;
-    case 7: g_tile_fwd = value; return MMAD_OK;
-    case 8: g_tile_adam_main = value; return MMAD_OK;
-    case 9: g_splitk_dw = value; return MMAD_OK;
-    case 10: g_splitk_dw_blocks = value; return MMAD_OK;
-    case 11: g_splitk_dw_min_stages = value; return MMAD_OK;
-    case 12: g_dw_ws = value; return MMAD_OK;
-    case 13: g_dw_ws_blocks = value; return MMAD_OK;
-    case 14: g_adam_prefetch = value; return MMAD_OK;
-    case 15: g_adam_nt = value; return MMAD_OK;
-    default: mmad_set_error("tune_set: unknown knob %d", knob); return MMAD_EINVAL;
+  if (!knob_valid(knob)) {
+    mmad_set_error("tune_set: unknown knob %d", knob);
+    return MMAD_EINVAL;
   }
+  g_knob[knob] = value;
+  return MMAD_OK;
+}
+int mmad_tune_get(int knob, int* value) {
+  if (!knob_valid(knob) || !value) {
+    mmad_set_error("tune_get: unknown knob %d", knob);
+    return MMAD_EINVAL;
+  }
+  *value = g_knob[knob];
+  return MMAD_OK;
 }
 
 int mmad_gemm_splitk_for(int Mp, int Np, int K, int dtype, int epi) {

@@ -79,8 +79,6 @@ struct GemmEpi {
   int splitk;
   int tiles_n, group_m;
   int tile_force;        // caller's tile choice + 1 (0 = none; ignored if it does not fit)
-  int lds_pad;           // extra (unused) dynamic LDS per workgroup: caps the
-                         // workgroups of this launch per CU (side-stream dW GEMMs)
   // graph-captured step (nullable): MSE target = dyn->x, Adam step terms
   // from dyn (see MmadDyn)
   const MmadDyn* dyn;
@@ -112,17 +110,12 @@ struct GemmEpi {
   float* bn_dbeta;
   float* bn_dbpart;
   int bn_act;            // BWD_DATA: the BN producer's activation (act' from a)
-  int apf;               // set by the launcher: Adam-state prefetch under the K loop (knob 14)
-  int ad_nt;             // set by the launcher: non-temporal Adam-state loads/stores (knob 15)
-  // BWD_WEIGHT without ad_p: the fp32 tile is stored write-through and the
-  // block raises tile_flag[blockIdx] for the streamed Adam (mmad_adam_stream)
-  unsigned* tile_flag;
-  int dbg;               // diagnostics (tools/gemm_sweep): 1 skip main loop, 2 skip epilogue,
+  int dbg;               // diagnostics (tools/gemm_phase): 1 skip main loop, 2 skip epilogue,
                          // 4 force the split-K combine's timeout path (tests),
-                         // 8 skip the FWD Welford partial stores (tools/gemm_phase),
-                         // 16 no Adam-state prefetch
+                         // 8 skip the FWD Welford partial stores
 };
 
+int mmad_knob(int k);          // the tune table (mmad_tune_set)
 int mmad_group_override();
 
 int mmad_tile_override();
@@ -132,10 +125,6 @@ int mmad_splitk_override();   // 0 = shape rule; 1, 2, 4, 8, 16 = forced split f
 int mmad_splitk_dw_override();     // the same for the dW GEMMs only (knob 9)
 int mmad_splitk_dw_blocks();       // dW split rule: target 64x64-tile blocks (knob 10)
 int mmad_splitk_dw_min_stages();   // dW split rule: minimum K stages per slice (knob 11)
-int mmad_dw_ws_enabled();          // Adam-fused dW GEMMs on the warp-specialised kernel (knob 12)
-int mmad_dw_ws_blocks();           // its persistent grid cap (knob 13)
-int mmad_adam_prefetch_enabled();  // Adam state loaded under the dW K loop (knob 14)
-int mmad_adam_nt_enabled();        // non-temporal Adam-state accesses in the dW epilogue (knob 15)
 int mmad_tile_adam_override();  // >= 0: tile of the Adam-fused dW GEMMs (-2: shape rule)
 int mmad_tile_adam_for(int Mp, int Np, int K);   // ... for a shape
 int mmad_tile_adam_main_override();  // >= 0: ... of those on the main stream
@@ -170,16 +159,5 @@ int mmad_gemm_read_status(unsigned* ctl, hipStream_t s, const char* who);
 bool mmad_gemm_bn_fusable(int dtype, int epi, int Mp, int Np);
 
 // cfg_used (nullable) receives the tile configuration launched
-// Adam over a flagged dW GEMM's tiles as they complete (launch on another
-// stream AFTER the GEMM; grid rounded to a multiple of 8, <= one block per CU)
-int mmad_adam_stream(int cfg, const float* g, int ld, int Mp, int Np, const GemmEpi& ep, int grid,
-                     hipStream_t s);
-// tile configuration of an Adam-fused dW GEMM under the static rules (-1: autotuned)
-int mmad_gemm_adam_dw_cfg(int Mp, int Np, int K, int tile_force);
-// two Adam-fused / plain dW GEMMs (EPI_BWD_WEIGHT) in one launch, tile configuration cfg
-int mmad_gemm_dispatch_pair(int dtype, int cfg, const void* A0, int lda0, const void* B0, int ldb0,
-                            int Mp0, int Np0, int K0, const GemmEpi& e0, const void* A1, int lda1,
-                            const void* B1, int ldb1, int Mp1, int Np1, int K1, const GemmEpi& e1,
-                            hipStream_t s);
 int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,
                        int Np, int K, const GemmEpi& ep, hipStream_t s, int* cfg_used = nullptr);

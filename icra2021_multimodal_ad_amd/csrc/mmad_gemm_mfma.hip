@@ -59,8 +59,6 @@ template <> struct Cfg<2> { static constexpr int BM = 128, BN = 256, WM = 2, WN 
 template <> struct Cfg<3> { static constexpr int BM = 64, BN = 64, WM = 2, WN = 2, NS = 4, NT = 256; };
 template <> struct Cfg<4> { static constexpr int BM = 64, BN = 128, WM = 2, WN = 2, NS = 5, NT = 256; };
 template <> struct Cfg<5> { static constexpr int BM = 128, BN = 128, WM = 2, WN = 2, NS = 4, NT = 256; };
-// the MMA half of the warp-specialised dW + Adam kernel (mmad_dw_adam_ws_kernel)
-template <> struct Cfg<6> { static constexpr int BM = 64, BN = 64, WM = 2, WN = 2, NS = 7, NT = 256; };
 constexpr int NCFG = 6;
 constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128};
 constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128};
@@ -190,22 +188,8 @@ __device__ __forceinline__ floatx4 frag_f32(const char* img, int rbase, int kc, 
   }
 }
 
-// main-loop schedule variants (build-time, measurement): 0 = every phase
-// pinned by sched_barrier(0) (default); 1 = compiler-scheduled phases; 2 = 1
-// + s_setprio(1) around each MFMA half; 3 = 0 + s_setprio
-#ifndef MMAD_LOOP_VARIANT
-#define MMAD_LOOP_VARIANT 0
-#endif
-#if MMAD_LOOP_VARIANT == 1 || MMAD_LOOP_VARIANT == 2
-#define MMAD_SB() do { } while (0)
-#else
+// every phase of the main loop pinned in issue order
 #define MMAD_SB() __builtin_amdgcn_sched_barrier(0)
-#endif
-#if MMAD_LOOP_VARIANT >= 2
-#define MMAD_PRIO(x) __builtin_amdgcn_s_setprio(x)
-#else
-#define MMAD_PRIO(x) do { } while (0)
-#endif
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -345,11 +329,6 @@ __device__ __forceinline__ bool col_wait(unsigned* ctr, unsigned gen0, unsigned*
   return shw[0] != 0u;
 }
 
-// Adam-state prefetch under the K loop (knob 14, default off: the held p/m/v
-// registers cost more than the hidden round trip, 36.6 vs 32.9 us on the
-// largest c2 layer; dbg bit 16 turns it off per launch)
-__device__ __forceinline__ bool mmad_apf_on(const GemmEpi& ep) { return ep.apf && !(ep.dbg & 16); }
-
 }  // namespace
 
 // -------------------------------------------------------------------------
@@ -359,8 +338,7 @@ __device__ __forceinline__ bool mmad_apf_on(const GemmEpi& ep) { return ep.apf &
 // dW GEMM contracts the raw activation and fixes up in the epilogue
 // (dW = scale[k] * acc + shift[k] * db[n]).  Every GEMM is a plain MFMA
 // contraction.
-// The body of one output tile; `bid` / `nblk` = this problem's block index /
-// block count (mmad_gemm_kernel: the grid; mmad_gemm_pair_kernel: its share).
+// The body of one output tile; `bid` / `nblk` = the block index / block count.
 template <typename T, typename TO, bool AK, bool BK_, int CFG, int EPI>
 __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, const T* __restrict__ B,
                                           int ldb, int K, const GemmEpi& ep, const int bid,
@@ -497,38 +475,12 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   // hipcc's lgkmcnt bookkeeping stays exact, and sched_barriers pin the order.
   using FR = typename SubFrag<T>::F;
   const int ra = wm * 16 * TM, rb = wn * 16 * TN;
-  // Adam-fused dW on the 64x64 tile: the tile's p/m/v (4 chunks per thread)
-  // are loaded into registers right after stage 0 has landed, so their HBM
-  // round trip runs under the first NS-1 K stages instead of after the loop.
-  // In issue order they sit behind stages 1..NS-1, so only the waits for
-  // those stages (iterations t <= NS-2) allow APF more newer operations; the
-  // wait for stage NS (older than nothing of them) retires them as well.
-  constexpr int APF_IT = (EPI == GEMM_EPI_BWD_WEIGHT && sizeof(TO) == 4)
-                             ? BM * (BN * (int)sizeof(TO) / 16) / NT : 0;
-  constexpr bool APF_OK = APF_IT > 0 && APF_IT <= 4;
-  constexpr int APF = APF_OK ? 3 * APF_IT : 0;          // vm ops: p, m, v chunks
-  static_assert((NS - 2) * NL + APF <= 63, "vmcnt range");
-  floatx4 aP[APF_OK ? APF_IT : 1], aM[APF_OK ? APF_IT : 1], aV[APF_OK ? APF_IT : 1];
-  const bool apf = APF_OK && ep.ad_p && S == 1 && nt >= 2 * NS - 1 && mmad_apf_on(ep);
   if (nt > 0) {
 #pragma unroll
     for (int s = 0; s < NS; ++s)
       if (s < nt) issue(s);
     if (nt >= NS) wait_vmcnt<(NS - 1) * NL>();
     else wait_vmcnt<0>();
-    if constexpr (APF_OK) {
-      if (apf) {
-        constexpr int CPRA = BN * (int)sizeof(TO) / 16;
-#pragma unroll
-        for (int u = 0; u < APF_IT; ++u) {
-          const int idx = u * NT + tid;
-          const size_t off = (size_t)(m0 + idx / CPRA) * ep.ldo + n0 + (idx % CPRA) * 4;
-          aP[u] = *(const floatx4*)(ep.ad_p + off);
-          aM[u] = *(const floatx4*)(ep.ad_m + off);
-          aV[u] = *(const floatx4*)(ep.ad_v + off);
-        }
-      }
-    }
     block_barrier();
     FR f0a[TM], f0b[TN], f1a[TM], f1b[TN];
     read_sub<T, AK, BK_, NAT, BM, BN, TM, TN>(smem, smem + IA::BYTES, ra, rb, 0, lane, f0a, f0b);
@@ -536,20 +488,15 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
     auto step = [&](int t, auto issue_c, auto last_c) {
       constexpr bool ISSUE = decltype(issue_c)::value, LAST = decltype(last_c)::value;
       const char* sa = smem + (t % NS) * SLOT;
-      MMAD_PRIO(1);
       mma_half<T, TM, TN, 0>(acc, f0a, f0b);
-      MMAD_PRIO(0);
       MMAD_SB();
       read_sub<T, AK, BK_, NAT, BM, BN, TM, TN>(sa, sa + IA::BYTES, ra, rb, 1, lane, f1a, f1b);
       MMAD_SB();
-      MMAD_PRIO(1);
       mma_half<T, TM, TN, 1>(acc, f0a, f0b);
-      MMAD_PRIO(0);
       MMAD_SB();
       if constexpr (!LAST) {
         if constexpr (ISSUE) {
-          if (APF_OK && apf && t <= NS - 2) wait_vmcnt<(NS - 2) * NL + APF>();
-          else wait_vmcnt<(NS - 2) * NL>();
+          wait_vmcnt<(NS - 2) * NL>();
         } else {
           wait_tail<NL>(nt - t - 2);
         }
@@ -558,18 +505,14 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         if constexpr (ISSUE) issue(t + NS);
         MMAD_SB();
       }
-      MMAD_PRIO(1);
       mma_half<T, TM, TN, 0>(acc, f1a, f1b);
-      MMAD_PRIO(0);
       MMAD_SB();
       if constexpr (!LAST) {
         const char* sn = smem + ((t + 1) % NS) * SLOT;
         read_sub<T, AK, BK_, NAT, BM, BN, TM, TN>(sn, sn + IA::BYTES, ra, rb, 0, lane, f0a, f0b);
       }
       MMAD_SB();
-      MMAD_PRIO(1);
       mma_half<T, TM, TN, 1>(acc, f1a, f1b);
-      MMAD_PRIO(0);
       MMAD_SB();
     };
     using T_ = std::true_type;
@@ -885,7 +828,6 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
     // (the three state arrays may alias as far as the compiler knows).
     constexpr int AG = ITERS < 4 ? ITERS : 4;
     static_assert(ITERS % AG == 0, "Adam chunk groups");
-    static_assert(!APF_OK || ITERS == APF_IT, "Adam prefetch layout");
 #pragma unroll
     for (int i0 = 0; i0 < ITERS; i0 += AG) {
       floatx4 P[AG], Mm[AG], Vv[AG];
@@ -895,20 +837,9 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         const int idx = (i0 + u) * NT + tid;
         const int rl = idx / CPR, ch = idx % CPR;
         off[u] = (size_t)(m0 + rl) * ep.ldo + n0 + ch * OEPC;
-        if (APF_OK && apf) {
-          P[u] = aP[(i0 + u) % (APF_OK ? APF_IT : 1)];
-          Mm[u] = aM[(i0 + u) % (APF_OK ? APF_IT : 1)];
-          Vv[u] = aV[(i0 + u) % (APF_OK ? APF_IT : 1)];
-        } else if (ep.ad_nt) {
-          // streaming state: keep the K loop's operand panels in L2
-          P[u] = __builtin_nontemporal_load((const floatx4*)(ep.ad_p + off[u]));
-          Mm[u] = __builtin_nontemporal_load((const floatx4*)(ep.ad_m + off[u]));
-          Vv[u] = __builtin_nontemporal_load((const floatx4*)(ep.ad_v + off[u]));
-        } else {
-          P[u] = *(const floatx4*)(ep.ad_p + off[u]);
-          Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
-          Vv[u] = *(const floatx4*)(ep.ad_v + off[u]);
-        }
+        P[u] = *(const floatx4*)(ep.ad_p + off[u]);
+        Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
+        Vv[u] = *(const floatx4*)(ep.ad_v + off[u]);
       }
 #pragma unroll
       for (int u = 0; u < AG; ++u) {
@@ -921,17 +852,10 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         bf16x4 sh;
 #pragma unroll
         for (int e = 0; e < 4; ++e) sh[e] = (bf16)P[u][e];
-        if (ep.ad_nt) {
-          __builtin_nontemporal_store(P[u], (floatx4*)(ep.ad_p + off[u]));
-          __builtin_nontemporal_store(Mm[u], (floatx4*)(ep.ad_m + off[u]));
-          __builtin_nontemporal_store(Vv[u], (floatx4*)(ep.ad_v + off[u]));
-          if (ep.ad_shadow) __builtin_nontemporal_store(sh, (bf16x4*)((bf16*)ep.ad_shadow + off[u]));
-        } else {
-          *(floatx4*)(ep.ad_p + off[u]) = P[u];
-          *(floatx4*)(ep.ad_m + off[u]) = Mm[u];
-          *(floatx4*)(ep.ad_v + off[u]) = Vv[u];
-          if (ep.ad_shadow) *(bf16x4*)((bf16*)ep.ad_shadow + off[u]) = sh;
-        }
+        *(floatx4*)(ep.ad_p + off[u]) = P[u];
+        *(floatx4*)(ep.ad_m + off[u]) = Mm[u];
+        *(floatx4*)(ep.ad_v + off[u]) = Vv[u];
+        if (ep.ad_shadow) *(bf16x4*)((bf16*)ep.ad_shadow + off[u]) = sh;
       }
     }
   } else {
@@ -954,12 +878,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
       const int row = m0 + rl;
       const int col = n0 + ch * OEPC;
-      if (EPI == GEMM_EPI_BWD_WEIGHT && ep.tile_flag) {
-        // handed to the streamed Adam (mmad_adam_stream_kernel): write-through
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            out + (size_t)m0 * ep.ldo, 0, BM * ep.ldo * (int)sizeof(TO), 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b128(v, rs, (rl * ep.ldo + col) * (int)sizeof(TO), 0, 16 /*sc1*/);
-      } else if (out) {
+      if (out) {
         *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
       }
       if constexpr (EPI == GEMM_EPI_SCORE) {
@@ -989,13 +908,6 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         for (int o = 1; o < CPR128; o <<= 1) sq += __shfl_xor(sq, o);
         if (ch % CPR128 == 0) ep.rowsq[(size_t)(col / 128) * ep.ldrow + row] = sq;
       }
-    }
-    if (EPI == GEMM_EPI_BWD_WEIGHT && ep.tile_flag) {
-      // every wave's sc1 tile stores landed, then one lane raises this
-      // block's flag (MI355X_MICROARCH.md hand-off table, row 1)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) __hip_atomic_store(ep.tile_flag + bid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if constexpr (EPI == GEMM_EPI_FWD) {
@@ -1305,419 +1217,6 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   gemm_body<T, TO, AK, BK_, CFG, EPI>(A, lda, B, ldb, K, ep, blockIdx.x, gridDim.x);
 }
 
-// Two independent problems of one epilogue and tile configuration in ONE
-// launch: blocks [0, n0) run problem 0, the rest problem 1 (the main-stream
-// tail's two Adam-fused dW GEMMs: one grid, so the second problem's blocks
-// fill the first one's last partial wave, and one launch less).  Each
-// problem keeps its own XCD-aware tile order and partial-sum orders, so the
-// results are those of two separate launches bit for bit.
-struct GemmPairArgs {
-  const void *A0, *B0, *A1, *B1;
-  int lda0, ldb0, K0, lda1, ldb1, K1, n0;
-  GemmEpi ep0, ep1;
-};
-template <typename T, typename TO, bool AK, bool BK_, int CFG, int EPI>
-__global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_pair_kernel(GemmPairArgs p) {
-  if ((int)blockIdx.x < p.n0)
-    gemm_body<T, TO, AK, BK_, CFG, EPI>((const T*)p.A0, p.lda0, (const T*)p.B0, p.ldb0, p.K0, p.ep0,
-                                        blockIdx.x, p.n0);
-  else
-    gemm_body<T, TO, AK, BK_, CFG, EPI>((const T*)p.A1, p.lda1, (const T*)p.B1, p.ldb1, p.K1, p.ep1,
-                                        blockIdx.x - p.n0, gridDim.x - p.n0);
-}
-
-// -------------------------------------------------------------------------
-// dW GEMM + fused Adam, warp-specialised and persistent (bf16 operands).
-//
-// The Adam-fused dW GEMM of mmad_gemm_kernel runs its K loop and then streams
-// the tile's Adam state (26 B per parameter) in the same waves, so HBM idles
-// during the loop and the MFMAs idle during the stream (in-situ 39 us for
-// 1658x2048 at B=1024: 26 % MFMA-busy, half the achievable HBM rate,
-// profiles/r02p_pmc_dw.json).  Here a 512-thread workgroup holds 4 MMA waves
-// (a 64x64 dW tile, 32x32 per wave, a 7-stage LDS-DMA ring, the same K order
-// as mmad_gemm_kernel: bit-identical results; a 128x64 tile spills with the
-// Adam state in registers) and 4 Adam waves, and walks tiles
-// vt = blockIdx.x + j * gridDim.x:
-//   * during tile j's K loop the Adam waves load tile j's p / m / v into
-//     registers (their own vmcnt: the MMA waves' counted waits never see
-//     these loads) and update tile j-1 from the fp32 dW tile the MMA waves left
-//     in LDS, one 4-wide chunk per loop barrier;
-//   * after the loop the MMA waves apply the BN-producer fix-up and stage
-//     dW in LDS; the last tile's update drains after the walk.
-// Both roles run the same barrier sequence (every s_barrier counts all 8
-// waves).  Measured (tuning knob 12, off by default): 56.6 us vs 38.0 us for
-// the plain kernel at 1658x2048, B=1024, cold Adam state (81 us with a
-// 128-workgroup grid; profiles/r02t_*): one 130 KB workgroup per CU keeps a
-// single tile's K loop in flight where the plain kernel runs two 64 KB
-// workgroups per CU, and the K loop is the latency-bound part.  The layer's small segment [bias | gamma | beta] is updated by the
-// Adam waves as in mmad_gemm_kernel (tile-indexed, every element once).
-template <int CFG>
-__global__ __launch_bounds__(2 * Cfg<CFG>::NT, 1) void mmad_dw_adam_ws_kernel(
-    const bf16* __restrict__ A, int lda, const bf16* __restrict__ B, int ldb, int K, GemmEpi ep,
-    int ntiles) {
-  using C = Cfg<CFG>;
-  constexpr int BM = C::BM, BN = C::BN, WM = C::WM, WN = C::WN, NS = C::NS, NT = C::NT;
-  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
-  using IA = Img<bf16, false, BM, NT>;
-  using IB = Img<bf16, false, BN, NT>;
-  constexpr int SLOT = IA::BYTES + IB::BYTES;
-  constexpr int NL = IA::CHUNKS + IB::CHUNKS;
-  constexpr int OSTRIDE = BN * 4 + 16;                 // fp32 dW staging row
-  constexpr int HBYTES = BM * OSTRIDE;
-  constexpr int CPR = BN * 4 / 16;                     // 16-B chunks per dW row
-  constexpr int ITA = BM * CPR / NT;                   // Adam chunks per Adam thread
-  constexpr int QG = 32;
-  constexpr int LDS_BYTES = NS * SLOT + HBYTES + 2 * BM * 4;
-  static_assert((NS - 1) * NL <= 63, "vmcnt range");
-  static_assert(LDS_BYTES <= 163840, "LDS budget");
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-  char* H = smem + NS * SLOT;                          // fp32 dW tile of the previous tile
-  float* dbl = (float*)(H + HBYTES);                   // [2][BM] db of the rows of tile j & 1
-
-  const int tid = threadIdx.x;
-  const bool mma = tid < NT;
-  const int t2 = mma ? tid : tid - NT;                 // index within the role
-  const int lane = tid & 63, w = t2 >> 6;
-  const int wm = w / WN, wn = w % WN;
-  const int g = lane >> 4, c = lane & 15;
-  const int grid = gridDim.x, bid = blockIdx.x;
-  const int my_tiles = bid < ntiles ? (ntiles - bid + grid - 1) / grid : 0;
-  const int nt = K / IA::BK;
-
-  float ad_step = ep.ad_step, ad_bc2 = ep.ad_bc2;
-  if (ep.dyn) {
-    ad_step = ep.dyn->ad_step;
-    ad_bc2 = ep.dyn->ad_bc2;
-  }
-  // logical tile -> (m0, n0): the XCD-aware grouped order of mmad_gemm_kernel
-  // (grid is a multiple of 8, so every tile of this block maps to its XCD)
-  auto coords = [&](int vt, int& m0, int& n0, int& tnn) {
-    const int q = ntiles >> 3, r = ntiles & 7, xcd = vt & 7;
-    const int lt = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (vt >> 3);
-    const int tiles_m = ntiles / ep.tiles_n;
-    const int per_group = ep.group_m * ep.tiles_n;
-    const int first_m = (lt / per_group) * ep.group_m;
-    const int gsz = min(tiles_m - first_m, ep.group_m);
-    const int tmm = first_m + (lt % per_group) % gsz;
-    tnn = (lt % per_group) / gsz;
-    m0 = tmm * BM;
-    n0 = tnn * BN;
-    return lt;
-  };
-
-  // the small segment of tile (lt, rows m0p.., column tile tnp): bias rows
-  // (tn == 0 tiles, g = db of those rows) and gamma | beta spread over tiles
-  auto small_segment = [&](int ltp, int m0p, int tnp, const float* dbrow) {
-    if (!ep.sm_p) return;
-    if (tnp == 0 && t2 < BM && m0p + t2 < ep.sm_bNp) {
-      const int n = m0p + t2;
-      float gg = ep.gb_src ? (n < ep.sm_bN ? dbrow[t2] : 0.f) : ep.sm_g[n];
-      if (ep.gb_src) ep.sm_g[n] = gg;
-      float pp = ep.sm_p[n], mm = ep.sm_m[n], vv = ep.sm_v[n];
-      adam_elem(pp, mm, vv, gg, ep.ad_b1, ep.ad_b2, ep.ad_eps, ad_step, ad_bc2);
-      ep.sm_p[n] = pp;
-      ep.sm_m[n] = mm;
-      ep.sm_v[n] = vv;
-    }
-    for (int q = ltp * NT + t2; ep.sm_bNp + q * 4 < ep.sm_n; q += ntiles * NT) {
-      const int i4 = ep.sm_bNp + q * 4;
-      const floatx4 gg = *(const floatx4*)(ep.sm_g + i4);
-      floatx4 pp = *(floatx4*)(ep.sm_p + i4), mm = *(floatx4*)(ep.sm_m + i4);
-      floatx4 vv = *(floatx4*)(ep.sm_v + i4);
-      adam4(pp, mm, vv, gg, ep.ad_b1, ep.ad_b2, ep.ad_eps, ad_step, ad_bc2);
-      *(floatx4*)(ep.sm_p + i4) = pp;
-      *(floatx4*)(ep.sm_m + i4) = mm;
-      *(floatx4*)(ep.sm_v + i4) = vv;
-    }
-  };
-
-  // The two roles run separate loops (disjoint register lifetimes: the MMA
-  // accumulators / fragments and the Adam state are never live together)
-  // with the same barrier sequence per tile j: B0, nt - 1 loop barriers (only
-  // for a real tile), B_end.  j = my_tiles is the Adam waves' drain.
-  if (mma) {
-    using FR = typename SubFrag<bf16>::F;
-    const int ra = wm * 16 * TM, rb = wn * 16 * TN;
-    for (int j = 0; j <= my_tiles; ++j) {
-      const bool has = j < my_tiles;
-      int m0 = 0, n0 = 0, tn = 0;
-      if (has) (void)coords(bid + j * grid, m0, n0, tn);
-      floatx4 acc[TM][TN];
-      float e_s[TN], e_t[TN];
-      if (has) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int jj = 0; jj < TN; ++jj) acc[i][jj] = floatx4{0.f, 0.f, 0.f, 0.f};
-        if (ep.b_scale) {   // epilogue constants first (their latency hides under the loop)
-#pragma unroll
-          for (int jj = 0; jj < TN; ++jj) {
-            const int col = n0 + wn * 16 * TN + jj * 16 + c;
-            e_s[jj] = ep.b_scale[col];
-            e_t[jj] = ep.b_shift[col];
-          }
-        }
-#pragma unroll
-        for (int st = 0; st < NS; ++st)
-          if (st < nt) {
-            char* base = smem + st * SLOT;
-            issue_stage<bf16, false, BM, NT>(base, A, lda, m0, st * IA::BK, t2);
-            issue_stage<bf16, false, BN, NT>(base + IA::BYTES, B, ldb, n0, st * IA::BK, t2);
-          }
-        if (nt >= NS) wait_vmcnt<(NS - 1) * NL>();
-        else wait_vmcnt<0>();
-      }
-      block_barrier();                                 // B0: stage 0 visible
-      if (has) {
-        FR f0a[TM], f0b[TN], f1a[TM], f1b[TN];
-        read_sub<bf16, false, false, true, BM, BN, TM, TN>(smem, smem + IA::BYTES, ra, rb, 0, lane, f0a, f0b);
-        wait_lgkm0();
-        auto issue = [&](int st) {
-          char* base = smem + (st % NS) * SLOT;
-          issue_stage<bf16, false, BM, NT>(base, A, lda, m0, st * IA::BK, t2);
-          issue_stage<bf16, false, BN, NT>(base + IA::BYTES, B, ldb, n0, st * IA::BK, t2);
-        };
-        auto step = [&](int t, auto issue_c, auto last_c) {
-          constexpr bool ISSUE = decltype(issue_c)::value, LAST = decltype(last_c)::value;
-          const char* sa = smem + (t % NS) * SLOT;
-          mma_half<bf16, TM, TN, 0>(acc, f0a, f0b);
-          __builtin_amdgcn_sched_barrier(0);
-          read_sub<bf16, false, false, true, BM, BN, TM, TN>(sa, sa + IA::BYTES, ra, rb, 1, lane, f1a, f1b);
-          __builtin_amdgcn_sched_barrier(0);
-          mma_half<bf16, TM, TN, 1>(acc, f0a, f0b);
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (!LAST) {
-            if constexpr (ISSUE) wait_vmcnt<(NS - 2) * NL>();
-            else wait_tail<NL>(nt - t - 2);
-            wait_lgkm0();
-            block_barrier();
-            if constexpr (ISSUE) issue(t + NS);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-          mma_half<bf16, TM, TN, 0>(acc, f1a, f1b);
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (!LAST) {
-            const char* sn = smem + ((t + 1) % NS) * SLOT;
-            read_sub<bf16, false, false, true, BM, BN, TM, TN>(sn, sn + IA::BYTES, ra, rb, 0, lane, f0a, f0b);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          mma_half<bf16, TM, TN, 1>(acc, f1a, f1b);
-          __builtin_amdgcn_sched_barrier(0);
-        };
-        using T_ = std::true_type;
-        using F_ = std::false_type;
-        int t = 0;
-        for (; t < nt - NS; ++t) step(t, T_{}, F_{});
-        for (; t < nt - 1; ++t) step(t, F_{}, F_{});
-        step(nt - 1, F_{}, T_{});
-        // BN-producer fix-up, then the fp32 dW tile into H (the previous
-        // tile's update finished reading H before the last loop barrier)
-        if (ep.b_scale) {
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float db = dbl[(j & 1) * BM + wm * 16 * TM + i * 16 + 4 * g + r];
-#pragma unroll
-              for (int jj = 0; jj < TN; ++jj) acc[i][jj][r] = fmaf(e_s[jj], acc[i][jj][r], e_t[jj] * db);
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int jj = 0; jj < TN; ++jj)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int rl = wm * 16 * TM + i * 16 + 4 * g + r;
-              const int cl = wn * 16 * TN + jj * 16 + c;
-              *(float*)(H + rl * OSTRIDE + cl * 4) = acc[i][jj][r];
-            }
-      }
-      block_barrier();                                 // B_end: H holds tile j; ring free
-    }
-  } else {
-    // Adam role (the same barrier count as the MMA role: B0, nt - 1, B_end):
-    //  bi = 0..ITA-1: chunk bi of the previous tile's update (its state loads
-    //    were issued a whole loop ago), the small segment after the last;
-    //  bi = 1: db of this tile's rows -> dbl (the MMA epilogue reads it
-    //    after the last loop barrier); bi = ITA: this tile's state loads.
-    // The dispatcher guarantees nt - 1 >= ITA (every H read precedes the
-    // last loop barrier, after which the MMA waves overwrite H).
-    floatx4 aP[ITA], aM[ITA], aV[ITA];
-    int prev_m0 = 0, prev_n0 = 0, prev_tn = 0, prev_lt = 0;
-    for (int j = 0; j <= my_tiles; ++j) {
-      const bool has = j < my_tiles;
-      int m0 = 0, n0 = 0, tn = 0, lt = 0;
-      if (has) lt = coords(bid + j * grid, m0, n0, tn);
-      block_barrier();                                 // B0
-      const int nb = has ? nt - 1 : 0;
-      for (int bi = 0; bi <= nb; ++bi) {
-        if (j > 0) {
-          if (bi == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-          for (int u = 0; u < ITA; ++u) {
-            if (has && u != bi) continue;
-            const int idx = u * NT + t2;
-            const int rl = idx / CPR, ch = idx % CPR;
-            const size_t off = (size_t)(prev_m0 + rl) * ep.ldo + prev_n0 + ch * 4;
-            const uint4v v = *(const uint4v*)(H + rl * OSTRIDE + ch * 16);
-            if (!ep.dw_nostore) *(uint4v*)((float*)ep.out + off) = v;
-            adam4(aP[u], aM[u], aV[u], __builtin_bit_cast(floatx4, v), ep.ad_b1, ep.ad_b2, ep.ad_eps,
-                  ad_step, ad_bc2);
-            *(floatx4*)(ep.ad_p + off) = aP[u];
-            *(floatx4*)(ep.ad_m + off) = aM[u];
-            *(floatx4*)(ep.ad_v + off) = aV[u];
-            if (ep.ad_shadow) {
-              bf16x4 sh;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) sh[e] = (bf16)aP[u][e];
-              *(bf16x4*)((bf16*)ep.ad_shadow + off) = sh;
-            }
-          }
-          if (!has || bi == ITA - 1) small_segment(prev_lt, prev_m0, prev_tn, dbl + ((j - 1) & 1) * BM);
-        }
-        if (has && bi == 1 && ep.gb_src && t2 < BM) {
-          // sequential partial order (= the flat reduction's), loads in flight together
-          float e_g[QG];
-#pragma unroll
-          for (int q = 0; q < QG; ++q)
-            e_g[q] = ep.gb_src[(size_t)min(q, ep.gb_parts - 1) * ep.gb_stride + m0 + t2];
-          float db = 0.f;
-#pragma unroll
-          for (int q = 0; q < QG; ++q) db += q < ep.gb_parts ? e_g[q] : 0.f;
-          for (int q = QG; q < ep.gb_parts; ++q) db += ep.gb_src[(size_t)q * ep.gb_stride + m0 + t2];
-          dbl[(j & 1) * BM + t2] = db;
-        }
-        if (has && bi == ITA) {
-#pragma unroll
-          for (int u = 0; u < ITA; ++u) {
-            const int idx = u * NT + t2;
-            const size_t off = (size_t)(m0 + idx / CPR) * ep.ldo + n0 + (idx % CPR) * 4;
-            aP[u] = *(const floatx4*)(ep.ad_p + off);
-            aM[u] = *(const floatx4*)(ep.ad_m + off);
-            aV[u] = *(const floatx4*)(ep.ad_v + off);
-          }
-        }
-        if (bi < nb) block_barrier();
-      }
-      block_barrier();                                 // B_end
-      prev_m0 = m0;
-      prev_n0 = n0;
-      prev_tn = tn;
-      prev_lt = lt;
-    }
-  }
-}
-
-// -------------------------------------------------------------------------
-// Streamed Adam for a dW GEMM (tuning knob 16, the tail layers of the fused
-// step).  The Adam-fused dW kernel runs its K loop (L2-fed, latency-bound)
-// and then the tile's Adam stream (26 B per parameter from HBM) one after the
-// other in the same waves, and the co-resident blocks of a CU do the same in
-// lockstep, so HBM idles through the loops and the loops wait for the stream.
-// Here the dW GEMM (mmad_gemm_kernel, no Adam) writes each fp32 tile
-// write-through and raises the flag of its block; this kernel, launched
-// beside it on another stream, walks the producer's blocks f = a, a + grid,
-// ... (a multiple-of-8 grid: f and a share an XCD under round-robin
-// dispatch, a speed bonus only), loads the tile's p / m / v BEFORE polling
-// its flag (they do not depend on the GEMM), then reads the dW tile with sc1
-// loads and applies the same adam4 as the fused epilogue (same bits).  The
-// consumer resets each flag after use.  One 256-thread block per CU, no LDS:
-// the GEMM's blocks always fit beside it, and it is enqueued after the
-// GEMM, so the producer is never starved; a flag that never rises within
-// ~2^20 polls sets the sticky error word and the block exits.
-template <int BM, int BN>
-__global__ __launch_bounds__(256) void mmad_adam_stream_kernel(const float* __restrict__ g, int ld,
-                                                                GemmEpi ep, int ntiles) {
-  constexpr int NT = 256;
-  constexpr int CPR = BN / 4;                  // 16-B chunks per row
-  constexpr int CH = BM * CPR / NT;            // chunks per thread per tile
-  constexpr int AG = CH < 4 ? CH : 4;          // chunks in flight per group
-  static_assert(CH % AG == 0, "chunk groups");
-  __shared__ unsigned okw;
-  const int tid = threadIdx.x;
-  float ad_step = ep.ad_step, ad_bc2 = ep.ad_bc2;
-  if (ep.dyn) {
-    ad_step = ep.dyn->ad_step;
-    ad_bc2 = ep.dyn->ad_bc2;
-  }
-  for (int f = blockIdx.x; f < ntiles; f += gridDim.x) {
-    // producer block f -> output tile (the mapping of mmad_gemm_kernel, S = 1)
-    int tm, tn;
-    {
-      const int q = ntiles >> 3, r = ntiles & 7, xcd = f & 7;
-      const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (f >> 3);
-      const int tiles_m = ntiles / ep.tiles_n;
-      const int per_group = ep.group_m * ep.tiles_n;
-      const int first_m = (tile / per_group) * ep.group_m;
-      const int gsz = min(tiles_m - first_m, ep.group_m);
-      tm = first_m + (tile % per_group) % gsz;
-      tn = (tile % per_group) / gsz;
-    }
-    const size_t base = (size_t)(tm * BM) * ld + tn * BN;
-    floatx4 P[AG], Mm[AG], Vv[AG];
-    size_t off[AG];
-#pragma unroll
-    for (int u = 0; u < AG; ++u) {
-      const int idx = u * NT + tid;
-      off[u] = base + (size_t)(idx / CPR) * ld + (idx % CPR) * 4;
-      P[u] = *(const floatx4*)(ep.ad_p + off[u]);
-      Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
-      Vv[u] = *(const floatx4*)(ep.ad_v + off[u]);
-    }
-    if (tid == 0) {
-      unsigned ok = 0u;
-      for (unsigned spins = 0; spins < (1u << 20); ++spins) {
-        if (__hip_atomic_load(ep.tile_flag + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-          ok = 1u;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (!ok) __hip_atomic_store(ep.bn_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      okw = ok;
-    }
-    __syncthreads();
-    if (!okw) return;   // uniform: the host reports the sticky word
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(g + (size_t)(tm * BM) * ld), 0, BM * ld * 4, 0x00020000);
-#pragma unroll
-    for (int i0 = 0; i0 < CH; i0 += AG) {
-      if (i0 > 0) {
-#pragma unroll
-        for (int u = 0; u < AG; ++u) {
-          const int idx = (i0 + u) * NT + tid;
-          off[u] = base + (size_t)(idx / CPR) * ld + (idx % CPR) * 4;
-          P[u] = *(const floatx4*)(ep.ad_p + off[u]);
-          Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
-          Vv[u] = *(const floatx4*)(ep.ad_v + off[u]);
-        }
-      }
-      floatx4 G[AG];
-#pragma unroll
-      for (int u = 0; u < AG; ++u) {
-        const int idx = (i0 + u) * NT + tid;
-        G[u] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
-                                               rs, ((idx / CPR) * ld + tn * BN + (idx % CPR) * 4) * 4, 0, 16 /*sc1*/));
-      }
-#pragma unroll
-      for (int u = 0; u < AG; ++u) {
-        adam4(P[u], Mm[u], Vv[u], G[u], ep.ad_b1, ep.ad_b2, ep.ad_eps, ad_step, ad_bc2);
-        *(floatx4*)(ep.ad_p + off[u]) = P[u];
-        *(floatx4*)(ep.ad_m + off[u]) = Mm[u];
-        *(floatx4*)(ep.ad_v + off[u]) = Vv[u];
-        if (ep.ad_shadow) {
-          bf16x4 sh;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) sh[e] = (bf16)P[u][e];
-          *(bf16x4*)((bf16*)ep.ad_shadow + off[u]) = sh;
-        }
-      }
-    }
-    if (tid == 0) __hip_atomic_store(ep.tile_flag + f, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // -------------------------------------------------------------------------
 // host-side planning and launch
 // -------------------------------------------------------------------------
@@ -1771,7 +1270,7 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
   const int S = ep.splitk > 1 ? ep.splitk : 1;
   ep.group_m = plan_group_m(ntiles, tiles_m, BM, BN);
   dim3 grd(ntiles * S), blk(CFG_NT[cfg]);
-  const size_t dyn = ep.lds_pad > 0 ? (size_t)ep.lds_pad : 0;
+  const size_t dyn = 0;
   switch (cfg) {
     case 0: mmad_gemm_kernel<T, TO, AK, BK_, 0, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
     case 1: mmad_gemm_kernel<T, TO, AK, BK_, 1, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
@@ -1899,7 +1398,6 @@ static int tune_cfg(int dtype, int epi, const void* A, int lda, const void* B, i
   et.sm_p = nullptr;
   et.bn_rmean = nullptr;   // fused BN: no running-statistics update while timing
   et.bn_rvar = nullptr;
-  et.tile_flag = nullptr;   // no hand-off from a trial launch
   hipEvent_t e0, e1;
   MMAD_HIP_CHECK(hipEventCreate(&e0));
   MMAD_HIP_CHECK(hipEventCreate(&e1));
@@ -2011,33 +1509,6 @@ int mmad_gemm_plan(int Mp, int Np, int K, int epi, int dtype) {
   return it != g_tune.end() ? it->second : heuristic_cfg(Mp, Np, epi);
 }
 
-// the warp-specialised dW + Adam kernel for an Adam-fused dW GEMM (bf16, no
-// split): 64x64 tiles, a persistent grid of at most mmad_dw_ws_blocks()
-// workgroups (a multiple of 8), >= 9 K stages (its Adam schedule needs
-// nt - 1 >= 8 loop barriers)
-static bool dw_ws_fits(int dtype, int epi, const GemmEpi& ep, int Mp, int Np, int K) {
-  return mmad_dw_ws_enabled() && epi == GEMM_EPI_BWD_WEIGHT && dtype == MMAD_BF16 && ep.ad_p &&
-         ep.splitk <= 1 && Mp % 128 == 0 && Np % 64 == 0 && K % 64 == 0 && K / 64 >= 9;
-}
-static int launch_dw_ws(const void* A, int lda, const void* B, int ldb, int Mp, int Np, int K,
-                        const GemmEpi& ep_in, hipStream_t s) {
-  constexpr int BM = Cfg<6>::BM, BN = Cfg<6>::BN;
-  GemmEpi ep = ep_in;
-  const int tiles_m = Mp / BM, tiles_n = Np / BN, ntiles = tiles_m * tiles_n;
-  ep.tiles_n = tiles_n;
-  int gm = (int)(sqrt(ntiles / 8.0 * BN / BM) + 0.5);
-  const int env_gm = mmad_group_override();
-  if (env_gm > 0) gm = env_gm;
-  ep.group_m = gm < 1 ? 1 : (gm > tiles_m ? tiles_m : gm);
-  int cap = mmad_dw_ws_blocks();
-  cap = cap < 8 ? 8 : cap / 8 * 8;
-  const int grid = ntiles < cap ? (ntiles + 7) / 8 * 8 : cap;
-  mmad_dw_adam_ws_kernel<6><<<dim3(grid), dim3(2 * Cfg<6>::NT), 0, s>>>(
-      (const bf16*)A, lda, (const bf16*)B, ldb, K, ep, ntiles);
-  MMAD_LAUNCH_CHECK();
-  return MMAD_OK;
-}
-
 int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,
                        int Np, int K, const GemmEpi& ep_in, hipStream_t s, int* cfg_used) {
   MMAD_CHECK_ARG(Mp % 128 == 0 && Np % 128 == 0 && K % 128 == 0,
@@ -2046,24 +1517,16 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   MMAD_CHECK_ARG(dtype == MMAD_BF16 || dtype == MMAD_F32, "gemm: bad dtype %d", dtype);
   GemmEpi ep = ep_in;
   ep.dbg = mmad_dbg_override();
-  ep.apf = mmad_adam_prefetch_enabled();
-  ep.ad_nt = mmad_adam_nt_enabled();
   const bool bnf = ep.bn_sync != nullptr;
   MMAD_CHECK_ARG(!bnf || epi == GEMM_EPI_FWD || epi == GEMM_EPI_BWD_DATA,
                  "gemm: fused BN only for the forward / bwd-data epilogues");
   MMAD_CHECK_ARG(!bnf || Np / 64 <= MMAD_BN_EXIT, "gemm: fused BN: Np=%d too wide", Np);
   // the fused BN barrier needs one block per output tile (no split) and the
   // whole grid resident
-  ep.splitk = (ep.sk_slab && ep.sk_ctl && !bnf && !ep.tile_flag) ? mmad_gemm_splitk(Mp, Np, K, dtype, epi) : 1;
-  MMAD_CHECK_ARG(!ep.tile_flag || (epi == GEMM_EPI_BWD_WEIGHT && !ep.ad_p),
-                 "gemm: tile flags only for a dW GEMM without the fused Adam");
+  ep.splitk = (ep.sk_slab && ep.sk_ctl && !bnf) ? mmad_gemm_splitk(Mp, Np, K, dtype, epi) : 1;
   auto allowed = [&](int c) {
     return c >= 0 && c < NCFG && cfg_fits(c, Mp, Np, epi) && (!bnf || coresident(dtype, epi, c, Mp, Np));
   };
-  if (dw_ws_fits(dtype, epi, ep, Mp, Np, K)) {
-    if (cfg_used) *cfg_used = 6;
-    return launch_dw_ws(A, lda, B, ldb, Mp, Np, K, ep, s);
-  }
   const int env = mmad_tile_override();
   const int env_epi = ep.ad_p ? mmad_tile_adam_for(Mp, Np, K) : mmad_tile_epi_override(epi);
   int cfg;
@@ -2104,98 +1567,4 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   }
   if (cfg_used) *cfg_used = cfg;
   return launch_cfg(dtype, epi, A, lda, B, ldb, Mp, Np, K, ep, cfg, s);
-}
-
-// the streamed Adam of a flagged dW GEMM launched with tile configuration cfg
-// (ep: ad_* state, tile_flag, bn_err = sticky error word)
-int mmad_adam_stream(int cfg, const float* g, int ld, int Mp, int Np, const GemmEpi& ep_in, int grid,
-                     hipStream_t s) {
-  MMAD_CHECK_ARG(cfg >= 0 && cfg < NCFG && cfg_fits(cfg, Mp, Np, GEMM_EPI_BWD_WEIGHT),
-                 "adam_stream: bad tile configuration %d for %dx%d", cfg, Mp, Np);
-  MMAD_CHECK_ARG(ep_in.tile_flag && ep_in.bn_err && ep_in.ad_p && ep_in.ad_m && ep_in.ad_v,
-                 "adam_stream: missing flags / state");
-  const int BM = CFG_BM[cfg], BN = CFG_BN[cfg];
-  const int tiles_m = Mp / BM, tiles_n = Np / BN, ntiles = tiles_m * tiles_n;
-  GemmEpi ep = ep_in;
-  ep.tiles_n = tiles_n;
-  ep.group_m = plan_group_m(ntiles, tiles_m, BM, BN);
-  // at most two 256-thread workgroups per CU (no LDS): the GEMM's blocks,
-  // which it waits for, must always find room beside it
-  grid = grid < 8 ? 8 : (grid > 512 ? 512 : grid / 8 * 8);
-  if (grid > (ntiles + 7) / 8 * 8) grid = (ntiles + 7) / 8 * 8;
-  switch (BM * 1000 + BN) {
-    case 64064: mmad_adam_stream_kernel<64, 64><<<grid, 256, 0, s>>>(g, ld, ep, ntiles); break;
-    case 64128: mmad_adam_stream_kernel<64, 128><<<grid, 256, 0, s>>>(g, ld, ep, ntiles); break;
-    case 128128: mmad_adam_stream_kernel<128, 128><<<grid, 256, 0, s>>>(g, ld, ep, ntiles); break;
-    case 256128: mmad_adam_stream_kernel<256, 128><<<grid, 256, 0, s>>>(g, ld, ep, ntiles); break;
-    case 128256: mmad_adam_stream_kernel<128, 256><<<grid, 256, 0, s>>>(g, ld, ep, ntiles); break;
-    default: mmad_set_error("adam_stream: tile %dx%d", BM, BN); return MMAD_EUNSUPPORTED;
-  }
-  MMAD_LAUNCH_CHECK();
-  return MMAD_OK;
-}
-
-// Two dW GEMMs (EPI_BWD_WEIGHT, no split, no tile flags) in one launch with
-// tile configuration cfg: mmad_gemm_pair_kernel
-int mmad_gemm_dispatch_pair(int dtype, int cfg, const void* A0, int lda0, const void* B0, int ldb0,
-                            int Mp0, int Np0, int K0, const GemmEpi& e0, const void* A1, int lda1,
-                            const void* B1, int ldb1, int Mp1, int Np1, int K1, const GemmEpi& e1,
-                            hipStream_t s) {
-  MMAD_CHECK_ARG(dtype == MMAD_BF16 || dtype == MMAD_F32, "gemm_pair: bad dtype %d", dtype);
-  MMAD_CHECK_ARG(cfg >= 0 && cfg < NCFG && cfg_fits(cfg, Mp0, Np0, GEMM_EPI_BWD_WEIGHT) &&
-                     cfg_fits(cfg, Mp1, Np1, GEMM_EPI_BWD_WEIGHT),
-                 "gemm_pair: tile configuration %d does not fit both problems", cfg);
-  MMAD_CHECK_ARG(K0 % 128 == 0 && K1 % 128 == 0 && K0 > 0 && K1 > 0, "gemm_pair: bad K");
-  MMAD_CHECK_ARG(!e0.tile_flag && !e1.tile_flag && !e0.bn_sync && !e1.bn_sync,
-                 "gemm_pair: plain dW epilogues only");
-  GemmPairArgs p{};
-  p.A0 = A0; p.B0 = B0; p.lda0 = lda0; p.ldb0 = ldb0; p.K0 = K0;
-  p.A1 = A1; p.B1 = B1; p.lda1 = lda1; p.ldb1 = ldb1; p.K1 = K1;
-  const int BM = CFG_BM[cfg], BN = CFG_BN[cfg];
-  auto prep = [&](GemmEpi& ep, const GemmEpi& in, int Mp, int Np) {
-    ep = in;
-    ep.dbg = mmad_dbg_override();
-    ep.apf = mmad_adam_prefetch_enabled();
-    ep.ad_nt = mmad_adam_nt_enabled();
-    ep.splitk = 1;
-    const int tm = Mp / BM, tn = Np / BN;
-    ep.tiles_n = tn;
-    ep.group_m = plan_group_m(tm * tn, tm, BM, BN);
-    return tm * tn;
-  };
-  const int n0 = prep(p.ep0, e0, Mp0, Np0);
-  const int n1 = prep(p.ep1, e1, Mp1, Np1);
-  p.n0 = n0;
-  dim3 grd(n0 + n1), blk(CFG_NT[cfg]);
-#define MMAD_PAIR(T_, C_) \
-  mmad_gemm_pair_kernel<T_, float, false, false, C_, GEMM_EPI_BWD_WEIGHT><<<grd, blk, 0, s>>>(p); break;
-#define MMAD_PAIR_T(T_)        \
-  switch (cfg) {               \
-    case 0: MMAD_PAIR(T_, 0)   \
-    case 1: MMAD_PAIR(T_, 1)   \
-    case 2: MMAD_PAIR(T_, 2)   \
-    case 3: MMAD_PAIR(T_, 3)   \
-    case 4: MMAD_PAIR(T_, 4)   \
-    default: MMAD_PAIR(T_, 5)  \
-  }
-  if (dtype == MMAD_BF16) {
-    MMAD_PAIR_T(bf16)
-  } else {
-    MMAD_PAIR_T(float)
-  }
-#undef MMAD_PAIR_T
-#undef MMAD_PAIR
-  MMAD_LAUNCH_CHECK();
-  return MMAD_OK;
-}
-
-// the tile configuration mmad_gemm_dispatch gives an Adam-fused dW GEMM of
-// this shape with this tile_force (-1: not decided by the static rules --
-// autotuned or the warp-specialised kernel -- so not predictable here)
-int mmad_gemm_adam_dw_cfg(int Mp, int Np, int K, int tile_force) {
-  if (mmad_dw_ws_enabled()) return -1;
-  auto fits = [&](int c) { return c >= 0 && c < NCFG && cfg_fits(c, Mp, Np, GEMM_EPI_BWD_WEIGHT); };
-  if (fits(tile_force - 1)) return tile_force - 1;
-  const int e = mmad_tile_adam_for(Mp, Np, K);
-  return fits(e) ? e : -1;
 }

@@ -7,17 +7,6 @@
 #include "mmad_ops.h"
 
 #define SLAB_COLS 64
-// launch-shape knobs (measurement only): MMAD_FOLD_RPT = 64-row groups of
-// consumer rows per bn_fold_k block (2 or 4), MMAD_BNB_PU = partial chunks per
-// group loaded at once by bn_bwd_apply_k (8; 16 = the default above 32 chunks)
-static const int g_fold_rpt = [] {
-  const char* e = getenv("MMAD_FOLD_RPT");
-  return e ? atoi(e) : 2;
-}();
-static const int g_bnb_pu = [] {
-  const char* e = getenv("MMAD_BNB_PU");
-  return e ? atoi(e) : 16;
-}();
 #define SLAB_ROWS 128
 
 namespace {
@@ -907,7 +896,7 @@ int mmad_bn_finalize_fold(int dtype, int M, int N, int Mp, int Np, const float* 
   MMAD_CHECK_ARG(Nc_p % 128 == 0, "bn_finalize_fold: consumer rows not a multiple of 128");
   // consumer rows per block: 64 * rpt (the Welford merge is recomputed per
   // block, so fewer, taller blocks read fewer partials)
-  const int rpt = (g_fold_rpt == 4 && Nc_p % 256 == 0) ? 4 : 2;
+  const int rpt = 2;   // 64-row consumer groups per block (4 measured no faster, r02bj_*)
   dim3 grd(Np / 64, Nc_p / (64 * rpt));
   hipStream_t s = (hipStream_t)stream;
 #define MMAD_FOLD(TW_, R_)                                                                        \
@@ -950,7 +939,7 @@ int mmad_bn_act_bwd_apply(int dtype, int act, float slope, int M, int N, int Mp,
                           void* stream) {
   dim3 grd(Np / SLAB_COLS, Mp / SLAB_ROWS);
   hipStream_t s = (hipStream_t)stream;
-  const bool wide = nparts > 4 * 8 && g_bnb_pu != 8;
+  const bool wide = nparts > 4 * 8;   // 16 partial chunks per round trip (8 no faster, r02bj_*)
 #define MMAD_BNB(PU_)                                                                              \
   if (dtype == MMAD_BF16)                                                                          \
     bn_bwd_apply_k<bf16, PU_><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const bf16*)dy,   \

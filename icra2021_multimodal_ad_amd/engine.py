@@ -10,7 +10,6 @@ strided views into these buffers, so ``state_dict`` / ``load_state_dict`` /
 ``torch.optim`` all see the same memory the kernels use.
 """
 import ctypes
-import os
 
 import torch
 
@@ -66,7 +65,7 @@ class NativeAE:
         # differentiable forward records it and its backward checks it
         self.gen = 0
         self.adam_step_count = 0
-        self.use_graph = os.environ.get("MMAD_TRAIN_GRAPH", "0") == "1"
+        self.use_graph = bool(_native.SCHEDULE["train_graph"])
 
     # ------------------------------------------------------------------ memory
     def _alloc(self, device, src=None):
@@ -78,9 +77,9 @@ class NativeAE:
         self.running = torch.zeros(2 * self.n_bn, **kw)
         self.running[self.n_bn:] = 1.0
         # bf16: two weight shadows (mmad_ae_set_shadow_pair), ping-ponged by
-        # the fused step on large calls (the executor picks per call:
-        # MMAD_SHADOW_PAIR_ROWS); MMAD_SHADOW_PAIR=0 keeps one
-        self._pair = self.dt == _native.BF16 and os.environ.get("MMAD_SHADOW_PAIR", "1") == "1"
+        # the fused step on large calls (the executor picks per call: knob
+        # pair_rows); _native.SCHEDULE["shadow_pair"] = False keeps one
+        self._pair = self.dt == _native.BF16 and bool(_native.SCHEDULE["shadow_pair"])
         self._shadow_buf = (torch.zeros((2 if self._pair else 1) * self.n_weight, device=device,
                                         dtype=torch.bfloat16)
                             if self.dt == _native.BF16 else None)
@@ -251,7 +250,7 @@ class NativeAE:
             assert eps.numel() == k * B * self.btl
         self.adam_step_count += 1
         self.gen += 1
-        # eager multi-stream schedule by default.  MMAD_TRAIN_GRAPH=1 replays
+        # eager multi-stream schedule by default.  SCHEDULE["train_graph"] replays
         # one captured hipGraph per step instead (mmad_ae_train_step_graph);
         # measured slower on ROCm 7 (profiles/r02e_host.log: host 377 vs 325
         # us/step, GPU 675 vs 524 us/step at C2), so it stays opt-in

@@ -43,31 +43,41 @@ enum { MMAD_ACT_NONE = 0, MMAD_ACT_LEAKYRELU = 1, MMAD_ACT_RELU = 2, MMAD_ACT_SI
 const char* mmad_last_error_string(void);
 int mmad_abi_version(void);
 int mmad_pad_granule(void);
-/* Tuning knobs (no reference counterpart): knob 0 = GEMM tile override
- * (-1 autotuned; 0 = 128x128/512 thr, 1 = 256x128, 2 = 128x256, 3 = 64x64/256
- * thr, 4 = 64x128, 5 = 128x128/256 thr; a tile that does not divide a shape
- * falls back to the tuned one), knob 1 = XCD tile-group height override (-1
- * auto), knob 2 = per-shape autotune on first dispatch (1, default) or static
- * heuristic (0), knob 3 = diagnostics (tools/gemm_sweep; 4 = force the split-K
- * combine's timeout path, tests only), knob 4 = split-K
- * factor override for GEMMs given split-K workspace (0 = shape rule, 1/2/4/
- * 8/16), knob 9 = the same for the dW GEMMs only, knobs 10 / 11 = the dW
- * split rule's target number of 64x64-tile blocks (0 = no split, default) and minimum K stages
- * per slice (8), knob 12 = Adam-fused dW GEMMs on the warp-specialised
- * persistent kernel (1) or the plain tile kernel (0, default: measured
- * faster), knob 13 = that kernel's grid cap (256 workgroups), knob 14 = load
- * the Adam state of a 64x64 Adam-fused dW tile under its K loop (1) or after it
- * (0, default: measured faster, 32.9 vs 36.6 us for the largest c2 layer),
- * knob 15 = non-temporal loads/stores of that Adam state (MMAD_ADAM_NT),
- * knob 5 = tile of the dW GEMMs with the fused Adam epilogue (default 3 =
- * 64x64; -1 = autotuned like the others), knobs 6 / 7 = tile of the bwd-data /
- * forward GEMMs (-1 = autotuned), knob 8 = tile of the Adam-fused dW GEMMs
- * run on the main stream at the end of the backward (-1 = knob 5).
- * Defaults from MMAD_GEMM_TILE / MMAD_GEMM_GROUP_M / MMAD_GEMM_AUTOTUNE /
- * MMAD_GEMM_SPLITK / MMAD_GEMM_TILE_ADAM / MMAD_GEMM_TILE_BWD_DATA /
- * MMAD_GEMM_TILE_FWD / MMAD_GEMM_TILE_ADAM_MAIN / MMAD_GEMM_SPLITK_DW /
- * MMAD_SPLITK_DW_BLOCKS / MMAD_SPLITK_DW_MIN_STAGES / MMAD_DW_WS / MMAD_DW_WS_BLOCKS. */
+/* Tuning knobs (no reference counterpart).  One process-wide table, set only
+ * through mmad_tune_set (the library reads no environment variables).  GEMM
+ * knobs are read per dispatch; the executor's schedule knobs (16-27) are
+ * copied into a handle by mmad_ae_create, so set them before creating it.
+ *   0  GEMM tile override (-1 autotuned; 0 = 128x128/512 thr, 1 = 256x128,
+ *      2 = 128x256, 3 = 64x64/256 thr, 4 = 64x128, 5 = 128x128/256 thr; a tile
+ *      that does not divide a shape falls back to the tuned one)
+ *   1  XCD tile-group height override (-1 rule)
+ *   2  per-shape autotune on first dispatch (1, default) or static heuristic (0)
+ *   3  diagnostics bits (tools/gemm_phase; 4 = force the split-K combine's
+ *      timeout path, tests only)
+ *   4  split-K factor override for GEMMs given split-K workspace (0 = shape
+ *      rule, 1/2/4/8/16); 9 = the same for the dW GEMMs only; 10 / 11 = the dW
+ *      split rule's target number of 64x64-tile blocks (0 = no split, default)
+ *      and minimum K stages per slice (8)
+ *   5  tile of the Adam-fused dW GEMMs (-2 shape rule, -1 autotuned); 8 = of
+ *      those on the main stream at the end of the backward (-1 = knob 5);
+ *      6 / 7 = tile of the bwd-data / forward GEMMs (-1 autotuned)
+ *   12-15 retired (EINVAL)
+ *   16 train-mode BN schedule (-1 dtype default: bf16 fused, fp32 apply;
+ *      0 apply kernels, 1 fold into the consumer, 2 fused into the GEMMs)
+ *   17 backward BN schedule (-1 = the forward's, 2 = fused into bwd-data)
+ *   18 fused BN up to this many padded rows per call (2048; fold above)
+ *   19 dW GEMMs of the last layers on the main stream (2)
+ *   20 ping-pong weight shadows from this many padded rows (4096); 21 = main-
+ *      stream dW GEMMs then (1)
+ *   22 record the bwd-data event every n-th side-stream layer (2)
+ *   23 reduce the loss on the side stream right after the forward (1)
+ *   24 data parallel: exchange the small bucket after this layer's bwd-data (1)
+ *   25 also materialise dW in the fused step (0)
+ *   26 side stream at the highest priority instead of the lowest (0)
+ *   27 executor events with the system-scope fence (0) */
+#define MMAD_KNOB_COUNT 28
 int mmad_tune_set(int knob, int value);
+int mmad_tune_get(int knob, int* value);
 /* The split-K factor the dispatcher picks for a padded GEMM shape (Mp x Np
  * output, K deep) with epilogue `epi` (0 fwd, 1 MSE, 2 bwd-data, 3 dW,
  * 4 score) under the current knobs: 1, 2, 4, 8 or 16 (query only). */

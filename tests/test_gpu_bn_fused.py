@@ -1,4 +1,4 @@
-"""Train-mode BatchNorm fused into the producing GEMMs (MMAD_BN_MODE=2): the
+"""Train-mode BatchNorm fused into the producing GEMMs (tune knob bn_mode = 2): the
 forward GEMM's epilogue finishes the whole-batch statistics and writes
 y = BN(a), the bwd-data GEMM's epilogue writes dz (per-column-tile barrier
 between the blocks of one output column; csrc/mmad_gemm_mfma.hip).
@@ -6,7 +6,7 @@ between the blocks of one output column; csrc/mmad_gemm_mfma.hip).
 Pinned against the reference goldens (fp32: the same bars as
 test_gpu_parity.py's train-step test -- loss rtol 1e-4, gradients within 1e-4
 of max|g| of the fp64 truth or 2x the reference's own fp32 deviation, running
-statistics rtol 1e-4), against the kernel-per-phase schedule (MMAD_BN_MODE=0)
+statistics rtol 1e-4), against the kernel-per-phase schedule (bn_mode = 0)
 at the BASELINE C2 / C3 shapes, and for determinism (bit-identical repeats,
 bit-identical across forced tile configurations)."""
 import numpy as np
@@ -23,8 +23,8 @@ pytestmark = pytest.mark.gpu
 
 
 def _mk(monkeypatch, mode, *a, **kw):
-    monkeypatch.setenv("MMAD_BN_MODE", str(mode))
-    return _model(*a, **kw)
+    with _native.tune(bn_mode=int(mode)):
+        return _model(*a, **kw)
 
 
 @pytest.mark.parametrize("name", CASES)
@@ -140,38 +140,15 @@ def test_fused_bn_deterministic_and_tile_independent(monkeypatch):
     assert torch.equal(outs[0][0], outs[1][0])   # same tiles: bit-identical loss too
 
 
-@pytest.mark.parametrize("rows", [1024, 4096])
-def test_split_tail_matches_fused_tail(monkeypatch, rows):
-    """The split tail (MMAD_DW_SPLIT=1: layers 0 and 1 as a plain dW GEMM on a
-    tail stream + a flat Adam pass) against the default fused tail (Adam in
-    the dW epilogue): the same dW accumulation and the same Adam formula, so
-    the same parameters bit for bit after 3 steps, and the same losses."""
-    sd = init_state_dict(2048, 100, 5, seed=14)
-    ms = []
-    for split in ("1", "0"):
-        monkeypatch.setenv("MMAD_DW_SPLIT", split)
-        m, _ = _mk(monkeypatch, 1, 2048, 100, 5, sd, dtype="bf16")
-        m._native.sync_shadow(force=True)
-        ms.append(m)
-    for s in range(3):
-        x = torch.from_numpy(synth_windows(rows, 2048, seed=80 + s)).cuda()
-        la, lb = (float(m._native.train_step_fused(x)) for m in ms)
-        assert la == lb, (s, la, lb)
-    for m in ms:
-        m._native.check_status()
-    assert torch.equal(ms[0]._native.params, ms[1]._native.params)
-
-
 def test_fold_forward_fused_backward_c3_vib(monkeypatch):
-    """MMAD_BN_MODE_BWD=2: the BatchNorm backward fused into the bwd-data
+    """Knob bn_mode_bwd = 2: the BatchNorm backward fused into the bwd-data
     GEMMs after a FOLD forward (the fused backward needs only a, the saved
     mean / rstd and gamma, which bn_fold_k leaves), at the C3 shape through
     the fused step: finite, within 1 % of the default schedule's loss over 3
     steps, no barrier timeout."""
     sd = init_state_dict(2048, 100, 5, seed=16, enc_out=200)
-    monkeypatch.setenv("MMAD_BN_MODE_BWD", "2")
-    ma, _ = _model(2048, 100, 5, sd, dtype="bf16", models="vib_ae", k=1)
-    monkeypatch.delenv("MMAD_BN_MODE_BWD")
+    with _native.tune(bn_mode_bwd=2):
+        ma, _ = _model(2048, 100, 5, sd, dtype="bf16", models="vib_ae", k=1)
     mb, _ = _model(2048, 100, 5, sd, dtype="bf16", models="vib_ae", k=1)
     ma._native.sync_shadow(force=True)
     mb._native.sync_shadow(force=True)

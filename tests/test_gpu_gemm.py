@@ -149,12 +149,11 @@ def test_shadow_pair_matches_single_shadow(monkeypatch, pair_rows):
     from icra2021_multimodal_ad_amd.data import synth_windows
     sd = init_state_dict(1728, 100, 5, seed=5)
     xs = [torch.from_numpy(synth_windows(512 * (1 + i % 2), 1728, seed=10 + i)).cuda() for i in range(4)]
-    monkeypatch.setenv("MMAD_SHADOW_PAIR_ROWS", pair_rows)
     res = {}
     for pair in ("1", "0"):
-        monkeypatch.setenv("MMAD_SHADOW_PAIR", pair)
         cfg = types.SimpleNamespace(input_size=1728, btl_size=100, n_layers=5, gpu_id=0, dtype="bf16")
-        m = get_model(cfg)
+        with _native.tune(pair_rows=int(pair_rows), shadow_pair=pair == "1"):
+            m = get_model(cfg)
         m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
         assert m._native._pair == (pair == "1")
         losses = [float(m.train_step_async(x)) for x in xs]

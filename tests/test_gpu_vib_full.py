@@ -21,6 +21,7 @@ import torch
 
 from oracle import ae_oracle as O
 from oracle.model_io import model_from_state_dict, grads_to_flat
+from icra2021_multimodal_ad_amd import _native
 from icra2021_multimodal_ad_amd.common_utils import init_state_dict
 from icra2021_multimodal_ad_amd.data import synth_windows
 
@@ -85,12 +86,11 @@ def _torch_cpu_grads(x, sd, eps):
 def test_vib_ae_full_size_fp32_matches_oracle(d, bn_mode, monkeypatch):
     """bn_mode "2": train-mode BN fused into the producing GEMMs (the layers
     whose grid is co-resident; the rest fall back to the apply kernels)."""
-    if bn_mode is not None:
-        monkeypatch.setenv("MMAD_BN_MODE", bn_mode)
     sd = init_state_dict(d, 100, 5, seed=40 + d % 7, enc_out=200)
     x = synth_windows(B, d, seed=41)
     eps = np.random.default_rng(42).standard_normal((K_SAMPLES, B, 100)).astype(np.float32)
-    m = _model(d, sd, "f32")
+    with _native.tune(**({"bn_mode": int(bn_mode)} if bn_mode is not None else {})):
+        m = _model(d, sd, "f32")
     xd, ed = torch.from_numpy(x).cuda(), torch.from_numpy(eps).cuda()
     # beta 0 first: the reconstruction term alone (same noise, same bits)
     recon = float(m._native.train_step(xd, k=K_SAMPLES, eps=ed, beta_kl=0.0))

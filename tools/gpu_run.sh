@@ -1,0 +1,54 @@
+# One parameterised GPU-box runner (replaces the per-call one-shot scripts).
+# Usage on the box:  bash tools/gpu_run.sh <tag> <step> [<step> ...]
+# Steps (run in order; the first failure ends the call, no GPU step after it):
+#   tests            full `pytest -m gpu` suite
+#   tests:<expr>     `pytest -m gpu -k <expr>`
+#   smoke            __graft_entry__.smoke()
+#   bench[:<args>]   python bench.py <args, commas -> spaces>
+#   prof[:<args>]    rocprofv3 --kernel-trace --stats of bench.py <args>
+#   py:<script,args> python <script> <args>          (tools/*.py helpers)
+#   pmc:<ctr+ctr>:<script,args>  one rocprofv3 --pmc pass (counters joined by '+')
+# Every GPU step runs under its own timeout; logs go to gpurun_out/<tag>_*.
+set -o pipefail
+T=${1:?tag}
+shift
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+i=0
+for step in "$@"; do
+  i=$((i + 1))
+  kind=${step%%:*}
+  arg=""
+  [[ "$step" == *:* ]] && arg=${step#*:}
+  log=gpurun_out/${T}_${i}_${kind}.log
+  case "$kind" in
+    tests)
+      if [ -n "$arg" ]; then
+        timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf -k "$arg" --timeout 300 --timeout-method thread > "$log" 2>&1
+      else
+        timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > "$log" 2>&1
+      fi ;;
+    smoke)
+      timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1 ;;
+    bench)
+      timeout -k 10 400 python -u bench.py ${arg//,/ } > "$log" 2>&1 ;;
+    prof)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_${i}_prof -o run -- \
+        python3 bench.py ${arg//,/ } > "$log" 2>&1 ;;
+    py)
+      timeout -k 10 400 python -u ${arg//,/ } > "$log" 2>&1 ;;
+    pmc)
+      ctr=${arg%%:*}
+      cmd=${arg#*:}
+      timeout -s KILL 120 rocprofv3 --pmc ${ctr//+/ } -d gpurun_out/${T}_${i}_pmc -o run -- \
+        python3 ${cmd//,/ } > "$log" 2>&1 ;;
+    *)
+      echo "unknown step $step" >&2; exit 2 ;;
+  esac
+  rc=$?
+  echo "[gpu_run] step $i ($step) exit $rc"
+  if [ $rc -ne 0 ]; then
+    tail -30 "$log"
+    exit $rc
+  fi
+done
