@@ -403,8 +403,9 @@ def run(args):
         # from the executor by the n1_same_workload run above)
         probe_dist = model.dist
         model.dist = None
-        for i in range(n_probe):
-            model.train_step_async(pool[i % len(pool)], opt)
+        with mdist.rank_local():      # a step that still carried the exchange raises here
+            for i in range(n_probe):
+                model.train_step_async(pool[i % len(pool)], opt)
         model.dist = probe_dist
         torch.cuda.synchronize()
         buf = (ctypes.c_float * n_probe)()

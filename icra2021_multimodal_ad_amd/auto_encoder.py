@@ -68,6 +68,30 @@ class _AEFunction(torch.autograd.Function):
         return (None, None, *grads)
 
 
+def _check_status_all(model):
+    """model._native.check_status() (a kernel barrier / split-K combine that
+    timed out leaves that call's outputs unwritten).  Under data parallelism
+    the failure is local to one GPU, so the flag is MAX-all-reduced and every
+    rank raises together instead of the others blocking in the next
+    collective."""
+    d = getattr(model, "dist", None)
+    if d is None or getattr(d, "world", 1) <= 1:
+        model._native.check_status()
+        return
+    import torch.distributed as tdist
+    err = None
+    try:
+        model._native.check_status()
+    except Exception as e:   # noqa: BLE001 -- re-raised on every rank below
+        err = e
+    dev = "cuda" if tdist.get_backend(d.group) == "nccl" else "cpu"
+    flag = torch.tensor([0.0 if err is None else 1.0], device=dev)
+    tdist.all_reduce(flag, op=tdist.ReduceOp.MAX, group=d.group)
+    if float(flag.item()) != 0.0:
+        raise err if err is not None else _native.NativeError(
+            "a kernel barrier timed out on another rank; this step's results are invalid")
+
+
 class AutoEncoder(AbstractModel):
     """models/auto_encoder.py:21-123.
 
@@ -238,6 +262,9 @@ class AutoEncoder(AbstractModel):
         bwd [+ grad all-reduce] + Adam) with the loss left on the device."""
         if not self.training:
             self.train()
+        if self.dist is not None and self.dist.world > 1:
+            from .dist import assert_collective_context
+            assert_collective_context("train_step_async with the data-parallel exchange attached")
         nat = self._native
         seed = 0x9E3779B97F4A7C15 & ((1 << 63) - 1)
         if self.dist is None or self.dist.native:
@@ -318,7 +345,7 @@ class AutoEncoder(AbstractModel):
         x = x.view(x.size(0), -1)
         loss = model.train_step_async(x, engine.optimizer)
         loss = float(loss)
-        model._native.check_status()
+        _check_status_all(model)
         return (loss,)
 
     @staticmethod
@@ -336,7 +363,7 @@ class AutoEncoder(AbstractModel):
                 # data parallel: the whole batch's sum-MSE = sum of the shards'
                 model.dist.all_reduce_sum(loss)
         loss = float(loss)
-        model._native.check_status()
+        _check_status_all(model)
         return (loss,)
 
     @staticmethod

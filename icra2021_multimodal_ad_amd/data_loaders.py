@@ -93,7 +93,12 @@ class BatchLoader:
     Data parallel (world > 1): every rank draws the same sampler order (same
     seed), a global batch is ``batch_size * world`` windows and this rank gets
     its contiguous rows of it (dist.shard_rows), so the ranks together step
-    through exactly the single-process sequence of windows."""
+    through exactly the single-process sequence of windows.  The one
+    exception: a last global batch of fewer than 2 * world windows is dropped
+    on every rank (the decision depends only on the global count, so all ranks
+    agree) -- some shard would get 0 rows (no native step exists for it, while
+    the other ranks wait in the exchange) or 1 row (train-mode BatchNorm over
+    one window, which torch's BatchNorm1d refuses too)."""
 
     def __init__(self, dataset, batch_size, sampler, rank=0, world=1):
         self.dataset = dataset
@@ -101,11 +106,18 @@ class BatchLoader:
         self.sampler = sampler
         self.rank, self.world = int(rank), int(world)
 
+    def _global_batches(self):
+        n, gb = len(self.sampler), self.batch_size * self.world
+        starts = list(range(0, n, gb))
+        if self.world > 1 and starts and n - starts[-1] < 2 * self.world:
+            starts.pop()
+        return starts
+
     def __iter__(self):
         order = np.fromiter(iter(self.sampler), dtype=np.int64, count=len(self.sampler))
         dev = self.dataset.data.device
         gb = self.batch_size * self.world
-        for s in range(0, len(order), gb):
+        for s in self._global_batches():
             idx = order[s:s + gb]
             if self.world > 1:
                 q, r = divmod(len(idx), self.world)
@@ -115,8 +127,7 @@ class BatchLoader:
                    self.dataset.targets[torch.from_numpy(idx)])
 
     def __len__(self):
-        gb = self.batch_size * self.world
-        return (len(self.sampler) + gb - 1) // gb
+        return len(self._global_batches())
 
 
 class SyntheticWindowDataset:

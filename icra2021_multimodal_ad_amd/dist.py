@@ -23,7 +23,9 @@ rank / world), validation losses are summed over the ranks so every rank
 keeps the same best-on-valid state, BatchNorm running statistics are averaged
 at every epoch end, and scoring is sharded by rows with the per-window scores
 all-gathered (shard_rows / gather_rows) before AUROC."""
+import contextlib
 import os
+import threading
 
 import torch
 import torch.distributed as dist
@@ -54,6 +56,29 @@ def gather_rows(local, n, group=None):
     return torch.cat(out, dim=0)
 
 
+_LOCAL = threading.local()
+
+
+@contextlib.contextmanager
+def rank_local():
+    """Marks code that only SOME ranks run (e.g. rank 0's kernel probe in
+    bench.py).  Inside it, any call that would enter a collective exchange
+    raises (assert_collective_context) instead of blocking forever in a
+    collective the other ranks never join (round 2's r02zf bench hang)."""
+    prev = getattr(_LOCAL, "depth", 0)
+    _LOCAL.depth = prev + 1
+    try:
+        yield
+    finally:
+        _LOCAL.depth = prev
+
+
+def assert_collective_context(what):
+    if getattr(_LOCAL, "depth", 0) > 0:
+        raise RuntimeError(f"{what} inside a rank-local region (dist.rank_local): the other ranks "
+                           f"would never join its collectives; detach the exchange first")
+
+
 def init_from_env(backend=None):
     """Initialise the default process group from torchrun's env vars.
     Returns (rank, world_size, local_rank)."""
@@ -69,21 +94,44 @@ def init_from_env(backend=None):
 
 
 class NativeComm:
-    """An RCCL communicator owned by libmmad (include/mmad.h, mmad_comm_*)."""
+    """An RCCL communicator owned by libmmad (include/mmad.h, mmad_comm_*).
 
-    def __init__(self, group=None):
+    Construction is collective and agreed in stages over the torch process
+    group, so one rank's failure never leaves the others blocked in RCCL:
+    rank 0 broadcasts the unique id together with a success flag (a failed id
+    query makes every rank raise before any RCCL call); mmad_comm_create is
+    then entered by every rank once all have agreed they are ready.  ``fail_stage`` (tests) makes this rank fail
+    at 'uid' (rank 0's id query) or 'create'."""
+
+    def __init__(self, group=None, fail_stage=None):
         import ctypes
         from . import _native
         self._lib = _native.load()
+        self.handle = None
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         n = self._lib.mmad_comm_unique_id_bytes()
         uid = (ctypes.c_char * n)()
+        ok = 1
         if self.rank == 0:
-            _native.check(self._lib.mmad_comm_get_unique_id(uid), "mmad_comm_get_unique_id")
-        obj = [bytes(uid) if self.rank == 0 else None]
+            try:
+                if fail_stage == "uid":
+                    raise RuntimeError("injected unique-id failure")
+                _native.check(self._lib.mmad_comm_get_unique_id(uid), "mmad_comm_get_unique_id")
+            except Exception:   # noqa: BLE001 -- every rank learns it from the flag
+                ok = 0
+        obj = [(ok, bytes(uid)) if self.rank == 0 else None]
         dist.broadcast_object_list(obj, src=0, group=group)
-        uid = (ctypes.c_char * n).from_buffer_copy(obj[0])
+        ok, raw = obj[0]
+        if not ok:
+            raise RuntimeError("rank 0 could not create the RCCL unique id")
+        # every rank must reach mmad_comm_create (RCCL's init blocks until all
+        # ranks have called it): agree first that all are ready
+        ready = fail_stage != "create"
+        if not _agree(ready, group, "cuda" if dist.get_backend(group) == "nccl" else "cpu"):
+            raise RuntimeError("a rank could not prepare the RCCL communicator"
+                               + ("" if ready else " (injected failure on this rank)"))
+        uid = (ctypes.c_char * n).from_buffer_copy(raw)
         h = ctypes.c_void_p()
         _native.check(self._lib.mmad_comm_create(ctypes.byref(h), uid, self.world, self.rank),
                       "mmad_comm_create")
@@ -115,8 +163,23 @@ class NativeComm:
             pass
 
 
+def _agree(flag, group, device):
+    """MIN of a 0/1 flag over the ranks (every rank calls it)."""
+    t = torch.tensor([1.0 if flag else 0.0], device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return float(t.item()) == 1.0
+
+
 class DataParallel:
-    def __init__(self, group=None, native=None):
+    """Gradient exchange for the data-parallel step.  The native RCCL path is
+    chosen by three collective agreements (each a MIN over the ranks, so the
+    ranks always take the same path and never wait in a collective another
+    rank skipped): every rank wants it; every rank built its communicator;
+    every rank's checked self-test all-reduce passed.  Otherwise all ranks use
+    torch.distributed.  ``_fail`` (tests): inject a failure on this rank at
+    'uid' / 'create' / 'selftest'."""
+
+    def __init__(self, group=None, native=None, _fail=None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.comm = None
@@ -124,28 +187,35 @@ class DataParallel:
             native = (self.world > 1 and torch.cuda.is_available()
                       and dist.get_backend(group) == "nccl"
                       and os.environ.get("MMAD_NATIVE_COMM", "1") != "0")
-        if native:
-            # every rank must agree: fall back to the torch path together if
-            # any rank could not build the communicator
-            comm, err = None, None
+        if self.world <= 1:
+            return
+        dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+        if not _agree(native, group, dev):
+            return
+        comm, err = None, None
+        try:
+            comm = NativeComm(group, fail_stage=_fail if _fail in ("uid", "create") else None)
+        except Exception as e:  # noqa: BLE001 -- reported below, then fallback together
+            err = e
+            comm = None
+        built = _agree(comm is not None, group, dev)
+        passed = False
+        if built:
             try:
-                comm = NativeComm(group)
+                if _fail == "selftest":
+                    raise RuntimeError("injected self-test failure")
                 comm.self_test()
-            except Exception as e:  # noqa: BLE001 -- reported below, then fallback
+                passed = True
+            except Exception as e:  # noqa: BLE001
                 err = e
-                if comm is not None:
-                    comm.close()
-                    comm = None
-            ok = torch.tensor([0.0 if comm is None else 1.0], device="cuda")
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
-            if float(ok.item()) == 1.0:
-                self.comm = comm
-            else:
-                if comm is not None:
-                    comm.close()
-                if dist.get_rank(group) == 0:
-                    print(f"[mmad] native RCCL exchange unavailable ({err}); using torch.distributed",
-                          flush=True)
+        if built and _agree(passed, group, dev):
+            self.comm = comm
+            return
+        if comm is not None:
+            comm.close()
+        if dist.get_rank(group) == 0:
+            print(f"[mmad] native RCCL exchange unavailable ({err}); using torch.distributed",
+                  flush=True)
 
     def close(self):
         if self.comm is not None:

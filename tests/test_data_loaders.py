@@ -78,3 +78,27 @@ def test_dataset_is_seeded_and_labelled():
     tr, va, te = a.get_loaders(500, indexes_list=[[0, 1], [2], [3, 4]])
     assert [x.shape[0] for x, _ in va] == [1] and [x.shape[0] for x, _ in te] == [2]
     assert isinstance(tr, BatchLoader) and sorted(tr.sampler) == [0, 1]
+
+
+def test_dp_tail_batch_too_small_for_every_rank_is_dropped():
+    """world 2, batch 4: 9 windows = two global batches of 8 and a tail of 1
+    (< 2 * world) -- dropped on both ranks; a tail of 4 (= 2 rows per rank) is
+    kept.  No rank ever gets fewer than 2 rows; both ranks yield the same
+    number of batches; single process keeps every window."""
+    from icra2021_multimodal_ad_amd.data_loaders import SequentialIndicesSampler
+    ds = types.SimpleNamespace(data=torch.arange(20, dtype=torch.float32)[:, None],
+                               targets=torch.zeros(20))
+    for n, want in ((17, 2), (20, 3), (19, 2), (21, 3)):
+        if n > 20:
+            ds = types.SimpleNamespace(data=torch.arange(n, dtype=torch.float32)[:, None],
+                                       targets=torch.zeros(n))
+        lens = []
+        for rank in (0, 1):
+            ld = BatchLoader(ds, 4, SequentialIndicesSampler(list(range(n))), rank, 2)
+            got = [x.shape[0] for x, _ in ld]
+            assert len(got) == len(ld) == want, (n, rank, got)
+            assert min(got) >= 2, (n, rank, got)
+            lens.append(got)
+        assert len(lens[0]) == len(lens[1])
+        single = BatchLoader(ds, 4, SequentialIndicesSampler(list(range(n))), 0, 1)
+        assert sum(x.shape[0] for x, _ in single) == n

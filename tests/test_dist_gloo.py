@@ -127,3 +127,61 @@ def test_two_rank_sharding_gather_and_loaders():
         assert len(single) == len(out[0][name]) == len(out[1][name])
         for i, xb in enumerate(single):
             np.testing.assert_array_equal(np.concatenate([out[0][name][i], out[1][name][i]]), xb)
+
+
+def _fallback_worker(rank, world, port, fail, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from icra2021_multimodal_ad_amd import dist as mdist
+    mdist.init_from_env(backend="gloo")
+    stage, bad_rank = fail
+    dp = mdist.DataParallel(native=True, _fail=stage if rank == bad_rank else None)
+    t = torch.tensor([float(rank + 1)])
+    dp.all_reduce_sum(t)                       # the torch path works on every rank
+    out[rank] = (dp.native, float(t.item()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_native_comm_failure_on_one_rank_falls_back_together():
+    """a rank whose native communicator cannot be built (rank 0's
+    unique-id query, or any rank before RCCL init) must not leave its peers
+    blocked in a collective: the staged agreement makes every rank fall back to
+    torch.distributed together (no hang: the test joins within its timeout)."""
+    for fail in (("uid", 0), ("create", 1), ("create", 0)):
+        port = _free_port()
+        mgr = mp.Manager()
+        out = mgr.dict()
+        ctx = mp.get_context("spawn")
+        ps = [ctx.Process(target=_fallback_worker, args=(r, 2, port, fail, out)) for r in range(2)]
+        for p in ps:
+            p.start()
+        for p in ps:
+            p.join(120)
+        alive = [p.is_alive() for p in ps]
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+        assert not any(alive), f"hang with failure {fail}"
+        assert all(p.exitcode == 0 for p in ps), (fail, [p.exitcode for p in ps])
+        assert out[0] == (False, 3.0) and out[1] == (False, 3.0), (fail, dict(out))
+
+
+def test_rank_local_guard():
+    """dist.rank_local marks code only some ranks run; a collective step
+    entered inside it raises instead of hanging (AutoEncoder.train_step_async
+    calls assert_collective_context whenever an exchange is attached)."""
+    import pytest
+    from icra2021_multimodal_ad_amd import dist as mdist
+    mdist.assert_collective_context("outside")          # no-op
+    with mdist.rank_local():
+        with pytest.raises(RuntimeError, match="rank-local"):
+            mdist.assert_collective_context("a DP step")
+        with mdist.rank_local():
+            pass
+        with pytest.raises(RuntimeError):
+            mdist.assert_collective_context("still inside")
+    mdist.assert_collective_context("outside again")
+    import inspect
+    from icra2021_multimodal_ad_amd.auto_encoder import AutoEncoder
+    assert "assert_collective_context" in inspect.getsource(AutoEncoder.train_step_async)
