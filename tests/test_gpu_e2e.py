@@ -10,10 +10,12 @@ same configuration from the same initial weights on the same batches.
 
 Bars: scoring -- on one trained model, the product's BASE/SAP/NAP AUROC
 within 0.002 of the CPU oracle's on the same weights (north star, the hot
-path); training -- the product's AUROC after training within the band an
-independent fp32 implementation (the CPU oracle, trained on the same batches,
-in the fixture) lands from the reference; bf16 (the throughput path) --
-within a stated band.  Per-seed values are printed."""
+path); training -- the product's AUROC after training as close to the
+reference as the reference lands to ITSELF under a second fp32 summation
+order (measured in the fixture: 8 vs 1 torch threads), and the best-on-valid
+epoch selection compared (the configuration's best epoch is not the last);
+bf16 (the throughput path) -- within a stated band.  Per-seed values are
+printed and written to gpurun_out/e2e_*.json."""
 import types
 
 import numpy as np
@@ -66,33 +68,75 @@ def _run_cached(g, seed, dtype):
     return _RUNS[(seed, dtype)]
 
 
-@pytest.mark.parametrize("seed", [0, 1, 2])
-def test_e2e_training_parity_fp32(e2e, seed):
-    """Train -> score -> AUROC against the reference's own run.  The bar is set
-    by the CPU oracle (an independent fp32 restatement pinned to the
-    reference's goldens) trained on the same batches: after n_epochs of Adam,
-    summation-order noise moves any fp32 implementation's AUROC off the
-    reference's -- |oracle - reference| reaches 0.014 (SAP) and 0.022 (NAP) on
-    these seeds.  Ours must stay within max(0.002, 2x the oracle's largest
-    deviation over the seeds) per score type, and the loss EMAs within 5 %."""
+def _floor(g, m, key="auroc"):
+    """The reference's own noise floor per seed: |AUROC(8 threads) -
+    AUROC(1 thread)| of two reference trainings of the same program
+    (tests/golden/gen_e2e.py)."""
+    return [abs(float(g[f"s{s_}/{m}/{key}"]) - float(g[f"s{s_}/ref1/{m}/{key}"])) for s_ in (0, 1, 2)]
+
+
+def _record(name, payload):
+    """Per-seed deltas of a GPU run, for profiles/ (gpurun_out/ on the box)."""
+    import json
+    import os
+    os.makedirs("gpurun_out", exist_ok=True)
+    path = os.path.join("gpurun_out", f"e2e_{name}.json")
+    with open(path, "w") as f:
+        json.dump(payload, f, indent=1)
+
+
+def test_e2e_training_parity_fp32(e2e):
+    """Train -> score -> AUROC against the reference's own run, judged by the
+    reference's measured noise floor.  The fixture trains the reference twice
+    per seed (8 and 1 torch threads: two fp32 summation orders of the same
+    program) -- after 20 epochs of Adam it lands 0.0006-0.0096 (BASE),
+    0.007-0.017 (SAP) and 0.016-0.048 (NAP) AUROC from itself, and seed 2
+    even selects a different best epoch (19 vs 15).  The product (a third fp32
+    order, on the GPU) must land as close to the reference as the reference
+    lands to itself: per method, mean over seeds |ours - ref| <= max(0.002,
+    2 x the mean floor), every seed within max(0.002, 3 x the largest floor);
+    the best-on-valid epoch equal to one of the reference's two runs, or a
+    near-tie (the reference's valid loss at our epoch within 3 % of its
+    minimum); train / valid loss EMAs within 5 %.  The per-seed deltas are
+    written to gpurun_out/e2e_fp32_training.json."""
     g = e2e
-    p = f"s{seed}/"
-    det, th, vh, res = _run_cached(g, seed, "f32")
-    lab = det.last_test_label
-    assert np.array_equal(lab, g[p + "test_label"])           # same split, same order
-    th_dev = np.abs(np.asarray(th) / g[p + "train_history"] - 1).max()
-    vh_dev = np.abs(np.asarray(vh) / g[p + "valid_history"] - 1).max()
-    rows = [(m, det.last_row[f"{m}_auroc"], float(g[p + f"{m}/auroc"]),
-             float(g[p + f"oracle/{m}/auroc"]), det.last_row[f"{m}_aupr"], float(g[p + f"{m}/aupr"]))
-            for m in METHODS]
-    print(f"\nseed {seed} fp32: best epoch {det.best_epoch} (ref {int(g[p + 'best_epoch'])}), "
-          f"max rel dev of the train/valid loss EMA {th_dev:.2e}/{vh_dev:.2e}; AUROC ours/ref/oracle: "
-          + "; ".join(f"{m} {a:.4f}/{r:.4f}/{o:.4f}" for m, a, r, o, _, _ in rows))
-    for m, a, r, _, _, _ in rows:
-        oracle_dev = max(abs(float(g[f"s{s_}/oracle/{m}/auroc"]) - float(g[f"s{s_}/{m}/auroc"]))
-                         for s_ in (0, 1, 2))
-        assert abs(a - r) <= max(0.002, 2.0 * oracle_dev), (m, a, r, oracle_dev)
-    assert th_dev < 0.05 and vh_dev < 0.05, (th, vh)
+    rec = {"what": "product fp32 training vs the reference (8 threads) and the reference's noise "
+                   "floor |ref(8 threads) - ref(1 thread)|", "seeds": {}}
+    deltas = {m: [] for m in METHODS}
+    for seed in (0, 1, 2):
+        p = f"s{seed}/"
+        det, th, vh, res = _run_cached(g, seed, "f32")
+        lab = det.last_test_label
+        assert np.array_equal(lab, g[p + "test_label"])           # same split, same order
+        th_dev = float(np.abs(np.asarray(th) / g[p + "train_history"] - 1).max())
+        vh_dev = float(np.abs(np.asarray(vh) / g[p + "valid_history"] - 1).max())
+        row = {"best_epoch": int(det.best_epoch), "ref_best_epoch": int(g[p + "best_epoch"]),
+               "ref1_best_epoch": int(g[p + "ref1/best_epoch"]),
+               "train_ema_max_rel_dev": th_dev, "valid_ema_max_rel_dev": vh_dev}
+        for m in METHODS:
+            a, r, r1 = det.last_row[f"{m}_auroc"], float(g[p + f"{m}/auroc"]), float(g[p + f"ref1/{m}/auroc"])
+            deltas[m].append(abs(a - r))
+            row[m] = {"auroc": a, "ref_auroc": r, "ref1_auroc": r1, "delta": a - r, "floor": abs(r1 - r),
+                      "oracle_auroc": float(g[p + f"oracle/{m}/auroc"])}
+        rec["seeds"][seed] = row
+        print(f"\nseed {seed} fp32: best epoch {det.best_epoch} (ref {row['ref_best_epoch']}, "
+              f"1-thread ref {row['ref1_best_epoch']}); loss EMA dev {th_dev:.2e}/{vh_dev:.2e}; "
+              + "; ".join(f"{m} ours {row[m]['auroc']:.4f} ref {row[m]['ref_auroc']:.4f} "
+                          f"ref1 {row[m]['ref1_auroc']:.4f}" for m in METHODS))
+        vref = np.asarray(g[p + "valid_history"])
+        ok_epoch = (det.best_epoch in (row["ref_best_epoch"], row["ref1_best_epoch"])
+                    or vref[det.best_epoch - 1] <= 1.03 * vref.min())
+        assert ok_epoch, (seed, det.best_epoch, vref.tolist())
+        assert th_dev < 0.05 and vh_dev < 0.05, (seed, th, vh)
+    for m in METHODS:
+        fl = _floor(g, m)
+        rec[m] = {"mean_abs_delta": float(np.mean(deltas[m])), "mean_floor": float(np.mean(fl)),
+                  "max_floor": float(np.max(fl))}
+    _record("fp32_training", rec)
+    for m in METHODS:
+        fl = _floor(g, m)
+        assert np.mean(deltas[m]) <= max(0.002, 2.0 * np.mean(fl)), (m, deltas[m], fl)
+        assert np.max(deltas[m]) <= max(0.002, 3.0 * np.max(fl)), (m, deltas[m], fl)
 
 
 def test_e2e_scoring_auroc_parity_on_trained_model(e2e):
@@ -167,6 +211,9 @@ def test_e2e_bf16_scoring_and_training(e2e):
         ref = [float(g[f"s{s_}/{m}/auroc"]) for s_ in (0, 1, 2)]
         print(f"\n{m}: reference AUROC mean {np.mean(ref):.4f} (spread {np.ptp(ref):.4f}); "
               f"bf16-trained - reference: {', '.join(f'{d:+.4f}' for d in diffs[m])}")
+    _record("bf16_training", {"what": "bf16-trained product AUROC - reference (8 threads) per seed, "
+                                      "with the reference's fp32 noise floor",
+                              **{m: {"delta": diffs[m], "floor": _floor(g, m)} for m in METHODS}})
     assert np.max(np.abs(diffs["base"])) <= 0.02, diffs["base"]
 
 
