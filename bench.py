@@ -75,6 +75,30 @@ def cpu_model():
     return "unknown"
 
 
+def host_cores():
+    """The host cores this process may actually use: the CPU affinity mask,
+    capped by the cgroup CPU quota (cgroup v2 cpu.max / v1 cfs quota).  On the
+    GPU box the affinity mask lists the whole machine (256 CPUs) while the
+    lease's quota is 16; torch with 256 threads on a 16-CPU quota runs ~300x
+    slower than with 16."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    used = n if quota is None else max(1, min(n, int(quota)))
+    return used, n, quota
+
+
 def cpu_baseline(d, batch, vib, budget_s=12.0):
     """The reference's modules in torch-CPU fp32 (oracle/torch_ref.py): whole
     train steps (fwd + loss + bwd + Adam) at the same D and batch, timed on
@@ -83,8 +107,8 @@ def cpu_baseline(d, batch, vib, budget_s=12.0):
     from oracle import torch_ref
     from icra2021_multimodal_ad_amd.common_utils import init_state_dict, ae_widths
     from icra2021_multimodal_ad_amd.data import synth_windows
-    # every host core this process may run on (the lease's affinity)
-    threads = len(os.sched_getaffinity(0))
+    # every host core this process may run on (affinity capped by the cgroup quota)
+    threads, n_aff, quota = host_cores()
     torch.set_num_threads(threads)
     enc_out = 200 if vib else None
     enc, dec = ae_widths(d, 100, 5, enc_out=enc_out)
@@ -105,7 +129,8 @@ def cpu_baseline(d, batch, vib, budget_s=12.0):
             "sample": f"{n} train steps of the reference's modules in torch-CPU fp32 "
                       f"(nn.Linear/LeakyReLU/BatchNorm1d, MSELoss(sum), optim.Adam; "
                       f"oracle/torch_ref.py{', VIB-AE' if vib else ''}) at D={d}, batch={batch}, "
-                      f"{el:.1f} s, torch threads={threads} = len(os.sched_getaffinity(0))"}
+                      f"{el:.1f} s, torch threads={threads} (affinity {n_aff} CPUs, cgroup quota "
+                      f"{quota if quota is not None else 'none'})"}
 
 
 def dw_adam_bytes(N, K, B, es=2):

@@ -42,7 +42,8 @@ def cpu_baseline(d, budget_s=10.0):
     from oracle.model_io import model_from_state_dict
     from icra2021_multimodal_ad_amd.common_utils import init_state_dict
     from icra2021_multimodal_ad_amd.data import synth_windows
-    threads = len(os.sched_getaffinity(0))   # every host core of this process
+    from bench import host_cores
+    threads, n_aff, quota = host_cores()     # affinity capped by the cgroup quota
     m = model_from_state_dict(init_state_dict(d, 100, 5, seed=0))
     x = synth_windows(4096, d, seed=3)
     n, t0 = 0, time.perf_counter()
@@ -55,7 +56,8 @@ def cpu_baseline(d, budget_s=10.0):
     el = time.perf_counter() - t0
     return {"value": n / el, "unit": "windows/sec", "cores": threads, "kind": "port",
             "sample": f"{n} windows of oracle get_diffs+BASE+SAP (numpy fp32, batch 698) at D={d}, "
-                      f"{el:.1f} s, BLAS threads={threads} = len(os.sched_getaffinity(0))"}
+                      f"{el:.1f} s, BLAS threads={threads} (affinity {n_aff} CPUs, cgroup quota "
+                      f"{quota if quota is not None else 'none'})"}
 
 
 def _setup(dim, dtype, N, batch):

@@ -128,6 +128,20 @@ __device__ __forceinline__ void issue_stage(char* img, const T* __restrict__ G, 
   }
 }
 
+// chunk i (< Img::CHUNKS) of one stage of one operand (issue_stage = all i)
+template <typename T, bool KMAJ, int ROWS, int NT>
+__device__ __forceinline__ void issue_chunk(char* img, const T* __restrict__ G, int ld, int r0, int k0,
+                                            int tid, int i) {
+  using I = Img<T, KMAJ, ROWS, NT>;
+  constexpr int EPC = 16 / sizeof(T);
+  const int p = NT * i + tid;
+  const int row = p / I::CPROW;
+  const int j = (p % I::CPROW) ^ swz<T, KMAJ, I::RB>(row);
+  const T* src = KMAJ ? G + (size_t)(r0 + row) * ld + k0 + j * EPC
+                      : G + (size_t)(k0 + row) * ld + r0 + j * EPC;
+  dma16(src, img + (NT * i + (tid & ~63)) * 16);
+}
+
 // ---- bf16 fragment reads (16x16x32 MFMA operand) ---------------------------
 // Natural k order for both layouts: lane group g owns k = 8g..8g+7 (K-major:
 // one ds_read_b128; MN-major: two ds_read_b64_tr_b16 of k rows 8g..8g+3 and
@@ -221,11 +235,18 @@ __device__ __forceinline__ void read_sub(const char* sa, const char* sb, int ra,
 
 // MFMAs of fragment rows i in [H*TM/2, (H+1)*TM/2): a sub-step is issued as
 // two such groups with the next fragment reads between them
-template <typename T, int TM, int TN, int H>
+// row_hook(i) runs after the MFMAs of fragment row i: the next stage's
+// LDS-DMA is spread over them (a burst of DMA issues right after the barrier
+// delays the MFMAs behind it; tools/ubench_gemm8.hip "di1": +10-12 %)
+struct NoHook {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+template <typename T, int TM, int TN, int H, typename Hook = NoHook>
 __device__ __forceinline__ void mma_half(floatx4 (&acc)[TM][TN], const typename SubFrag<T>::F (&fa)[TM],
-                                         const typename SubFrag<T>::F (&fb)[TN]) {
+                                         const typename SubFrag<T>::F (&fb)[TN], Hook row_hook = Hook{}) {
 #pragma unroll
-  for (int i = H * TM / 2; i < (H + 1) * TM / 2; ++i)
+  for (int i = H * TM / 2; i < (H + 1) * TM / 2; ++i) {
+    row_hook(i);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       if constexpr (sizeof(T) == 2) {
@@ -236,6 +257,7 @@ __device__ __forceinline__ void mma_half(floatx4 (&acc)[TM][TN], const typename 
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
       }
     }
+  }
 }
 
 // lgkmcnt(0) as a real s_waitcnt (vmcnt/expcnt at max) so the compiler's own
@@ -465,6 +487,13 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
     issue_stage<T, AK, BM, NT>(base, A, lda, m0, k0, tid);
     issue_stage<T, BK_, BN, NT>(base + IA::BYTES, B, ldb, n0, k0, tid);
   };
+  // chunk q (< NL) of stage s: A chunks first, then B
+  auto issue_q = [&](int s, int q) {
+    char* base = smem + (s % NS) * SLOT;
+    const int k0 = kbase + s * IA::BK;
+    if (q < IA::CHUNKS) issue_chunk<T, AK, BM, NT>(base, A, lda, m0, k0, tid, q);
+    else issue_chunk<T, BK_, BN, NT>(base + IA::BYTES, B, ldb, n0, k0, tid, q - IA::CHUNKS);
+  };
 
   // ---- main loop: NS-slot LDS ring, all slots in flight; fragment registers
   // double-buffered one sub-step ahead.  Per stage t:
@@ -502,17 +531,24 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         }
         wait_lgkm0();
         block_barrier();                     // stage t+1 visible; slot t free
-        if constexpr (ISSUE) issue(t + NS);
         MMAD_SB();
       }
-      mma_half<T, TM, TN, 0>(acc, f1a, f1b);
+      // stage t+NS into the freed slot t, spread over this sub-step's MFMA rows
+      auto dma_row = [&](int i) {
+        if constexpr (ISSUE) {
+#pragma unroll
+          for (int q = 0; q < NL; ++q)
+            if (q * TM / NL == i) issue_q(t + NS, q);
+        }
+      };
+      mma_half<T, TM, TN, 0>(acc, f1a, f1b, dma_row);
       MMAD_SB();
       if constexpr (!LAST) {
         const char* sn = smem + ((t + 1) % NS) * SLOT;
         read_sub<T, AK, BK_, NAT, BM, BN, TM, TN>(sn, sn + IA::BYTES, ra, rb, 0, lane, f0a, f0b);
       }
       MMAD_SB();
-      mma_half<T, TM, TN, 1>(acc, f1a, f1b);
+      mma_half<T, TM, TN, 1>(acc, f1a, f1b, dma_row);
       MMAD_SB();
     };
     using T_ = std::true_type;

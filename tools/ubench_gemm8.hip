@@ -60,7 +60,10 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int rbase, int kk, int l
   return *(const bf16x8*)(img + m * 128 + (((kk * 4 + g) ^ ((m >> 1) & 7)) << 4));
 }
 
-template <int BM, int BN, int WM, int WN, int NBUF, int STAG>
+// DI = 1: the next tile's LDS-DMA spread over the MFMAs of the following
+// k-step instead of issued in one burst after the barrier.  NOMMA: no MFMA
+// (fragment reads and the DMA ring only: the operand-feed ceiling)
+template <int BM, int BN, int WM, int WN, int NBUF, int STAG, int DI = 0, int NOMMA = 0>
 __global__ __launch_bounds__(512, 1) void gemm8(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                 bf16* __restrict__ C, int M, int N, int K, int tiles_n,
                                                 int group_m, int store) {
@@ -101,6 +104,20 @@ __global__ __launch_bounds__(512, 1) void gemm8(const bf16* __restrict__ A, cons
     issue_op<BM, NT>(base, A, K, m0, t * 64, tid);
     issue_op<BN, NT>(base + ABYTES, B, K, n0, t * 64, tid);
   };
+  // chunk q (0..NL-1) of tile t's DMA: A chunks first, then B
+  constexpr int CHA = BM * 128 / 16 / NT;
+  auto issue_q = [&](int t, int q) {
+    char* base = smem + (t % NBUF) * SLOT;
+    if (q < CHA) {
+      const int p = NT * q + tid, row = p >> 3, j = (p & 7) ^ ((row >> 1) & 7);
+      dma16(A + (size_t)(m0 + row) * K + t * 64 + j * 8, base + (NT * q + (tid & ~63)) * 16);
+    } else {
+      const int qq = q - CHA;
+      const int p = NT * qq + tid, row = p >> 3, j = (p & 7) ^ ((row >> 1) & 7);
+      dma16(B + (size_t)(n0 + row) * K + t * 64 + j * 8, base + ABYTES + (NT * qq + (tid & ~63)) * 16);
+    }
+  };
+  int pend = -1;   // DI: tile whose DMA is still to be issued during the next MFMAs
   // wait until tile t+1 has landed, given no issue after t+NBUF-1 exists
   auto wait_next = [&](int t) {
     const int later = min(nt - 1, t + NBUF - 1) - (t + 1);   // tiles issued after t+1
@@ -116,12 +133,30 @@ __global__ __launch_bounds__(512, 1) void gemm8(const bf16* __restrict__ A, cons
 #pragma unroll
     for (int j = 0; j < TN; ++j) fb[s][j] = frag(base + ABYTES, rb + j * 16, kk, lane);
   };
+  auto mfma = [&](int s, int i, int j) {
+    if constexpr (NOMMA) {
+      asm volatile("" :: "v"(fa[s][i]), "v"(fb[s][j]));
+    } else {
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][i], fb[s][j], acc[i][j], 0, 0, 0);
+    }
+  };
+  auto pend_issue = [&](int i) {     // DI: this row's share of the pending DMA
+    if constexpr (DI) {
+      if (pend >= 0) {
+#pragma unroll
+        for (int q = 0; q < NL; ++q)
+          if (q * TM / NL == i) issue_q(pend, q);
+        if (i == TM - 1) pend = -1;
+      }
+    }
+  };
   auto mma = [&](int s) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[s][i], fb[s][j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < TN; ++j) mfma(s, i, j);
+      pend_issue(i);
+    }
   };
   // [A](t): MFMAs of k-step 0 with the k-step-1 reads between them
   auto stepA = [&](int t) {
@@ -129,8 +164,8 @@ __global__ __launch_bounds__(512, 1) void gemm8(const bf16* __restrict__ A, cons
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < TN; ++j) mfma(0, i, j);
+      pend_issue(i);
       if (i == 0) {
         const char* base = smem + (t % NBUF) * SLOT;
 #pragma unroll
@@ -149,7 +184,10 @@ __global__ __launch_bounds__(512, 1) void gemm8(const bf16* __restrict__ A, cons
     wait_next(t);
     wait_lgkm0();
     bar();
-    if (t + NBUF < nt) issue(t + NBUF);
+    if (t + NBUF < nt) {
+      if constexpr (DI) pend = t + NBUF;
+      else issue(t + NBUF);
+    }
   };
 
   // prologue
@@ -223,13 +261,13 @@ __global__ void ref_k(const bf16* A, const bf16* B, float* C, int M, int N, int 
   C[(size_t)m * N + n] = s;
 }
 
-template <int BM, int BN, int WM, int WN, int NBUF, int STAG>
+template <int BM, int BN, int WM, int WN, int NBUF, int STAG, int DI = 0, int NOMMA = 0>
 static float run(const bf16* A, const bf16* B, bf16* C, int M, int N, int K, int store, int iters) {
   const int tiles_m = M / BM, tiles_n = N / BN, ntiles = tiles_m * tiles_n;
   int gm = (int)(sqrt(ntiles / 8.0 * BN / BM) + 0.5);
   gm = gm < 1 ? 1 : (gm > tiles_m ? tiles_m : gm);
   auto launch = [&]() {
-    gemm8<BM, BN, WM, WN, NBUF, STAG><<<ntiles, 512>>>(A, B, C, M, N, K, tiles_n, gm, store);
+    gemm8<BM, BN, WM, WN, NBUF, STAG, DI, NOMMA><<<ntiles, 512>>>(A, B, C, M, N, K, tiles_n, gm, store);
   };
   for (int i = 0; i < 3; ++i) launch();
   CK(hipGetLastError());
@@ -306,19 +344,22 @@ int main(int argc, char** argv) {
     }
     mmad_tune_set(0, -1);
   }
-#define RUN(BM_, BN_, WM_, WN_, NB_, ST_)                                                         \
+#define RUN(BM_, BN_, WM_, WN_, NB_, ST_, DI_)                                                    \
   if (M % BM_ == 0 && N % BN_ == 0) {                                                           \
     char nm[64];                                                                                \
-    snprintf(nm, sizeof nm, "gemm8 %dx%d w%dx%d nb%d st%d", BM_, BN_, WM_, WN_, NB_, ST_);      \
-    report(nm, run<BM_, BN_, WM_, WN_, NB_, ST_>(A, B, C, M, N, K, 1, iters), true);            \
+    snprintf(nm, sizeof nm, "gemm8 %dx%d w%dx%d nb%d st%d di%d", BM_, BN_, WM_, WN_, NB_, ST_, DI_); \
+    report(nm, run<BM_, BN_, WM_, WN_, NB_, ST_, DI_>(A, B, C, M, N, K, 1, iters), true);       \
     snprintf(nm, sizeof nm, "  (no store)");                                                    \
-    report(nm, run<BM_, BN_, WM_, WN_, NB_, ST_>(A, B, C, M, N, K, 0, iters), false);           \
+    report(nm, run<BM_, BN_, WM_, WN_, NB_, ST_, DI_>(A, B, C, M, N, K, 0, iters), false);      \
+    snprintf(nm, sizeof nm, "  (no MFMA: feed ceiling)");                                       \
+    report(nm, run<BM_, BN_, WM_, WN_, NB_, ST_, DI_, 1>(A, B, C, M, N, K, 0, iters), false);   \
   }
-  RUN(256, 128, 4, 2, 3, 0)
-  RUN(256, 128, 4, 2, 3, 1)
-  RUN(256, 128, 4, 2, 2, 1)
-  RUN(128, 256, 2, 4, 3, 1)
-  RUN(256, 256, 2, 4, 2, 0)
-  RUN(128, 128, 2, 4, 4, 1)
+  RUN(256, 128, 4, 2, 3, 0, 0)
+  RUN(256, 128, 4, 2, 3, 0, 1)
+  RUN(256, 128, 4, 2, 2, 1, 0)
+  RUN(256, 128, 4, 2, 2, 1, 1)
+  RUN(256, 128, 4, 2, 3, 1, 1)
+  RUN(256, 256, 2, 4, 2, 0, 0)
+  RUN(256, 256, 2, 4, 2, 0, 1)
   return 0;
 }
