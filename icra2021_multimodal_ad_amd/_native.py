@@ -52,6 +52,9 @@ SIGNATURES = {
     "mmad_activation_bwd": (_I, [_I, _F, _I, _I, _P, _I64, _P, _I64, _P, _I64, _P]),
     "mmad_colsum": (_I, [_I, _I, _I, _P, _I, _F, _P, _P]),
     "mmad_sum": (_I, [_I64, _P, _F, _P, _I, _P]),
+    "mmad_mse_loss_ws_floats": (_I, []),
+    "mmad_mse_loss": (_I, [_I64, _P, _P, _I, _P, _P, _P]),
+    "mmad_mse_grad": (_I, [_I64, _P, _P, _P, _I, _P, _P, _P]),
     "mmad_pack_input": (_I, [_I, _I, _I, _I, _I, _P, _I, _P, _P]),
     "mmad_unpack_output": (_I, [_I, _I, _I, _I, _P, _P, _I, _P]),
     "mmad_adam": (_I, [_I64, _P, _P, _P, _P, _F, _F, _F, _F, _F, _P, _I64, _P]),

@@ -1287,3 +1287,68 @@ int mmad_activation_bwd(int act, float slope, int M, int N, const float* y, int6
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Standalone reconstruction loss, modules/loss.py:47-52 (Loss('mse',
+// reduction)): sum (or mean) of (y_hat - y)^2 and its gradient.  (Inside the
+// autoencoder the sum-MSE is fused into the last decoder GEMM's epilogue;
+// this is the plugin-surface Loss called on its own.)  Deterministic: a fixed
+// grid of MSE_PARTS blocks, each a fixed strided order, then one block sums
+// the partials in order.
+namespace {
+constexpr int MSE_PARTS = 256;
+__global__ __launch_bounds__(256) void mse_partials_k(int64_t n, const float* __restrict__ a,
+                                                      const float* __restrict__ b, float* __restrict__ part) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  const bool vec = (((uintptr_t)a | (uintptr_t)b) % 16) == 0;
+  const int64_t n4 = vec ? n / 4 : 0;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)MSE_PARTS * 256) {
+    const floatx4 x = ((const floatx4*)a)[i], y = ((const floatx4*)b)[i];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = x[e] - y[e];
+      acc = fmaf(d, d, acc);
+    }
+  }
+  for (int64_t i = 4 * n4 + blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)MSE_PARTS * 256) {
+    const float d = a[i] - b[i];
+    acc = fmaf(d, d, acc);
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+__global__ __launch_bounds__(256) void mse_grad_k(int64_t n, const float* __restrict__ a,
+                                                  const float* __restrict__ b, const float* __restrict__ g,
+                                                  float scale, float* __restrict__ da, float* __restrict__ db) {
+  const float s = scale * (g ? g[0] : 1.f);
+  for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float d = s * (a[i] - b[i]);
+    if (da) da[i] = d;
+    if (db) db[i] = -d;
+  }
+}
+}  // namespace
+
+int mmad_mse_loss_ws_floats(void) { return MSE_PARTS; }
+
+int mmad_mse_loss(int64_t n, const float* y_hat, const float* y, int mean, float* loss_out, float* work,
+                  void* stream) {
+  MMAD_CHECK_ARG(n >= 1 && y_hat && y && loss_out && work, "mse_loss: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  mse_partials_k<<<MSE_PARTS, 256, 0, s>>>(n, y_hat, y, work);
+  MMAD_LAUNCH_CHECK();
+  return mmad_sum(MSE_PARTS, work, mean ? (float)(1.0 / (double)n) : 1.f, loss_out, 0, stream);
+}
+
+int mmad_mse_grad(int64_t n, const float* y_hat, const float* y, const float* g, int mean, float* d_yhat,
+                  float* d_y, void* stream) {
+  MMAD_CHECK_ARG(n >= 1 && y_hat && y && (d_yhat || d_y), "mse_grad: bad arguments");
+  const float scale = mean ? (float)(2.0 / (double)n) : 2.f;
+  const int64_t blocks = (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096;
+  mse_grad_k<<<(int)blocks, 256, 0, (hipStream_t)stream>>>(n, y_hat, y, g, scale, d_yhat, d_y);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}

@@ -97,10 +97,47 @@ class Activation(nn.Module):
         return _ActivationFn.apply(x, ACT_ENUM[self.name])
 
 
+class _MSEFn(torch.autograd.Function):
+    """modules/loss.py:47-52 sum / mean reduction of (y_hat - y)^2 on the
+    device (mmad_mse_loss: deterministic two-level reduction; backward
+    mmad_mse_grad)."""
+
+    @staticmethod
+    def forward(ctx, y_hat, y, mean):
+        _native.require_gpu(y_hat)
+        a = y_hat.detach().float().contiguous()
+        b = y.detach().to(a.device).float().contiguous()
+        if a.shape != b.shape:
+            raise ValueError(f"mse: y_hat {tuple(a.shape)} and y {tuple(b.shape)} differ")
+        out = torch.empty((), device=a.device, dtype=torch.float32)
+        work = torch.empty(int(_native.load().mmad_mse_loss_ws_floats()), device=a.device)
+        call("mmad_mse_loss", a.numel(), ptr(a), ptr(b), 1 if mean else 0, ptr(out), ptr(work),
+             stream_ptr())
+        ctx.save_for_backward(a, b)
+        ctx.mean = mean
+        ctx.dtypes = (y_hat.dtype, y.dtype)
+        return out.to(y_hat.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = g.detach().float().reshape(1).contiguous()
+        need_a, need_b = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        da = torch.empty_like(a) if need_a else None
+        db = torch.empty_like(b) if need_b else None
+        if need_a or need_b:
+            call("mmad_mse_grad", a.numel(), ptr(a), ptr(b), ptr(g), 1 if ctx.mean else 0, ptr(da),
+                 ptr(db), stream_ptr())
+        return (da.to(ctx.dtypes[0]) if da is not None else None,
+                db.to(ctx.dtypes[1]) if db is not None else None, None)
+
+
 class Loss(nn.Module):
     """modules/loss.py:20-53 (same names/reductions).  The AE's
     ``Loss('mse', reduction='sum')`` is fused into the last decoder GEMM by the
-    native train step; called directly it evaluates with torch ops."""
+    native train step; called on its own the MSE (sum / mean) runs the native
+    mmad_mse_loss / mmad_mse_grad (differentiable); the other criteria, which
+    the autoencoder path never uses, are torch's modules as in the reference."""
 
     def __init__(self, loss, weight=None, reduction="sum"):
         self.reduction = reduction
@@ -128,6 +165,8 @@ class Loss(nn.Module):
         if self.loss is not None:
             if self.is_classification_task():
                 y = y.long()
+            if self.name == "mse" and self.reduction in ("sum", "mean"):
+                return _MSEFn.apply(y_hat, y, self.reduction == "mean")
             return self.loss(y_hat, y)
         return y_hat.mean()
 

@@ -222,6 +222,17 @@ int mmad_colsum(int n_parts, int N, int Np, const float* partials, int part_stri
 
 /* out[0] = scale * sum of n floats (single block, deterministic). */
 int mmad_sum(int64_t n, const float* x, float scale, float* out, int accumulate, void* stream);
+/* modules/loss.py:47-52, Loss('mse', reduction) called on its own (inside the
+ * autoencoder it is fused into the last decoder GEMM): loss_out[0] = sum (mean
+ * != 0: mean) of (y_hat - y)^2 over n fp32 elements, deterministic order.
+ * work: device scratch of mmad_mse_loss_ws_floats() floats.  mmad_mse_grad:
+ * d_yhat = g[0] * (2 or 2/n) * (y_hat - y), d_y = -d_yhat (either nullable;
+ * g = the upstream scalar gradient on the device, nullable = 1). */
+int mmad_mse_loss_ws_floats(void);
+int mmad_mse_loss(int64_t n, const float* y_hat, const float* y, int mean, float* loss_out, float* work,
+                  void* stream);
+int mmad_mse_grad(int64_t n, const float* y_hat, const float* y, const float* g, int mean, float* d_yhat,
+                  float* d_y, void* stream);
 
 /* f32 [M][ld_x] -> packed dtype [Mp][Kp] (zero padding). */
 int mmad_pack_input(int dtype, int M, int K, int Mp, int Kp, const float* x, int ld_x, void* out,

@@ -174,3 +174,25 @@ def test_standalone_activation_matches_torch(act, shape):
     yr.backward(gy)
     assert torch.allclose(y, yr, rtol=1e-5, atol=1e-6)
     assert torch.allclose(x.grad, xr.grad, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("reduction,shape", [("sum", (1000, 1728)), ("mean", (37, 5)), ("sum", (3,))])
+def test_standalone_mse_loss_matches_torch(reduction, shape):
+    """fc_module.Loss('mse', reduction) on its own (modules/loss.py:47-52)
+    runs the native mmad_mse_loss / mmad_mse_grad: loss within 1e-5 relative
+    of torch's MSELoss, both input gradients within 1e-6 (fp32), deterministic
+    (same bits twice); odd sizes take the scalar tail."""
+    from icra2021_multimodal_ad_amd.fc_module import Loss
+    g = torch.Generator().manual_seed(5)
+    a = torch.randn(shape, generator=g).cuda().requires_grad_()
+    b = torch.randn(shape, generator=g).cuda().requires_grad_()
+    crit = Loss("mse", reduction=reduction)
+    out = crit(a, b)
+    ref_a, ref_b = a.detach().cpu().double().requires_grad_(), b.detach().cpu().double().requires_grad_()
+    ref = torch.nn.MSELoss(reduction=reduction)(ref_a, ref_b)
+    assert abs(float(out) - float(ref)) <= 1e-5 * abs(float(ref))
+    assert torch.equal(out, crit(a, b))
+    (out * 3.0).backward()
+    (ref * 3.0).backward()
+    for got, want in ((a.grad, ref_a.grad), (b.grad, ref_b.grad)):
+        assert torch.allclose(got.cpu().double(), want, rtol=1e-6, atol=1e-6)

@@ -1,0 +1,64 @@
+"""BASELINE C5 at its own size: mmad_ae_score_stream at D=2048 with 65,536-row
+batches (the scoring batch bench.py --config c5 and bench_score.py use), bf16.
+
+Checked through the C-ABI: a pass over 2 x 65,536 + 1,000 windows (ragged
+last batch) is finite; the captured hipGraph replay equals the eager pass bit
+for bit; nothing is written past N; and 256 windows (the first and the last
+128) are within the bf16 band of the CPU oracle's get_diffs
+(reconstruction_aggregation.py:6-37) on the same weights and BN statistics,
+per layer: relative Frobenius error of the per-window squared-diff sums
+< 3e-2 (bf16 operands, fp32 accumulation, vs the fp64-accumulated numpy
+restatement in fp32)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+D, BATCH = 2048, 65536
+
+
+def test_score_stream_c5_size_graph_eager_and_oracle():
+    import types
+    from oracle import ae_oracle as O
+    from oracle.model_io import model_from_state_dict
+    from icra2021_multimodal_ad_amd.common_utils import init_state_dict
+    from icra2021_multimodal_ad_amd.data import synth_windows_device
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    from icra2021_multimodal_ad_amd.reconstruction_aggregation import score_windows
+    dev = torch.device("cuda", 0)
+    cfg = types.SimpleNamespace(input_size=D, btl_size=100, n_layers=5, gpu_id=0, dtype="bf16")
+    model = get_model(cfg)
+    sd = init_state_dict(D, 100, 5, seed=77)
+    model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    for i in range(5):                                 # real BN running statistics
+        model.train_step_async(synth_windows_device(1024, D, dev, seed=900 + i))
+    model.eval()
+    nat = model._native
+    n = 2 * BATCH + 1000
+    x = torch.empty((n, D), device=dev)
+    for s in range(0, n, BATCH):
+        k = min(BATCH, n - s)
+        x[s:s + k] = synth_windows_device(k, D, dev, seed=31 + s)
+    out = torch.full((nat.n_enc + 1, n + 7), float("nan"), device=dev)
+    eager = score_windows(x, model, batch_size=BATCH, out=out[:, :n], graph=False).clone()
+    assert torch.isfinite(eager).all()
+    first = score_windows(x, model, batch_size=BATCH, out=out[:, :n]).clone()    # eager + capture
+    out[:, :n].fill_(float("nan"))
+    replay = score_windows(x, model, batch_size=BATCH, out=out[:, :n]).clone()
+    nat.check_status()
+    assert nat._lib.mmad_ae_graph_count(nat._h) >= 1
+    assert torch.equal(first, eager) and torch.equal(replay, eager)
+    assert torch.isnan(out[:, n:]).all()
+    # 256 windows against the oracle on the same weights / BN statistics
+    om = model_from_state_dict({k: v.cpu().numpy() for k, v in model.state_dict().items()})
+    rows = np.r_[0:128, n - 128:n]
+    xs = x[torch.from_numpy(rows).to(dev)].cpu().numpy()
+    diffs = O.get_diffs(xs, om)
+    ref = np.stack([(np.asarray(d, np.float64) ** 2).sum(1) for d in diffs])
+    got = replay[:, torch.from_numpy(rows).to(dev)].double().cpu().numpy()
+    assert ref.shape == got.shape, (ref.shape, got.shape)
+    for layer in range(ref.shape[0]):
+        rel = np.linalg.norm(got[layer] - ref[layer]) / np.linalg.norm(ref[layer])
+        print(f"layer {layer}: rel err {rel:.2e}")
+        assert rel < 3e-2, (layer, rel)
