@@ -83,7 +83,35 @@ def ema_update(v, x, alpha=0.98):
     return x if v is None else v * alpha + (1 - alpha) * x
 
 
-def run_reference(seed):
+def score_reference(model, dset, cfg, train_loader, valid_loader, test_loader, nap=True):
+    """The reference's own scoring of its current model (eval mode, no state
+    change): get_diffs + utils.metric BASE / SAP / NAP."""
+    from reconstruction_aggregation import get_diffs
+    from utils import metric
+    model.eval()
+    with torch.no_grad():
+        tr_x, _ = dset.get_transformed_data(train_loader)
+        va_x, _ = dset.get_transformed_data(valid_loader)
+        te_x, te_y = dset.get_transformed_data(test_loader)
+        te_y = np.where(np.isin(np.asarray(te_y), [cfg.target_class]), True, False)
+        tr = get_diffs(tr_x, model, batch_size=cfg.batch_size)
+        va = get_diffs(va_x, model)
+        te = get_diffs(te_x, model)
+    end = cfg.n_layers + 1 - cfg.end_layer_index
+    res = {}
+    with contextlib.redirect_stdout(io.StringIO()), tempfile.TemporaryDirectory() as td:
+        res["base"] = metric.get_recon_loss(va[0], te[0], te_y, f1_quantiles=[.90])
+        res["sap"] = metric.get_d_loss(tr, va, te, te_y, gpu_id=-1, start_layer_index=cfg.start_layer_index,
+                                       end_layer_index=end, norm_type=2, f1_quantiles=[.90])
+        if nap:
+            cfg.train_diffs = os.path.join(td, "train_diffs.pt")
+            res["nap"] = metric.get_d_norm_loss(tr, va, te, te_y, cfg, gpu_id=-1,
+                                                start_layer_index=cfg.start_layer_index,
+                                                end_layer_index=end, norm_type=2, f1_quantiles=[.90])
+    return res, te_y, len(tr_x)
+
+
+def run_reference(seed, per_epoch_nap=True):
     from model_builder import get_model
     from models.auto_encoder import AutoEncoder
     from reconstruction_aggregation import get_diffs
@@ -96,7 +124,7 @@ def run_reference(seed):
     dset, train_loader, valid_loader, test_loader = get_loaders(cfg, device="cpu")
     optimizer = torch.optim.Adam(model.parameters(), lr=1e-3)
     eng = types.SimpleNamespace(model=model, optimizer=optimizer, config=cfg)
-    train_hist, valid_hist = [], []
+    train_hist, valid_hist, epoch_auroc = [], [], {}
     lowest, best, best_epoch = np.inf, None, 0
     for epoch in range(1, cfg.n_epochs + 1):
         ema = None
@@ -111,28 +139,19 @@ def run_reference(seed):
         if vema < lowest:
             lowest, best, best_epoch = vema, deepcopy(model.state_dict()), epoch
         valid_hist.append(vema)
+        # the reference's AUROC of THIS epoch's model: another implementation
+        # whose best-on-valid selection lands on a near-tie epoch is compared
+        # with the reference at that epoch (tests/test_gpu_e2e.py)
+        r, _, _ = score_reference(model, dset, cfg, train_loader, valid_loader, test_loader,
+                                  nap=per_epoch_nap)
+        for m in r:
+            epoch_auroc.setdefault(m, []).append(float(r[m][1]))
     model.load_state_dict(best)
-    model.eval()
-    with torch.no_grad():
-        tr_x, _ = dset.get_transformed_data(train_loader)
-        va_x, _ = dset.get_transformed_data(valid_loader)
-        te_x, te_y = dset.get_transformed_data(test_loader)
-        te_y = np.where(np.isin(np.asarray(te_y), [cfg.target_class]), True, False)
-        tr = get_diffs(tr_x, model, batch_size=cfg.batch_size)
-        va = get_diffs(va_x, model)
-        te = get_diffs(te_x, model)
+    r, te_y, n_train = score_reference(model, dset, cfg, train_loader, valid_loader, test_loader)
     out = {}
-    end = cfg.n_layers + 1 - cfg.end_layer_index
-    with contextlib.redirect_stdout(io.StringIO()), tempfile.TemporaryDirectory() as td:
-        r_base = metric.get_recon_loss(va[0], te[0], te_y, f1_quantiles=[.90])
-        r_sap = metric.get_d_loss(tr, va, te, te_y, gpu_id=-1, start_layer_index=cfg.start_layer_index,
-                                  end_layer_index=end, norm_type=2, f1_quantiles=[.90])
-        cfg.train_diffs = os.path.join(td, "train_diffs.pt")
-        r_nap = metric.get_d_norm_loss(tr, va, te, te_y, cfg, gpu_id=-1,
-                                       start_layer_index=cfg.start_layer_index, end_layer_index=end,
-                                       norm_type=2, f1_quantiles=[.90])
-    for name, r in (("base", r_base), ("sap", r_sap), ("nap", r_nap)):
-        score, auroc, aupr, f1, prec, rec = r
+    for name in ("base", "sap", "nap"):
+        r_ = r[name]
+        score, auroc, aupr, f1, prec, rec = r_
         out[f"{name}/score"] = np.asarray(score, np.float32)
         out[f"{name}/auroc"] = np.float64(auroc)
         out[f"{name}/aupr"] = np.float64(aupr)
@@ -143,7 +162,9 @@ def run_reference(seed):
     out["train_history"] = np.asarray(train_hist, np.float64)
     out["valid_history"] = np.asarray(valid_hist, np.float64)
     out["best_epoch"] = np.int64(best_epoch)
-    out["n_train"] = np.int64(len(tr_x))
+    out["n_train"] = np.int64(n_train)
+    for m, v in epoch_auroc.items():
+        out[f"epoch_auroc/{m}"] = np.asarray(v, np.float64)
     return out
 
 
@@ -194,11 +215,12 @@ def main():
     for s in a.seeds:
         t0 = time.time()
         torch.set_num_threads(1)
-        o1 = run_reference(s)
+        o1 = run_reference(s, per_epoch_nap=False)
         torch.set_num_threads(8)
         o = run_reference(s)
         for k in ("base/auroc", "sap/auroc", "nap/auroc", "base/aupr", "sap/aupr", "nap/aupr",
-                  "best_epoch", "valid_history", "train_history"):
+                  "best_epoch", "valid_history", "train_history", "epoch_auroc/base",
+                  "epoch_auroc/sap"):
             o["ref1/" + k] = o1[k]
         o.update(run_oracle(s))
         res.update({f"s{s}/{k}": v for k, v in o.items()})

@@ -68,11 +68,16 @@ def _run_cached(g, seed, dtype):
     return _RUNS[(seed, dtype)]
 
 
-def _floor(g, m, key="auroc"):
-    """The reference's own noise floor per seed: |AUROC(8 threads) -
-    AUROC(1 thread)| of two reference trainings of the same program
-    (tests/golden/gen_e2e.py)."""
-    return [abs(float(g[f"s{s_}/{m}/{key}"]) - float(g[f"s{s_}/ref1/{m}/{key}"])) for s_ in (0, 1, 2)]
+def _epoch_floor(g, m):
+    """The reference's own noise floor: |AUROC(8 threads) - AUROC(1 thread)|
+    of two reference trainings of the same program, per seed and epoch
+    (tests/golden/gen_e2e.py scores every epoch's model).  NAP is scored per
+    epoch by the 8-thread run only; its floor is the best-epoch pair."""
+    if f"s0/ref1/epoch_auroc/{m}" in g.files:
+        return np.concatenate([np.abs(g[f"s{s_}/epoch_auroc/{m}"] - g[f"s{s_}/ref1/epoch_auroc/{m}"])
+                               for s_ in (0, 1, 2)])
+    return np.asarray([abs(float(g[f"s{s_}/{m}/auroc"]) - float(g[f"s{s_}/ref1/{m}/auroc"]))
+                       for s_ in (0, 1, 2)])
 
 
 def _record(name, payload):
@@ -87,21 +92,27 @@ def _record(name, payload):
 
 def test_e2e_training_parity_fp32(e2e):
     """Train -> score -> AUROC against the reference's own run, judged by the
-    reference's measured noise floor.  The fixture trains the reference twice
-    per seed (8 and 1 torch threads: two fp32 summation orders of the same
-    program) -- after 20 epochs of Adam it lands 0.0006-0.0096 (BASE),
-    0.007-0.017 (SAP) and 0.016-0.048 (NAP) AUROC from itself, and seed 2
-    even selects a different best epoch (19 vs 15).  The product (a third fp32
-    order, on the GPU) must land as close to the reference as the reference
-    lands to itself: per method, mean over seeds |ours - ref| <= max(0.002,
-    2 x the mean floor), every seed within max(0.002, 3 x the largest floor);
-    the best-on-valid epoch equal to one of the reference's two runs, or a
-    near-tie (the reference's valid loss at our epoch within 3 % of its
-    minimum); train / valid loss EMAs within 5 %.  The per-seed deltas are
-    written to gpurun_out/e2e_fp32_training.json."""
+    reference's measured noise floor.
+
+    The fixture trains the reference twice per seed (8 and 1 torch threads:
+    two fp32 summation orders of the same program) and scores every epoch's
+    model.  Two effects move any other fp32 implementation off it:
+    * the trajectory: at the same epoch the two reference runs differ by the
+      per-epoch floor (AUROC, averaged over epochs and seeds);
+    * the best-on-valid selection (novelty_detection.py:114-125): the
+      validation loss plateaus within a few %, so the argmin flips between
+      near-tie epochs -- the reference's own two runs pick epoch 23 vs 19 on
+      seed 2, and epoch 6 vs the plateau's end moves BASE AUROC by ~0.05.
+    So: (1) the product's best epoch is the argmin of its own validation EMAs
+    (the selection logic) and a near-tie of the reference's (its valid loss
+    there within 3 % of its minimum); (2) the product's AUROC is compared with
+    the reference's AUROC AT THAT EPOCH: mean over seeds |ours - ref| <=
+    max(0.002, 2 x the mean per-epoch floor), every seed <= max(0.002, 3 x the
+    floor's 90th percentile); (3) train / valid loss EMAs within 5 %.  Every
+    value is written to gpurun_out/e2e_fp32_training.json."""
     g = e2e
-    rec = {"what": "product fp32 training vs the reference (8 threads) and the reference's noise "
-                   "floor |ref(8 threads) - ref(1 thread)|", "seeds": {}}
+    rec = {"what": "product fp32 training vs the reference (8 threads) at the product's selected "
+                   "epoch; floor = |ref(8 threads) - ref(1 thread)| per epoch", "seeds": {}}
     deltas = {m: [] for m in METHODS}
     for seed in (0, 1, 2):
         p = f"s{seed}/"
@@ -110,33 +121,38 @@ def test_e2e_training_parity_fp32(e2e):
         assert np.array_equal(lab, g[p + "test_label"])           # same split, same order
         th_dev = float(np.abs(np.asarray(th) / g[p + "train_history"] - 1).max())
         vh_dev = float(np.abs(np.asarray(vh) / g[p + "valid_history"] - 1).max())
-        row = {"best_epoch": int(det.best_epoch), "ref_best_epoch": int(g[p + "best_epoch"]),
+        e = int(det.best_epoch)
+        vref = np.asarray(g[p + "valid_history"])
+        row = {"best_epoch": e, "ref_best_epoch": int(g[p + "best_epoch"]),
                "ref1_best_epoch": int(g[p + "ref1/best_epoch"]),
+               "ref_valid_at_ours_over_min": float(vref[e - 1] / vref.min()),
                "train_ema_max_rel_dev": th_dev, "valid_ema_max_rel_dev": vh_dev}
         for m in METHODS:
-            a, r, r1 = det.last_row[f"{m}_auroc"], float(g[p + f"{m}/auroc"]), float(g[p + f"ref1/{m}/auroc"])
-            deltas[m].append(abs(a - r))
-            row[m] = {"auroc": a, "ref_auroc": r, "ref1_auroc": r1, "delta": a - r, "floor": abs(r1 - r),
-                      "oracle_auroc": float(g[p + f"oracle/{m}/auroc"])}
+            a = det.last_row[f"{m}_auroc"]
+            r_e = float(g[p + f"epoch_auroc/{m}"][e - 1])
+            deltas[m].append(abs(a - r_e))
+            row[m] = {"auroc": a, "ref_auroc_same_epoch": r_e, "ref_auroc_best": float(g[p + f"{m}/auroc"]),
+                      "ref1_auroc_best": float(g[p + f"ref1/{m}/auroc"]), "delta_same_epoch": a - r_e,
+                      "oracle_auroc_best": float(g[p + f"oracle/{m}/auroc"])}
         rec["seeds"][seed] = row
-        print(f"\nseed {seed} fp32: best epoch {det.best_epoch} (ref {row['ref_best_epoch']}, "
-              f"1-thread ref {row['ref1_best_epoch']}); loss EMA dev {th_dev:.2e}/{vh_dev:.2e}; "
-              + "; ".join(f"{m} ours {row[m]['auroc']:.4f} ref {row[m]['ref_auroc']:.4f} "
-                          f"ref1 {row[m]['ref1_auroc']:.4f}" for m in METHODS))
-        vref = np.asarray(g[p + "valid_history"])
-        ok_epoch = (det.best_epoch in (row["ref_best_epoch"], row["ref1_best_epoch"])
-                    or vref[det.best_epoch - 1] <= 1.03 * vref.min())
-        assert ok_epoch, (seed, det.best_epoch, vref.tolist())
+        print(f"\nseed {seed} fp32: best epoch {e} (ref {row['ref_best_epoch']}, 1-thread ref "
+              f"{row['ref1_best_epoch']}; ref valid there {row['ref_valid_at_ours_over_min']:.4f} x min); "
+              f"loss EMA dev {th_dev:.2e}/{vh_dev:.2e}; "
+              + "; ".join(f"{m} ours {row[m]['auroc']:.4f} ref@{e} {row[m]['ref_auroc_same_epoch']:.4f}"
+                          for m in METHODS))
+        assert e == int(np.argmin(np.asarray(vh))) + 1, (e, vh)    # selection logic
+        assert row["ref_valid_at_ours_over_min"] <= 1.03, (seed, e, vref.tolist())
         assert th_dev < 0.05 and vh_dev < 0.05, (seed, th, vh)
     for m in METHODS:
-        fl = _floor(g, m)
-        rec[m] = {"mean_abs_delta": float(np.mean(deltas[m])), "mean_floor": float(np.mean(fl)),
-                  "max_floor": float(np.max(fl))}
+        fl = _epoch_floor(g, m)
+        rec[m] = {"deltas_same_epoch": deltas[m], "mean_abs_delta": float(np.mean(deltas[m])),
+                  "floor_mean": float(np.mean(fl)), "floor_p90": float(np.quantile(fl, 0.9)),
+                  "floor_max": float(np.max(fl))}
     _record("fp32_training", rec)
     for m in METHODS:
-        fl = _floor(g, m)
-        assert np.mean(deltas[m]) <= max(0.002, 2.0 * np.mean(fl)), (m, deltas[m], fl)
-        assert np.max(deltas[m]) <= max(0.002, 3.0 * np.max(fl)), (m, deltas[m], fl)
+        fl = _epoch_floor(g, m)
+        assert np.mean(deltas[m]) <= max(0.002, 2.0 * np.mean(fl)), (m, deltas[m], rec[m])
+        assert np.max(deltas[m]) <= max(0.002, 3.0 * np.quantile(fl, 0.9)), (m, deltas[m], rec[m])
 
 
 def test_e2e_scoring_auroc_parity_on_trained_model(e2e):
@@ -159,14 +175,18 @@ def test_e2e_scoring_auroc_parity_on_trained_model(e2e):
     tr_x, va_x, te_x, lab = det.last_inputs
     te = O.get_diffs(te_x.cpu().numpy(), om)
     ref = {"base": O.base_score(te), "sap": O.sap_score(te)}
-    trc = _device_diffs(model, tr_x, det.config.batch_size).cpu().numpy().astype(np.float64)
+    trc = _device_diffs(model, tr_x, det.config.batch_size).cpu().numpy()
     tec = _device_diffs(model, te_x, 698).cpu().numpy()
-    mu = trc.mean(0)
-    xc = trc - mu
-    _, v = np.linalg.eigh(xc.T @ xc)                 # V of the SVD (N_train > width)
-    v = v[:, ::-1]
-    rot = (xc.astype(np.float32) @ v.astype(np.float32)).astype(np.float64)
-    fit = {"mu_r": mu.astype(np.float32), "v": v.astype(np.float32),
+    # the fit restated in numpy step for step as utils/normalize.py:25-70 does
+    # it (fp32 mean and centring, rotation in fp32) with the SVD's V from an
+    # fp64 eigendecomposition of the Gram matrix of the fp32-centred diffs
+    mu = trc.astype(np.float64).mean(0).astype(np.float32)
+    xc = trc - mu                                    # fp32, as x - mu
+    xd = xc.astype(np.float64)
+    _, v = np.linalg.eigh(xd.T @ xd)                 # V of the SVD (N_train > width)
+    v = v[:, ::-1][:, :min(xc.shape)]
+    rot = (xc @ v.astype(np.float32)).astype(np.float64)
+    fit = {"mu_r": mu, "v": v.astype(np.float32),
            "mu_s": rot.mean(0).astype(np.float32), "var": rot.var(0, ddof=1).astype(np.float32)}
     ref["nap"] = O.nap_score(tec, fit)
     for m in METHODS:
@@ -183,7 +203,8 @@ def test_e2e_bf16_scoring_and_training(e2e):
     """The bf16 throughput path.  Scoring: the fp32-trained model of seed 0
     loaded into a bf16 model scores BASE/SAP within 0.01 AUROC of the fp32
     scoring.  Training: bf16 training lands BASE within 0.02 of the
-    reference's AUROC on every seed; SAP/NAP after bf16 training are printed
+    reference's AUROC at the epoch it selects, on every seed; SAP/NAP after
+    bf16 training are printed
     (their AUROC moves with the training trajectory: the reference's own spread
     over seeds is 0.10 / 0.12)."""
     from icra2021_multimodal_ad_amd.model_builder import get_model
@@ -203,17 +224,23 @@ def test_e2e_bf16_scoring_and_training(e2e):
         print(f"\n{m}: bf16 scoring of the fp32-trained model {a16:.4f} vs fp32 {a32:.4f}")
         assert abs(a16 - a32) <= 0.01, (m, a16, a32)
     diffs = {m: [] for m in METHODS}
+    epochs = []
     for seed in (0, 1, 2):
         det, _, _, _ = _run(g, seed, "bf16")
+        e = int(det.best_epoch)
+        epochs.append(e)
         for m in METHODS:
-            diffs[m].append(det.last_row[f"{m}_auroc"] - float(g[f"s{seed}/{m}/auroc"]))
+            diffs[m].append(det.last_row[f"{m}_auroc"] - float(g[f"s{seed}/epoch_auroc/{m}"][e - 1]))
     for m in METHODS:
         ref = [float(g[f"s{s_}/{m}/auroc"]) for s_ in (0, 1, 2)]
         print(f"\n{m}: reference AUROC mean {np.mean(ref):.4f} (spread {np.ptp(ref):.4f}); "
               f"bf16-trained - reference: {', '.join(f'{d:+.4f}' for d in diffs[m])}")
-    _record("bf16_training", {"what": "bf16-trained product AUROC - reference (8 threads) per seed, "
-                                      "with the reference's fp32 noise floor",
-                              **{m: {"delta": diffs[m], "floor": _floor(g, m)} for m in METHODS}})
+    _record("bf16_training", {"what": "bf16-trained product AUROC - reference (8 threads) at the "
+                                      "product's selected epoch, per seed",
+                              "best_epochs": epochs,
+                              **{m: {"delta_same_epoch": diffs[m],
+                                     "ref_floor_mean": float(np.mean(_epoch_floor(g, m)))}
+                                 for m in METHODS}})
     assert np.max(np.abs(diffs["base"])) <= 0.02, diffs["base"]
 
 
