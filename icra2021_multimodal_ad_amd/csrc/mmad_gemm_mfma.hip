@@ -59,10 +59,25 @@ template <> struct Cfg<2> { static constexpr int BM = 128, BN = 256, WM = 2, WN 
 template <> struct Cfg<3> { static constexpr int BM = 64, BN = 64, WM = 2, WN = 2, NS = 4, NT = 256; };
 template <> struct Cfg<4> { static constexpr int BM = 64, BN = 128, WM = 2, WN = 2, NS = 5, NT = 256; };
 template <> struct Cfg<5> { static constexpr int BM = 128, BN = 128, WM = 2, WN = 2, NS = 4, NT = 256; };
-constexpr int NCFG = 6;
-constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128};
-constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128};
-constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256};
+// 256x256, 8 waves (2 x 4, wave tile 128x64), a 2-slot ring: twice the
+// operand reuse of 256x128 (128 FLOP per staged byte), for the large-row
+// bf16 GEMMs of the forward / score / MSE epilogues without the fused BN
+// (C5 scoring at 65,536 rows; tools/ubench_gemm8.hip: 0.47-0.55 of peak at
+// 16384 x 2048 x 1664 vs 0.33 for 256x128); its epilogue staging fills LDS
+constexpr int CFG_BIG = 6;
+template <> struct Cfg<6> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NS = 2, NT = 512; };
+constexpr int NCFG = 7;
+constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256};
+constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256};
+constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512};
+// the 256x256 tile: bf16 operands, forward-type epilogues, no fused BN
+template <typename T, int EPI>
+constexpr bool big_ok() {
+  return sizeof(T) == 2 && (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_MSE || EPI == GEMM_EPI_SCORE);
+}
+inline bool big_ok_rt(int dtype, int epi) {
+  return dtype == MMAD_BF16 && (epi == GEMM_EPI_FWD || epi == GEMM_EPI_MSE || epi == GEMM_EPI_SCORE);
+}
 
 template <typename T, bool KMAJ, int ROWS, int NT>
 struct Img {
@@ -378,14 +393,19 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   constexpr int SLOT = IA::BYTES + IB::BYTES;
   constexpr int NL = IA::CHUNKS + IB::CHUNKS;          // vm ops per thread per stage
   constexpr bool FWDLIKE = EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_MSE || EPI == GEMM_EPI_SCORE;
-  constexpr int QB = 8;                                // prefetched bias partials per lane
+  constexpr bool BIG = CFG == CFG_BIG;
+  static_assert(!BIG || big_ok<T, EPI>(), "256x256 tile: bf16 forward-type epilogues only");
+  // prefetched bias partials per lane (none for the 256x256 tile: its
+  // 128 accumulator registers leave no room to hold them across the loop)
+  constexpr int QB = BIG ? 0 : 8;
   constexpr int QG = 32;                               // prefetched dW row-sum partials
   constexpr int OSTRIDE = BN * (int)sizeof(TO) + 16;
   constexpr int OBYTES = BM * OSTRIDE + (EPI == GEMM_EPI_BWD_DATA ? BM * BN / 2 : 0);   // + fp64 [BM/16][BN]
   // fused train-mode BN: per-column merge results (2 x fp64 [BN]) + a flag word
   // (fwd: 4 chunk-group Welford merges + scale/shift; bwd-data: the sums --
   // its chunk-group sums reuse the fp64 piece scratch)
-  constexpr int XBYTES = EPI == GEMM_EPI_FWD ? 12 * BN * 8 + 2 * BN * 4 + 64
+  constexpr int XBYTES = BIG ? 0
+                         : EPI == GEMM_EPI_FWD ? 12 * BN * 8 + 2 * BN * 4 + 64
                          : EPI == GEMM_EPI_BWD_DATA ? 6 * BN * 8 + 64 : 0;
   constexpr int LDS_BYTES = (NS * SLOT > OBYTES + XBYTES) ? NS * SLOT : OBYTES + XBYTES;
   static_assert((NS - 1) * NL <= 63, "vmcnt range");
@@ -431,8 +451,9 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   const int g = lane >> 4, c = lane & 15;
   const int rw = m0 + wm * 16 * TM;  // first row of this wave
   const int cw = n0 + wn * 16 * TN;  // first col of this wave
-  float e_b[TN], e_s[TN], e_t[TN], e_p[TN][QB];
-  if constexpr (FWDLIKE) {
+  float e_b[TN], e_s[TN], e_t[TN], e_p[TN][QB > 0 ? QB : 1];
+  // (the 256x256 tile loads them after the loop: no registers to spare)
+  auto load_epi_consts = [&]() {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = cw + j * 16 + c;
@@ -448,7 +469,9 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         }
       }
     }
-  }
+  };
+  if constexpr (FWDLIKE && !BIG) load_epi_consts();
+
   // fused BN: this column's barrier generation, read before this block can
   // arrive (its latency hides under the main loop)
   unsigned gen0 = 0u;
@@ -504,7 +527,64 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   // hipcc's lgkmcnt bookkeeping stays exact, and sched_barriers pin the order.
   using FR = typename SubFrag<T>::F;
   const int ra = wm * 16 * TM, rb = wn * 16 * TN;
-  if (nt > 0) {
+  if constexpr (BIG) {
+    // 256x256 tile (bf16, both operands K-major): a 2-slot ring, one barrier
+    // per stage after both 32-deep sub-steps; the fragment registers of a
+    // sub-step are re-read row by row under the MFMAs that free them (their
+    // lifetimes do not overlap, so the 128 accumulators fit beside them), and
+    // stage t+2 is issued over the MFMA rows of stage t+1's first sub-step
+    // (tools/ubench_gemm8.hip "256x256 nb2 st0 di1")
+    if (nt > 0) {
+      FR fa[2][TM], fb[2][TN];
+      auto rd = [&](int t, int kk, int sl) {
+        const char* base = smem + (t % NS) * SLOT;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[sl][i] = frag_bf16<true, true, BM>(base, ra + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[sl][j] = frag_bf16<true, true, BN>(base + IA::BYTES, rb + j * 16, kk, lane);
+      };
+      int pend = -1;
+      issue(0);
+      if (nt > 1) issue(1);
+      if (nt > 1) wait_vmcnt<NL>();
+      else wait_vmcnt<0>();
+      block_barrier();
+      rd(0, 0, 0);
+      for (int t = 0; t < nt; ++t) {
+        const char* base = smem + (t % NS) * SLOT;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
+          if (pend >= 0) {
+#pragma unroll
+            for (int q = 0; q < NL; ++q)
+              if (q * TM / NL == i) issue_q(pend, q);
+          }
+          if (i == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              fb[1][j] = frag_bf16<true, true, BN>(base + IA::BYTES, rb + j * 16, 1, lane);
+          }
+          fa[1][i] = frag_bf16<true, true, BM>(base, ra + i * 16, 1, lane);
+        }
+        pend = -1;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1][i], fb[1][j], acc[i][j], 0, 0, 0);
+        if (t + 1 < nt) {
+          wait_vmcnt<0>();                   // stage t+1 landed (the only one in flight)
+          wait_lgkm0();
+          block_barrier();                   // stage t+1 visible; slot t free
+          if (t + 2 < nt) pend = t + 2;
+          rd(t + 1, 0, 0);
+        }
+      }
+    }
+  } else if (nt > 0) {
 #pragma unroll
     for (int s = 0; s < NS; ++s)
       if (s < nt) issue(s);
@@ -565,7 +645,9 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   // order (p0 + p1 + ... : independent of arrival order) and runs the
   // epilogue.  Counters / flags start at 0 (caller memset) and the last block
   // resets them, so consecutive launches on one stream reuse them.
-  if (S > 1) {
+  // (the 256x256 tile never splits: its combine would need a second set of
+  // 128 accumulator registers; the dispatcher does not pick it for a split)
+  if (!BIG && S > 1) {
     unsigned* cnt = ep.sk_ctl + tile;
     unsigned* flg = ep.sk_ctl + ntl + (size_t)tile * S;
     __syncthreads();
@@ -684,6 +766,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
     if (sum == 1.2345e-30f) ((float*)ep.out)[tid] = sum;
     return;
   }
+  if constexpr (FWDLIKE && BIG) load_epi_consts();
   // ===================== epilogue, register phase ==========================
   // per-call values of a graph-captured step come from device memory
   const float* tgt = ep.target;
@@ -815,7 +898,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   // fused BN (forward): the Welford partials are out -- arrive at the column
   // barrier now, store the a tile while the other blocks catch up
   unsigned* bn_shw = (unsigned*)(smem + OBYTES + XBYTES - 64);
-  if constexpr (EPI == GEMM_EPI_FWD) {
+  if constexpr (EPI == GEMM_EPI_FWD && !BIG) {
     if (ep.bn_sync) col_arrive(ep.bn_sync + tn, (unsigned)(ntl / ep.tiles_n), tid, bn_shw);
   }
   __syncthreads();  // main-loop LDS no longer read
@@ -946,7 +1029,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       }
     }
   }
-  if constexpr (EPI == GEMM_EPI_FWD) {
+  if constexpr (EPI == GEMM_EPI_FWD && !BIG) {
     if (ep.bn_sync) {
       // ---- fused BatchNorm(train) of this layer (layers/fc_layer.py:37-48,
       // Linear -> act -> BN): whole-batch mean / variance merged from every
@@ -1256,8 +1339,9 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
 // -------------------------------------------------------------------------
 // host-side planning and launch
 // -------------------------------------------------------------------------
-static bool cfg_fits(int cfg, int Mp, int Np, int epi) {
+static bool cfg_fits(int cfg, int Mp, int Np, int epi, int dtype) {
   if (Mp % CFG_BM[cfg] || Np % CFG_BN[cfg]) return false;
+  if (cfg == CFG_BIG && !big_ok_rt(dtype, epi)) return false;
   // the score epilogue reduces rows over 128-column groups inside one tile
   if (epi == GEMM_EPI_SCORE && CFG_BN[cfg] < 128) return false;
   return true;
@@ -1270,9 +1354,9 @@ int mmad_gemm_tiles(int Mp, int Np) { return (Mp / 64) * (Np / 64); }
 // static choice when autotuning is off or impossible (stream capture)
 template <typename Pred>
 static int heuristic_cfg(int Mp, int Np, int epi, Pred allowed) {
-  const int order[] = {1, 0, 5, 4, 3};
-  const int want[] = {200, 200, 200, 160, 0};
-  for (int i = 0; i < 5; ++i) {
+  const int order[] = {CFG_BIG, 1, 0, 5, 4, 3};
+  const int want[] = {512, 200, 200, 200, 160, 0};
+  for (int i = 0; i < 6; ++i) {
     const int c = order[i];
     if (!allowed(c)) continue;
     if (mmad_gemm_ntiles(c, Mp, Np) >= want[i]) return c;
@@ -1282,8 +1366,8 @@ static int heuristic_cfg(int Mp, int Np, int epi, Pred allowed) {
   (void)Mp; (void)Np; (void)epi;
   return -1;
 }
-static int heuristic_cfg(int Mp, int Np, int epi) {
-  return heuristic_cfg(Mp, Np, epi, [&](int c) { return cfg_fits(c, Mp, Np, epi); });
+static int heuristic_cfg(int Mp, int Np, int epi, int dtype) {
+  return heuristic_cfg(Mp, Np, epi, [&](int c) { return cfg_fits(c, Mp, Np, epi, dtype); });
 }
 
 // group height balancing the per-XCD A-panel (gm*BM rows) and B-panel
@@ -1313,7 +1397,15 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
     case 2: mmad_gemm_kernel<T, TO, AK, BK_, 2, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
     case 3: mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
     case 4: mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
-    default: mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
+    case 5: mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
+    default:
+      if constexpr (big_ok<T, EPI>()) {
+        mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep);
+      } else {
+        mmad_set_error("gemm: tile configuration %d does not support this dtype / epilogue", cfg);
+        return MMAD_EUNSUPPORTED;
+      }
+      break;
   }
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
@@ -1328,7 +1420,10 @@ static const void* kernel_ptr(int cfg) {
     case 2: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 2, EPI>;
     case 3: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI>;
     case 4: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI>;
-    default: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI>;
+    case 5: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI>;
+    default:
+      if constexpr (big_ok<T, EPI>()) return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI>;
+      return nullptr;
   }
 }
 static const void* kernel_for(int dtype, int epi, int cfg) {
@@ -1384,7 +1479,7 @@ bool mmad_gemm_bn_fusable(int dtype, int epi, int Mp, int Np) {
   if (epi != GEMM_EPI_FWD && epi != GEMM_EPI_BWD_DATA) return false;
   if (Mp % 128 || Np % 128 || Np / 64 > MMAD_BN_EXIT) return false;
   for (int c = 0; c < NCFG; ++c)
-    if (cfg_fits(c, Mp, Np, epi) && coresident(dtype, epi, c, Mp, Np)) return true;
+    if (cfg_fits(c, Mp, Np, epi, dtype) && c != CFG_BIG && coresident(dtype, epi, c, Mp, Np)) return true;
   return false;
 }
 
@@ -1441,7 +1536,8 @@ static int tune_cfg(int dtype, int epi, const void* A, int lda, const void* B, i
   float best_ms = 1e30f;
   int rc = MMAD_OK;
   for (int c = 0; c < NCFG && rc == MMAD_OK; ++c) {
-    if (!cfg_fits(c, Mp, Np, epi)) continue;
+    if (!cfg_fits(c, Mp, Np, epi, dtype)) continue;
+    if (c == CFG_BIG && (ep.bn_sync || ep.splitk > 1)) continue;   // no fused BN / split on 256x256
     if (ep.bn_sync && !coresident(dtype, epi, c, Mp, Np)) continue;
     rc = launch_cfg(dtype, epi, A, lda, B, ldb, Mp, Np, K, et, c, s);   // warm
     if (rc != MMAD_OK) break;
@@ -1539,10 +1635,10 @@ int mmad_gemm_read_status(unsigned* ctl, hipStream_t s, const char* who) {
 
 int mmad_gemm_plan(int Mp, int Np, int K, int epi, int dtype) {
   const int env = mmad_tile_override();
-  if (env >= 0 && env < NCFG && cfg_fits(env, Mp, Np, epi)) return env;
+  if (env >= 0 && env < NCFG && cfg_fits(env, Mp, Np, epi, dtype)) return env;
   std::lock_guard<std::mutex> lk(g_tune_mu);
   auto it = g_tune.find(TuneKey{dtype, epi, Mp, Np, K, 0});
-  return it != g_tune.end() ? it->second : heuristic_cfg(Mp, Np, epi);
+  return it != g_tune.end() ? it->second : heuristic_cfg(Mp, Np, epi, dtype);
 }
 
 int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B, int ldb, int Mp,
@@ -1561,7 +1657,9 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   // whole grid resident
   ep.splitk = (ep.sk_slab && ep.sk_ctl && !bnf) ? mmad_gemm_splitk(Mp, Np, K, dtype, epi) : 1;
   auto allowed = [&](int c) {
-    return c >= 0 && c < NCFG && cfg_fits(c, Mp, Np, epi) && (!bnf || coresident(dtype, epi, c, Mp, Np));
+    return c >= 0 && c < NCFG && cfg_fits(c, Mp, Np, epi, dtype) &&
+           (c != CFG_BIG || ep.splitk <= 1) &&
+           (!bnf || (c != CFG_BIG && coresident(dtype, epi, c, Mp, Np)));
   };
   const int env = mmad_tile_override();
   const int env_epi = ep.ad_p ? mmad_tile_adam_for(Mp, Np, K) : mmad_tile_epi_override(epi);
