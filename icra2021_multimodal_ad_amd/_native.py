@@ -90,8 +90,15 @@ SIGNATURES = {
     "mmad_comm_get_unique_id": (_I, [_P]),
     "mmad_comm_create": (_I, [ctypes.POINTER(_P), _P, _I, _I]),
     "mmad_comm_create_loopback": (_I, [ctypes.POINTER(_P), _F]),
+    "mmad_comm_create_loopback_ranks": (_I, [ctypes.POINTER(_P), _F, _I, _I]),
     "mmad_comm_destroy": (None, [_P]),
     "mmad_allreduce_bucket": (_I, [_P, _P, _I64, _P]),
+    "mmad_comm_rank": (_I, [_P]),
+    "mmad_comm_size": (_I, [_P]),
+    "mmad_reduce_scatter_bucket": (_I, [_P, _P, _I64, _P]),
+    "mmad_all_gather_bucket": (_I, [_P, _P, _I64, _I, _P]),
+    "mmad_ae_dp_sync_master": (_I, [_P, _P]),
+    "mmad_ae_dp_master_stale": (_I, [_P]),
     "mmad_ae_set_comm": (_I, [_P, _P]),
     "mmad_nap_fit_ws_bytes": (ctypes.c_size_t, [_I64, _I]),
     "mmad_minmax_norm_ws_bytes": (ctypes.c_size_t, [_I64, _I]),
@@ -112,7 +119,7 @@ KNOB = dict(tile=0, group_m=1, autotune=2, dbg=3, splitk=4, tile_adam=5, tile_bw
             tile_fwd=7, tile_adam_main=8, splitk_dw=9, splitk_dw_blocks=10, splitk_dw_min_stages=11,
             bn_mode=16, bn_mode_bwd=17, bn_fused_rows=18, dw_main=19, pair_rows=20, dw_main_ping=21,
             ev_every=22, loss_side=23, dp_small_at=24, keep_grads=25, side_prio=26,
-            event_sysfence=27)
+            event_sysfence=27, dp_shard=28)
 # host-side schedule choices of the Python executor wrapper (engine.py), read
 # when a model is built: a second bf16 weight shadow (ping-pong), and whether
 # train_step replays one captured hipGraph per step instead of the eager enqueue

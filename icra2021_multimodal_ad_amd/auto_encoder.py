@@ -206,7 +206,14 @@ class AutoEncoder(AbstractModel):
         return self
 
     def state_dict(self, *args, **kwargs):
-        """Reference key layout (60 keys for n_layers=5), contiguous copies."""
+        """Reference key layout (60 keys for n_layers=5), contiguous copies.
+        After sharded data-parallel steps the master weights are current only
+        on their owning ranks: call ``model.dist.epoch_end(model)`` (or
+        ``model._native.sync_master()``) on EVERY rank first -- doing it here
+        would put a collective into a call one rank may make alone."""
+        if getattr(self, "_native", None) is not None and self._native.master_stale:
+            raise RuntimeError("state_dict: the master weights are sharded over the data-parallel "
+                               "ranks; call model.dist.epoch_end(model) on every rank first")
         self._flush_counters()
         sd = super().state_dict(*args, **kwargs)
         if not kwargs.get("keep_vars", False):

@@ -75,6 +75,11 @@ struct mmad_ae {
   // goes on the comm stream right after the bwd-data GEMM of this layer
   // (ahead of this layer's and the lower layers' weight buckets); knob 24
   int dp_small_at = 1;
+  // data-parallel step: sharded weight buckets (knob 28); master_stale: the
+  // bf16 model's fp32 master weights / every model's Adam moments are
+  // current only on their owning rank since the last mmad_ae_dp_sync_master
+  int dp_shard = 1;
+  bool master_stale = false;
   int mse_tiles = 0;   // loss partials written by the last MSE GEMM
   // data parallelism: RCCL communicator (not owned), its stream and events
   mmad_comm* comm = nullptr;
@@ -347,6 +352,7 @@ int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, i
     h->dp_small_at = mmad_knob(24);
     h->keep_grads = mmad_knob(25);
     h->side_prio_hi = mmad_knob(26);
+    h->dp_shard = mmad_knob(28);
     h->ev_flags_ = ev_flags(mmad_knob(27));
   }
   for (int side = 0; side < 2; ++side) {
@@ -850,10 +856,27 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_dw[l], 0));
       MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_data[l], 0));
       const int64_t n = (int64_t)a.Np * a.Kp;
-      RET_IF(mmad_allreduce_bucket(h->comm, h->grads + a.w_off, n, h->cstream));
-      RET_IF(mmad_adam(n, h->params + a.w_off, h->grads + a.w_off, h->m + a.w_off, h->v + a.w_off,
-                       adam->b1, adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt,
-                       adam_shadow(h, a, w.ping), h->dtype == MMAD_BF16 ? n : 0, h->cstream));
+      const int nr = mmad_comm_size(h->comm) > 0 ? mmad_comm_size(h->comm) : 1;
+      if (h->dp_shard && n % nr == 0 && (n / nr) % 4 == 0) {
+        // ZeRO-1 form: reduce-scatter, Adam on this rank's shard, all-gather
+        // of the updated weights the next step reads (bf16 shadow / fp32 p)
+        const int64_t cnt = n / nr, off = a.w_off + (int64_t)mmad_comm_rank(h->comm) * cnt;
+        RET_IF(mmad_reduce_scatter_bucket(h->comm, h->grads + a.w_off, n, h->cstream));
+        void* sh = h->dtype == MMAD_BF16 ? (void*)((char*)h->shadow + off * 2) : nullptr;
+        RET_IF(mmad_adam(cnt, h->params + off, h->grads + off, h->m + off, h->v + off, adam->b1,
+                         adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt, sh,
+                         h->dtype == MMAD_BF16 ? cnt : 0, h->cstream));
+        if (h->dtype == MMAD_BF16)
+          RET_IF(mmad_all_gather_bucket(h->comm, (char*)h->shadow + a.w_off * 2, n, MMAD_BF16, h->cstream));
+        else
+          RET_IF(mmad_all_gather_bucket(h->comm, h->params + a.w_off, n, MMAD_F32, h->cstream));
+        if (nr > 1) h->master_stale = true;
+      } else {
+        RET_IF(mmad_allreduce_bucket(h->comm, h->grads + a.w_off, n, h->cstream));
+        RET_IF(mmad_adam(n, h->params + a.w_off, h->grads + a.w_off, h->m + a.w_off, h->v + a.w_off,
+                         adam->b1, adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt,
+                         adam_shadow(h, a, w.ping), h->dtype == MMAD_BF16 ? n : 0, h->cstream));
+      }
     } else if (adam) {
       // dW_l with this layer's Adam update fused into its epilogue.  It rewrites
       // W_l, so it starts only once the main stream has finished reading W_l
@@ -1085,6 +1108,9 @@ int mmad_ae_train_graph_count(const mmad_ae* h) { return h ? (int)h->tgraphs.siz
 int mmad_ae_set_comm(mmad_ae* h, mmad_comm* c) {
   MMAD_CHECK_ARG(h, "ae_set_comm: null handle");
   MMAD_CHECK_ARG(h->side, "ae_set_comm: bind the handle first");
+  MMAD_CHECK_ARG(c == h->comm || !h->master_stale,
+                 "ae_set_comm: the master weights are sharded over the ranks of the attached "
+                 "communicator: mmad_ae_dp_sync_master on every rank first");
   if (c && !h->cstream) {
     // highest priority: the exchange must not queue behind the dW GEMMs
     int least = 0, greatest = 0;
@@ -1096,6 +1122,24 @@ int mmad_ae_set_comm(mmad_ae* h, mmad_comm* c) {
     MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_cdone, h->ev_flags_));
   }
   h->comm = c;
+  return MMAD_OK;
+}
+
+int mmad_ae_dp_master_stale(const mmad_ae* h) { return h && h->master_stale ? 1 : 0; }
+
+int mmad_ae_dp_sync_master(mmad_ae* h, void* stream) {
+  MMAD_CHECK_ARG(h && h->params && h->m && h->v, "ae_dp_sync_master: unbound handle");
+  if (!h->comm || !h->master_stale) return MMAD_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int nr = mmad_comm_size(h->comm);
+  for (const AeLayer& a : h->L) {
+    const int64_t n = (int64_t)a.Np * a.Kp;
+    if (!(n % nr == 0 && (n / nr) % 4 == 0)) continue;   // an all-reduced bucket: already current
+    if (h->dtype == MMAD_BF16) RET_IF(mmad_all_gather_bucket(h->comm, h->params + a.w_off, n, MMAD_F32, st));
+    RET_IF(mmad_all_gather_bucket(h->comm, h->m + a.w_off, n, MMAD_F32, st));
+    RET_IF(mmad_all_gather_bucket(h->comm, h->v + a.w_off, n, MMAD_F32, st));
+  }
+  h->master_stale = false;
   return MMAD_OK;
 }
 

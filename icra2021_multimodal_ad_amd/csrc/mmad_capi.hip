@@ -61,6 +61,7 @@ int g_knob[MMAD_KNOB_COUNT] = {
     0,     // 25 also materialise dW in the fused step (grads buffer)
     0,     // 26 side stream at the highest priority (schedule sweeps)
     0,     // 27 executor events with the system-scope fence
+    1,     // 28 DP: sharded weight buckets (reduce-scatter, Adam on 1/N, all-gather)
 };
 }  // namespace
 int mmad_knob(int k) { return g_knob[k]; }

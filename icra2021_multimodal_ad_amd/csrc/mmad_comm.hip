@@ -22,6 +22,9 @@ struct RcclApi {
   ncclResult_t (*comm_destroy)(ncclComm_t);
   ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                              hipStream_t);
+  ncclResult_t (*reduce_scatter)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                                 hipStream_t);
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
   const char* (*error_string)(ncclResult_t);
   bool ok;
 };
@@ -37,9 +40,11 @@ const RcclApi& rccl() {
     api.comm_init_rank = (decltype(api.comm_init_rank))dlsym(h, "ncclCommInitRank");
     api.comm_destroy = (decltype(api.comm_destroy))dlsym(h, "ncclCommDestroy");
     api.all_reduce = (decltype(api.all_reduce))dlsym(h, "ncclAllReduce");
+    api.reduce_scatter = (decltype(api.reduce_scatter))dlsym(h, "ncclReduceScatter");
+    api.all_gather = (decltype(api.all_gather))dlsym(h, "ncclAllGather");
     api.error_string = (decltype(api.error_string))dlsym(h, "ncclGetErrorString");
     api.ok = api.get_unique_id && api.comm_init_rank && api.comm_destroy && api.all_reduce &&
-             api.error_string;
+             api.reduce_scatter && api.all_gather && api.error_string;
   });
   return api;
 }
@@ -104,9 +109,16 @@ int mmad_comm_create(mmad_comm** out, const void* unique_id, int nranks, int ran
 }
 
 int mmad_comm_create_loopback(mmad_comm** out, float scale) {
-  MMAD_CHECK_ARG(out && scale > 0.f, "comm_create_loopback: bad arguments");
+  return mmad_comm_create_loopback_ranks(out, scale, 1, 0);
+}
+
+int mmad_comm_create_loopback_ranks(mmad_comm** out, float scale, int nranks, int rank) {
+  MMAD_CHECK_ARG(out && scale > 0.f && nranks >= 1 && rank >= 0 && rank < nranks,
+                 "comm_create_loopback: bad arguments");
   mmad_comm* c = new mmad_comm;
   c->loopback = scale;
+  c->nranks = nranks;
+  c->rank = rank;
   *out = c;
   return MMAD_OK;
 }
@@ -132,3 +144,33 @@ int mmad_allreduce_bucket(mmad_comm* c, float* buf, int64_t n, void* stream) {
 }
 
 int mmad_comm_size(const mmad_comm* c) { return c ? c->nranks : 0; }
+int mmad_comm_rank(const mmad_comm* c) { return c ? c->rank : -1; }
+
+// Sharded exchange (the data-parallel step's ZeRO-1 form: each rank updates
+// the Adam state of its 1/N of a bucket).  In place, RCCL's own in-place
+// convention: rank r's shard is buf[r*n/N, (r+1)*n/N).
+int mmad_reduce_scatter_bucket(mmad_comm* c, float* buf, int64_t n, void* stream) {
+  MMAD_CHECK_ARG(c && (buf || n == 0) && n >= 0, "reduce_scatter_bucket: bad arguments");
+  MMAD_CHECK_ARG(n % c->nranks == 0, "reduce_scatter_bucket: n=%lld not divisible by %d ranks",
+                 (long long)n, c->nranks);
+  if (n == 0) return MMAD_OK;
+  if (c->loopback > 0.f) return mmad_allreduce_bucket(c, buf, n, stream);   // one rank: shard = all
+  const size_t cnt = (size_t)(n / c->nranks);
+  MMAD_RCCL_CHECK(rccl().reduce_scatter(buf, buf + (size_t)c->rank * cnt, cnt, ncclFloat32, ncclSum,
+                                        c->comm, (hipStream_t)stream));
+  return MMAD_OK;
+}
+
+int mmad_all_gather_bucket(mmad_comm* c, void* buf, int64_t n, int dtype, void* stream) {
+  MMAD_CHECK_ARG(c && (buf || n == 0) && n >= 0, "all_gather_bucket: bad arguments");
+  MMAD_CHECK_ARG(dtype == MMAD_F32 || dtype == MMAD_BF16, "all_gather_bucket: bad dtype %d", dtype);
+  MMAD_CHECK_ARG(n % c->nranks == 0, "all_gather_bucket: n=%lld not divisible by %d ranks", (long long)n,
+                 c->nranks);
+  if (n == 0 || c->loopback > 0.f || c->nranks == 1) return MMAD_OK;   // one rank holds every shard
+  const size_t cnt = (size_t)(n / c->nranks);
+  const size_t es = dtype == MMAD_BF16 ? 2 : 4;
+  MMAD_RCCL_CHECK(rccl().all_gather((const char*)buf + (size_t)c->rank * cnt * es, buf, cnt,
+                                    dtype == MMAD_BF16 ? ncclBfloat16 : ncclFloat32, c->comm,
+                                    (hipStream_t)stream));
+  return MMAD_OK;
+}

@@ -150,6 +150,23 @@ class NativeComm:
         want = self.world * (self.world + 1) / 2.0
         if not bool(torch.all(buf == want)):
             raise RuntimeError(f"native all-reduce self-test: got {float(buf[0])}, want {want}")
+        # every collective the sharded step uses: reduce-scatter (fp32) and
+        # all-gather (fp32 and bf16), in place
+        n = 4096 * self.world
+        buf = torch.full((n,), float(self.rank + 1), device="cuda", dtype=torch.float32)
+        _native.check(self._lib.mmad_reduce_scatter_bucket(self.handle, ptr(buf), n, stream_ptr()),
+                      "mmad_reduce_scatter_bucket")
+        shard = buf[self.rank * 4096:(self.rank + 1) * 4096]
+        if not bool(torch.all(shard == want)):
+            raise RuntimeError(f"native reduce-scatter self-test: got {float(shard[0])}, want {want}")
+        owners = torch.arange(self.world, device="cuda").repeat_interleave(4096).float() + 1.0
+        for dt, code in ((torch.float32, _native.F32), (torch.bfloat16, _native.BF16)):
+            g = torch.zeros(n, device="cuda", dtype=dt)
+            g[self.rank * 4096:(self.rank + 1) * 4096] = float(self.rank + 1)
+            _native.check(self._lib.mmad_all_gather_bucket(self.handle, ptr(g), n, code, stream_ptr()),
+                          "mmad_all_gather_bucket")
+            if not bool(torch.all(g.float() == owners)):
+                raise RuntimeError(f"native all-gather self-test ({dt}) failed")
 
     def close(self):
         if self.handle is not None and self.handle.value:
@@ -240,6 +257,14 @@ class DataParallel:
         if self.world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         return t
+
+    def epoch_end(self, model):
+        """Every rank, at every epoch end (before validation, which may deep-
+        copy the state_dict): all-gather the sharded master weights / Adam
+        moments of the native exchange, average the BN running statistics."""
+        if self.native:
+            model._native.sync_master()
+        self.average_running_stats(model)
 
     def average_running_stats(self, model):
         """BatchNorm running mean / var averaged over the ranks (SURVEY

@@ -121,10 +121,28 @@ class NativeAE:
         return self
 
     def set_comm(self, comm):
-        """Attach a dist.NativeComm (or None): mmad_ae_train_step then all-reduces
-        each layer's gradients on the executor's comm stream before its Adam."""
+        """Attach a dist.NativeComm (or None): mmad_ae_train_step then exchanges
+        each layer's gradients on the executor's comm stream before its Adam
+        (sharded: reduce-scatter, Adam on this rank's 1/N, all-gather).
+        Detaching first all-gathers the sharded master weights / Adam moments
+        (sync_master: collective, so detach on every rank at the same point)."""
+        if comm is None and getattr(self, "_comm", None) is not None:
+            self.sync_master()
         self._comm = comm        # keep the communicator alive as long as the handle uses it
         call("mmad_ae_set_comm", self._h, comm.handle if comm is not None else None)
+
+    @property
+    def master_stale(self):
+        """True while the sharded DP step has left the fp32 master weights (bf16
+        model) / the Adam moments current only on their owning rank."""
+        return bool(self._lib.mmad_ae_dp_master_stale(self._h))
+
+    def sync_master(self):
+        """All-gather the shards of the master weights and Adam moments after
+        sharded DP steps (collective: every rank, same point; a no-op when
+        nothing is stale)."""
+        if self.master_stale:
+            call("mmad_ae_dp_sync_master", self._h, stream_ptr())
 
     def __del__(self):
         try:

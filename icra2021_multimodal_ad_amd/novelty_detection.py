@@ -146,8 +146,9 @@ class NoveltyDetecter:
 
         if getattr(model, "dist", None) is not None:
             # data parallel: per-shard BN running statistics averaged for eval
+            # (and the sharded master weights gathered before any state_dict copy)
             trainer.add_event_handler(Events.EPOCH_COMPLETED,
-                                      lambda engine: model.dist.average_running_stats(model))
+                                      lambda engine: model.dist.epoch_end(model))
         trainer.add_event_handler(Events.EPOCH_COMPLETED, run_validation, evaluator, valid_loader)
 
         @trainer.on(Events.EPOCH_COMPLETED)

@@ -75,8 +75,10 @@ int mmad_pad_granule(void);
  *   24 data parallel: exchange the small bucket after this layer's bwd-data (1)
  *   25 also materialise dW in the fused step (0)
  *   26 side stream at the highest priority instead of the lowest (0)
- *   27 executor events with the system-scope fence (0) */
-#define MMAD_KNOB_COUNT 28
+ *   27 executor events with the system-scope fence (0)
+ *   28 data parallel: sharded weight buckets (reduce-scatter, Adam on 1/N,
+ *      all-gather; 1) or all-reduce + full Adam (0) */
+#define MMAD_KNOB_COUNT 29
 int mmad_tune_set(int knob, int value);
 int mmad_tune_get(int knob, int* value);
 /* The split-K factor the dispatcher picks for a padded GEMM shape (Mp x Np
@@ -376,16 +378,40 @@ int mmad_comm_create(mmad_comm** out, const void* unique_id, int nranks, int ran
  * "all-reduce" scales the bucket by `scale` (= the sum over `scale` identical
  * shards) after a short delay */
 int mmad_comm_create_loopback(mmad_comm** out, float scale);
+/* ... posing as rank `rank` of `nranks` (tests of the sharded step's shard
+ * arithmetic on one GPU: its reduce-scatter scales the whole bucket, its
+ * all-gather leaves the other ranks' shards untouched) */
+int mmad_comm_create_loopback_ranks(mmad_comm** out, float scale, int nranks, int rank);
 void mmad_comm_destroy(mmad_comm* c);
 /* in-place fp32 sum all-reduce of buf[n] on stream */
 int mmad_allreduce_bucket(mmad_comm* c, float* buf, int64_t n, void* stream);
+/* this communicator's rank / number of ranks (a loopback communicator: 0 / 1) */
+int mmad_comm_rank(const mmad_comm* c);
+int mmad_comm_size(const mmad_comm* c);
+/* sharded exchange, in place (n divisible by the rank count): sum
+ * reduce-scatter of fp32 buf[n] leaving rank r's sum in buf[r*n/N, (r+1)*n/N);
+ * all-gather of every rank's shard of buf[n] (dtype MMAD_F32 or MMAD_BF16).
+ * Loopback: the reduce-scatter is its all-reduce, the all-gather a no-op. */
+int mmad_reduce_scatter_bucket(mmad_comm* c, float* buf, int64_t n, void* stream);
+int mmad_all_gather_bucket(mmad_comm* c, void* buf, int64_t n, int dtype, void* stream);
 /* Attach (c != NULL) or detach a communicator.  With one attached,
  * mmad_ae_train_step runs the data-parallel step: each layer's dW lands in the
  * grads buffer, is all-reduced on the executor's comm stream as soon as it is
  * complete (overlapping the rest of the backward), then Adam-updated there;
  * bias/gamma/beta grads and the loss follow in one final bucket.  BatchNorm
- * statistics stay per shard (DDP semantics). */
+ * statistics stay per shard (DDP semantics).
+ * Sharded weight buckets (knob 28, default on; a bucket whose size the rank
+ * count does not divide falls back to the all-reduce): reduce-scatter of the
+ * fp32 gradient, Adam on this rank's 1/N of the bucket (p, m, v), then an
+ * all-gather of the updated bf16 weight shadow (bf16 model: 4 + 2 bytes per
+ * parameter on the wire instead of 8, the Adam state stream divided by N) or
+ * of the fp32 weights (fp32 model).  The bf16 model's fp32 master weights and
+ * every model's Adam moments are then current only on their owning rank:
+ * mmad_ae_dp_sync_master (collective: every rank, same point) all-gathers
+ * them; mmad_ae_dp_master_stale says whether one is due. */
 int mmad_ae_set_comm(mmad_ae* h, mmad_comm* c);
+int mmad_ae_dp_sync_master(mmad_ae* h, void* stream);
+int mmad_ae_dp_master_stale(const mmad_ae* h);
 
 /* optimizer.step() (models/auto_encoder.py:75) on the bound buffers. */
 int mmad_ae_adam(mmad_ae* h, float lr, float beta1, float beta2, float eps, int step,

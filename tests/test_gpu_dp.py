@@ -248,3 +248,69 @@ def test_native_comm_self_test_passes_and_catches_a_broken_exchange():
     with pytest.raises(RuntimeError, match="self-test"):
         NativeComm.self_test(bad)
     lib.mmad_comm_destroy(hb)
+
+
+@pytest.mark.parametrize("dtype,rank", [("bf16", 0), ("bf16", 1), ("f32", 1)])
+def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank):
+    """The sharded DP step (knob dp_shard: reduce-scatter, Adam on this rank's
+    1/N of each weight bucket, all-gather of the updated weights) on one GPU,
+    through a loopback communicator posing as rank `rank` of 2 (its
+    reduce-scatter doubles the whole bucket = 2 identical shards, its
+    all-gather leaves the other rank's shard alone).  This rank's shard of
+    every weight bucket -- p, m, v and the bf16 shadow -- equals "grads x 2,
+    then Adam" bit for bit; the other shard keeps its pre-step p / m / v;
+    the small bucket is all-reduced and fully updated; the handle reports
+    stale master weights and refuses to detach until synced."""
+    import ctypes
+    import types as _t
+    from icra2021_multimodal_ad_amd import _native
+    from icra2021_multimodal_ad_amd.data import synth_windows
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    from icra2021_multimodal_ad_amd.common_utils import init_state_dict
+    lib = _native.load()
+    h = ctypes.c_void_p()
+    assert lib.mmad_comm_create_loopback_ranks(ctypes.byref(h), 2.0, 2, rank) == 0
+    comm = _t.SimpleNamespace(handle=h)
+
+    def mk():
+        cfg = _t.SimpleNamespace(input_size=700, btl_size=40, n_layers=5, gpu_id=0, dtype=dtype)
+        m = get_model(cfg)
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in
+                           init_state_dict(700, 40, 5, seed=83).items()})
+        m._native.sync_shadow(force=True)
+        return m
+    try:
+        ma, mb = mk(), mk()
+        a, b = ma._native, mb._native
+        a.set_comm(comm)
+        x = torch.from_numpy(synth_windows(384, 700, seed=95)).cuda()
+        p0, m0, v0 = a.params.clone(), a.exp_avg.clone(), a.exp_avg_sq.clone()
+        la = float(a.train_step_fused(x))
+        lb = b.train_step(x)
+        b.grads.mul_(2.0)
+        b.adam()
+        torch.cuda.synchronize()
+        assert abs(la - 2.0 * float(lb)) <= 1e-5 * abs(la)
+        assert lib.mmad_ae_dp_master_stale(a._h) == 1
+        for L in a.layers:
+            n = L["Np"] * L["Kp"]
+            lo = L["w_off"] + rank * (n // 2)
+            own = slice(lo, lo + n // 2)
+            other = slice(L["w_off"] + (1 - rank) * (n // 2), L["w_off"] + (2 - rank) * (n // 2))
+            for name, ref0 in (("params", p0), ("exp_avg", m0), ("exp_avg_sq", v0)):
+                got, want = getattr(a, name), getattr(b, name)
+                assert torch.equal(got[own], want[own]), (name, L["w_off"])
+                assert torch.equal(got[other], ref0[other]), (name, "other shard changed")
+            if dtype == "bf16":
+                assert torch.equal(a.shadow[own], b.shadow[own])
+        nw = a.n_weight
+        for name in ("params", "exp_avg", "exp_avg_sq"):      # the small bucket: all-reduced
+            assert torch.equal(getattr(a, name)[nw:], getattr(b, name)[nw:]), name
+        assert lib.mmad_ae_set_comm(a._h, None) != 0          # stale: detach refused
+        with pytest.raises(RuntimeError, match="sharded"):
+            ma.state_dict()
+        a.sync_master()                                        # loopback all-gather: a no-op
+        assert not a.master_stale
+        a.set_comm(None)
+    finally:
+        lib.mmad_comm_destroy(h)
