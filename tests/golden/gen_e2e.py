@@ -83,14 +83,20 @@ def ema_update(v, x, alpha=0.98):
     return x if v is None else v * alpha + (1 - alpha) * x
 
 
-def score_reference(model, dset, cfg, train_loader, valid_loader, test_loader, nap=True):
+def score_reference(model, dset, cfg, train_loader, valid_loader, test_loader, nap=True, keep_rng=False):
     """The reference's own scoring of its current model (eval mode, no state
     change): get_diffs + utils.metric BASE / SAP / NAP."""
     from reconstruction_aggregation import get_diffs
     from utils import metric
     model.eval()
+    # reading the train split in sampler order draws a permutation from the
+    # train sampler: keep its generator where the training loop left it, so
+    # per-epoch scoring does not change the next epoch's batch order
+    rng_state = train_loader.sampler.rng.bit_generator.state if keep_rng else None
     with torch.no_grad():
         tr_x, _ = dset.get_transformed_data(train_loader)
+        if keep_rng:
+            train_loader.sampler.rng.bit_generator.state = rng_state
         va_x, _ = dset.get_transformed_data(valid_loader)
         te_x, te_y = dset.get_transformed_data(test_loader)
         te_y = np.where(np.isin(np.asarray(te_y), [cfg.target_class]), True, False)
@@ -143,7 +149,7 @@ def run_reference(seed, per_epoch_nap=True):
         # whose best-on-valid selection lands on a near-tie epoch is compared
         # with the reference at that epoch (tests/test_gpu_e2e.py)
         r, _, _ = score_reference(model, dset, cfg, train_loader, valid_loader, test_loader,
-                                  nap=per_epoch_nap)
+                                  nap=per_epoch_nap, keep_rng=True)
         for m in r:
             epoch_auroc.setdefault(m, []).append(float(r[m][1]))
     model.load_state_dict(best)

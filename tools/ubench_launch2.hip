@@ -7,6 +7,7 @@
 // Build: hipcc -O2 --offload-arch=gfx950 tools/ubench_launch2.hip -o tools/ubench_launch2
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <chrono>
 #include <functional>
 
 __global__ __launch_bounds__(256) void k_empty(float* out) { if (out && threadIdx.x == 4096) out[0] = 1.f; }
@@ -64,6 +65,44 @@ static float graph_us(const std::function<void()>& f, hipStream_t s) {
   return ms * 1000.f / 1000.f;
 }
 
+// the host cost of one hipGraphLaunch: a single-stream chain of 40 kernels vs
+// the same 40 kernels captured across two streams (a fork / join event pair
+// around every second kernel, like the train step's side-stream dW GEMMs)
+static void graph_host(hipStream_t s, hipStream_t s2, float* b) {
+  hipEvent_t ev[64];
+  for (auto& e : ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  for (int forked = 0; forked < 2; ++forked) {
+    hipGraph_t g; hipGraphExec_t ge;
+    (void)hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+    int k = 0;
+    for (int i = 0; i < 40; ++i) {
+      if (forked && i % 2 == 1) {
+        (void)hipEventRecord(ev[k], s);
+        (void)hipStreamWaitEvent(s2, ev[k++], 0);
+        k_empty<<<256, 256, 0, s2>>>(b);
+        (void)hipEventRecord(ev[k], s2);
+        (void)hipStreamWaitEvent(s, ev[k++], 0);
+      } else {
+        k_empty<<<256, 256, 0, s>>>(b);
+      }
+    }
+    (void)hipStreamEndCapture(s, &g);
+    (void)hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    for (int r = 0; r < 5; ++r) (void)hipGraphLaunch(ge, s);
+    (void)hipStreamSynchronize(s);
+    auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < 50; ++r) (void)hipGraphLaunch(ge, s);
+    auto t1 = std::chrono::steady_clock::now();
+    (void)hipStreamSynchronize(s);
+    auto t2 = std::chrono::steady_clock::now();
+    printf("graph of 40 kernels, %s: host %.1f us per hipGraphLaunch, wall %.1f us per replay\n",
+           forked ? "20 on a 2nd stream (fork/join events)" : "one stream",
+           std::chrono::duration<double, std::micro>(t1 - t0).count() / 50,
+           std::chrono::duration<double, std::micro>(t2 - t0).count() / 50);
+    (void)hipGraphExecDestroy(ge); (void)hipGraphDestroy(g);
+  }
+}
+
 int main() {
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -87,6 +126,9 @@ int main() {
       printf("grid %4d %-18s eager %6.2f us/launch  graph %6.2f us/launch\n", grid, v.name, eager_us(v.f, s),
              graph_us(v.f, s));
   }
+  hipStream_t s2;
+  CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+  graph_host(s, s2, b);
   CK(hipStreamSynchronize(s));
   return 0;
 }
