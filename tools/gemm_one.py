@@ -1,5 +1,5 @@
 """Run one GEMM shape repeatedly (for rocprofv3 PMC passes).
-Usage: python tools/gemm_one.py [kind=fwd|bwd_data|bwd_w] [layer=0] [batch=1024] [iters=20] [tile=-1] [gm=-1]"""
+Usage: python tools/gemm_one.py [kind=fwd|bwd_data|bwd_w] [layer=0] [batch=1024] [iters=20] [tile=-1] [gm=-1] [model=ae|vib_ae]"""
 import sys
 sys.path.insert(0, ".")
 import torch
@@ -12,7 +12,10 @@ B = int(sys.argv[3]) if len(sys.argv) > 3 else 1024
 iters = int(sys.argv[4]) if len(sys.argv) > 4 else 20
 tile = int(sys.argv[5]) if len(sys.argv) > 5 else -1
 gm = int(sys.argv[6]) if len(sys.argv) > 6 else -1
-widths = [2048, 1658, 1268, 879, 489, 100, 489, 879, 1268, 1658, 2048]
+model = sys.argv[7] if len(sys.argv) > 7 else "ae"
+from icra2021_multimodal_ad_amd.common_utils import ae_widths
+enc, dec = ae_widths(2048, 100, 5, enc_out=200 if model == "vib_ae" else None)   # VIB: mu | log-var
+widths = enc + dec[1:]
 K, N = widths[li], widths[li + 1]
 Kp, Np, Mp = pad(K), pad(N), pad(B)
 dev = torch.device("cuda", 0)
