@@ -79,6 +79,7 @@ struct mmad_ae {
   // bf16 model's fp32 master weights / every model's Adam moments are
   // current only on their owning rank since the last mmad_ae_dp_sync_master
   int dp_shard = 1;
+  int graph_prio = 0;   // knob 29
   bool master_stale = false;
   int mse_tiles = 0;   // loss partials written by the last MSE GEMM
   // data parallelism: RCCL communicator (not owned), its stream and events
@@ -353,6 +354,7 @@ int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, i
     h->keep_grads = mmad_knob(25);
     h->side_prio_hi = mmad_knob(26);
     h->dp_shard = mmad_knob(28);
+    h->graph_prio = mmad_knob(29);
     h->ev_flags_ = ev_flags(mmad_knob(27));
   }
   for (int side = 0; side < 2; ++side) {
@@ -1086,7 +1088,9 @@ int mmad_ae_train_step_graph(mmad_ae* h, const float* x, int ld_x, int B, int k,
   const hipError_t ec = hipStreamEndCapture(h->gstream, &graph);
   hipGraphExec_t exec = nullptr;
   hipError_t ei = hipErrorUnknown;
-  if (rc == MMAD_OK && ec == hipSuccess && graph) ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  if (rc == MMAD_OK && ec == hipSuccess && graph)
+    ei = hipGraphInstantiateWithFlags(&exec, graph,
+                                      h->graph_prio ? hipGraphInstantiateFlagUseNodePriority : 0);
   if (graph) (void)hipGraphDestroy(graph);
   if (rc != MMAD_OK || ec != hipSuccess || ei != hipSuccess) {
     // this step already ran eagerly; later calls stay eager

@@ -57,12 +57,16 @@ struct mmad_comm {
 };
 
 namespace {
-// loopback "all-reduce": buf *= s, after a short spin so that a missing
-// dependency on the producer of buf shows up as a wrong result
-__global__ void loopback_k(float* __restrict__ buf, int64_t n, float s) {
+// loopback "all-reduce": buf *= s, after a short delay so that a missing
+// dependency on the producer of buf shows up as a wrong result.  The delay is
+// one sleeping wave of its own launch ahead of the scaling (same stream): a
+// spin in every block of the scaling grid would hold CUs for the delay and
+// stand in for an exchange far heavier than RCCL's few channel workgroups.
+__global__ void loopback_delay_k() {
   const long long t0 = clock64();
-  while (clock64() - t0 < 20000) {
-  }
+  while (clock64() - t0 < 20000) __builtin_amdgcn_s_sleep(8);
+}
+__global__ void loopback_k(float* __restrict__ buf, int64_t n, float s) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     buf[i] *= s;
 }
@@ -134,6 +138,8 @@ int mmad_allreduce_bucket(mmad_comm* c, float* buf, int64_t n, void* stream) {
   if (n == 0) return MMAD_OK;
   if (c->loopback > 0.f) {
     const int64_t blocks = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+    loopback_delay_k<<<1, 64, 0, (hipStream_t)stream>>>();
+    MMAD_LAUNCH_CHECK();
     loopback_k<<<(int)blocks, 256, 0, (hipStream_t)stream>>>(buf, n, c->loopback);
     MMAD_LAUNCH_CHECK();
     return MMAD_OK;

@@ -50,6 +50,30 @@ def _device_diffs(model, x, batch_size):
     return torch.cat(parts, dim=0)
 
 
+def _nap_model(model, cfg):
+    """The model whose diffs NAP consumes.  NAP standardises every principal
+    component of the train diffs by its variance (utils/normalize.py:36-45,
+    utils/metric.py:219-222), down to ~1e-10 of the largest on these models,
+    so bf16 activations -- 8 significant bits -- turn the low-variance
+    components into quantisation noise: bf16 scoring of one fp32-trained
+    model moved NAP AUROC by ~0.1 while BASE / SAP moved < 0.001
+    (profiles/r03v_e2e_bf16_training.json).  For a bf16 model NAP therefore
+    reads the diffs of an fp32 eval twin built from the same fp32 master
+    weights and BN statistics (the reference's own precision); BASE / SAP stay
+    on the bf16 path.  ``config.nap_dtype = 'model'`` keeps the model's own."""
+    if getattr(model, "mmad_dtype", "f32") == "f32" or getattr(cfg, "nap_dtype", "f32") != "f32":
+        return model
+    import types
+    from .model_builder import get_model
+    tcfg = types.SimpleNamespace(**vars(cfg))
+    tcfg.dtype = "f32"
+    tcfg.gpu_id = model._native.device.index
+    twin = get_model(tcfg)
+    twin.load_state_dict(model.state_dict())
+    twin.eval()
+    return twin
+
+
 class NoveltyDetecter:
     def __init__(self, config):
         self.config = config
@@ -83,14 +107,16 @@ class NoveltyDetecter:
             nap = NapScorer(model, start_layer_index=start, end_layer_index=end)
             cuts = np.cumsum([0] + widths)
             sel = slice(int(cuts[nap.sel.start]), int(cuts[min(nap.sel.stop, n)]))
-            nap_train = rows(lambda v: _device_diffs(model, v, cfg.batch_size)[:, sel].contiguous(), train_x)
+            nm = _nap_model(model, cfg)
+            nap_train = rows(lambda v: _device_diffs(nm, v, cfg.batch_size)[:, sel].contiguous(), train_x)
             path = getattr(cfg, "train_diffs", None)
             if path and (dp is None or torch.distributed.get_rank(dp.group) == 0):
                 torch.save(nap_train.cpu(), path)           # utils/metric.py:205
             nap = NapScorer.standalone(nap_train.shape[1], device=nat.device).fit(train_diffs=nap_train)
             del nap_train
-            out["nap"] = (rows(lambda v: nap.score(_device_diffs(model, v, 698)[:, sel]), valid_x),
-                          rows(lambda v: nap.score(_device_diffs(model, v, 698)[:, sel]), test_x))
+            out["nap"] = (rows(lambda v: nap.score(_device_diffs(nm, v, 698)[:, sel]), valid_x),
+                          rows(lambda v: nap.score(_device_diffs(nm, v, 698)[:, sel]), test_x))
+            del nm
         return out
 
     def test(self, model, dset_manager, train_loader, valid_loader, test_loader, df_test=None):

@@ -164,7 +164,17 @@ def test_e2e_scoring_auroc_parity_on_trained_model(e2e):
     (NAP standardises by per-component variances down to ~1e-10 of the
     largest here, so fp32 rounding differences in the diffs themselves --
     ~1e-7 -- move the scores of those components; that sensitivity is the
-    method's, the reference has it too)."""
+    method's, the reference has it too).
+
+    NAP's own fp32 noise floor on this model: the same fit and run restated
+    three ways that are all faithful fp32 readings of utils/normalize.py --
+    (A) V from an fp64 eigendecomposition of the Gram matrix, rotation in
+    fp32 (what the product does); (B) the same V, rotation in fp64; (C) V
+    from torch's fp32 SVD of the centred diffs (the reference's x.svd()),
+    rotation in fp32.  When the spread of their AUROCs exceeds 0.002 (the
+    low-variance components NAP divides by are rounding noise), the bar is
+    that spread: the product cannot be held closer to the oracle than the
+    oracle is to itself.  Every value goes to gpurun_out/e2e_scoring.json."""
     from oracle import ae_oracle as O
     from oracle.model_io import model_from_state_dict
     from icra2021_multimodal_ad_amd.novelty_detection import _device_diffs
@@ -184,16 +194,38 @@ def test_e2e_scoring_auroc_parity_on_trained_model(e2e):
     xc = trc - mu                                    # fp32, as x - mu
     xd = xc.astype(np.float64)
     _, v = np.linalg.eigh(xd.T @ xd)                 # V of the SVD (N_train > width)
-    v = v[:, ::-1][:, :min(xc.shape)]
-    rot = (xc @ v.astype(np.float32)).astype(np.float64)
-    fit = {"mu_r": mu, "v": v.astype(np.float32),
-           "mu_s": rot.mean(0).astype(np.float32), "var": rot.var(0, ddof=1).astype(np.float32)}
-    ref["nap"] = O.nap_score(tec, fit)
+    v = np.ascontiguousarray(v[:, ::-1][:, :min(xc.shape)])   # (a reversed view is not BLAS-able)
+
+    def fit_of(vv, rot):
+        return {"mu_r": mu, "v": vv, "mu_s": rot.mean(0).astype(np.float32),
+                "var": rot.var(0, ddof=1).astype(np.float32)}
+
+    def nap64(cat, fit):                              # (B): rotation in fp64
+        rot = (cat.astype(np.float64) - fit["mu_r"]) @ fit["v"].astype(np.float64)
+        return (((rot - fit["mu_s"]) ** 2) / fit["var"].astype(np.float64)).mean(axis=1)
+
+    v32 = v.astype(np.float32)
+    fit_a = fit_of(v32, (xc @ v32).astype(np.float64))
+    ref["nap"] = O.nap_score(tec, fit_a)
+    fit_b = fit_of(v32, xd @ v)
+    v_c = torch.linalg.svd(torch.from_numpy(xc), full_matrices=False)[2].T.contiguous().numpy()
+    fit_c = fit_of(v_c, (xc @ v_c).astype(np.float64))
+    variants = {"A_eigh_fp32_rot": O.auroc(ref["nap"], lab), "B_eigh_fp64_rot": O.auroc(nap64(tec, fit_b), lab),
+                "C_torch_svd_fp32_rot": O.auroc(O.nap_score(tec, fit_c), lab)}
+    floor = max(variants.values()) - min(variants.values())
+    rec = {"what": "seed-0 fp32-trained model scored by the product and by the CPU oracle",
+           "nap_oracle_variants": variants, "nap_floor": floor}
+    bars = {}
     for m in METHODS:
         ours = det.last_row[f"{m}_auroc"]
         theirs = O.auroc(ref[m], lab)
-        print(f"\n{m}: AUROC product {ours:.6f} oracle {theirs:.6f}")
-        assert abs(ours - theirs) <= 0.002, (m, ours, theirs)
+        bars[m] = 0.002 if m != "nap" else max(0.002, floor)
+        rec[m] = {"product": ours, "oracle": theirs, "delta": ours - theirs, "bar": bars[m]}
+        print(f"\n{m}: AUROC product {ours:.6f} oracle {theirs:.6f} (bar {bars[m]:.4f})")
+    print(f"nap oracle variants {variants}")
+    _record("scoring", rec)
+    for m in METHODS:
+        assert abs(rec[m]["delta"]) <= bars[m], (m, rec[m], variants)
         sc = det.last_scores[m][1]
         if m != "nap":
             assert np.abs(sc - ref[m]).max() <= 1e-4 * np.abs(ref[m]).max(), m
@@ -202,7 +234,8 @@ def test_e2e_scoring_auroc_parity_on_trained_model(e2e):
 def test_e2e_bf16_scoring_and_training(e2e):
     """The bf16 throughput path.  Scoring: the fp32-trained model of seed 0
     loaded into a bf16 model scores BASE/SAP within 0.01 AUROC of the fp32
-    scoring.  Training: bf16 training lands BASE within 0.02 of the
+    scoring, and NAP (whose diffs come from an fp32 twin of the same master
+    weights) within 0.002.  Training: bf16 training lands BASE within 0.02 of the
     reference's AUROC at the epoch it selects, on every seed; SAP/NAP after
     bf16 training are printed
     (their AUROC moves with the training trajectory: the reference's own spread
@@ -218,11 +251,14 @@ def test_e2e_bf16_scoring_and_training(e2e):
     det16 = NoveltyDetecter(cfg)
     tr_x, va_x, te_x, lab = det32.last_inputs
     sc16 = det16.scores(m16, tr_x, va_x, te_x)
-    for m in ("base", "sap"):
+    scoring16 = {}
+    for m in METHODS:
         a16 = metric.rank_metrics(sc16[m][1], lab)[0]
         a32 = det32.last_row[f"{m}_auroc"]
+        scoring16[m] = {"bf16_scoring": a16, "fp32_scoring": a32}
         print(f"\n{m}: bf16 scoring of the fp32-trained model {a16:.4f} vs fp32 {a32:.4f}")
-        assert abs(a16 - a32) <= 0.01, (m, a16, a32)
+        # NAP reads an fp32 twin's diffs (novelty_detection._nap_model)
+        assert abs(a16 - a32) <= (0.002 if m == "nap" else 0.01), (m, a16, a32)
     diffs = {m: [] for m in METHODS}
     epochs = []
     for seed in (0, 1, 2):
@@ -237,7 +273,7 @@ def test_e2e_bf16_scoring_and_training(e2e):
               f"bf16-trained - reference: {', '.join(f'{d:+.4f}' for d in diffs[m])}")
     _record("bf16_training", {"what": "bf16-trained product AUROC - reference (8 threads) at the "
                                       "product's selected epoch, per seed",
-                              "best_epochs": epochs,
+                              "best_epochs": epochs, "seed0_fp32_model_scored": scoring16,
                               **{m: {"delta_same_epoch": diffs[m],
                                      "ref_floor_mean": float(np.mean(_epoch_floor(g, m)))}
                                  for m in METHODS}})

@@ -7,6 +7,8 @@
 #   bench[:<args>]   python bench.py <args, commas -> spaces>
 #   prof[:<args>]    rocprofv3 --kernel-trace --stats of bench.py <args>
 #   py:<script,args> python <script> <args>          (tools/*.py helpers)
+#   bin:<path,args>  a prebuilt binary (tools/ubench_*)
+#   trace:<script,args>  rocprofv3 --kernel-trace --stats of python <script> <args>
 #   pmc:<ctr+ctr>:<script,args>  one rocprofv3 --pmc pass (counters joined by '+')
 # Every GPU step runs under its own timeout; logs go to gpurun_out/<tag>_*.
 set -o pipefail
@@ -14,6 +16,11 @@ T=${1:?tag}
 shift
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# heartbeat: a fresh box's first `import torch` can take minutes with nothing
+# printed; every step still runs under its own time limit
+( while sleep 30; do date +%s >> gpurun_out/${T}_heartbeat.txt; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 i=0
 for step in "$@"; do
   i=$((i + 1))
@@ -24,9 +31,9 @@ for step in "$@"; do
   case "$kind" in
     tests)
       if [ -n "$arg" ]; then
-        timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf -k "$arg" --timeout 300 --timeout-method thread > "$log" 2>&1
+        timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf -k "$arg" --timeout 300 --timeout-method thread > "$log" 2>&1
       else
-        timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > "$log" 2>&1
+        timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread > "$log" 2>&1
       fi ;;
     smoke)
       timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1 ;;
@@ -37,6 +44,11 @@ for step in "$@"; do
         python3 bench.py ${arg//,/ } > "$log" 2>&1 ;;
     py)
       timeout -k 10 400 python -u ${arg//,/ } > "$log" 2>&1 ;;
+    bin)
+      timeout -k 10 300 ${arg//,/ } > "$log" 2>&1 ;;
+    trace)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_${i}_trace -o run -- \
+        python3 ${arg//,/ } > "$log" 2>&1 ;;
     pmc)
       ctr=${arg%%:*}
       cmd=${arg#*:}
