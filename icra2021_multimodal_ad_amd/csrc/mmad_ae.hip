@@ -80,6 +80,13 @@ struct mmad_ae {
   // current only on their owning rank since the last mmad_ae_dp_sync_master
   int dp_shard = 1;
   int graph_prio = 0;   // knob 29
+  // data-parallel step: the weight buckets of the last dp_tail_layers layers
+  // of the backward (their exchange is what the step waits for at its end)
+  // go out in dp_chunks row chunks, each exchanged as soon as its piece of the
+  // dW GEMM is done (knob 30; 1 = one bucket per layer)
+  static constexpr int kMaxChunks = 8;
+  int dp_chunks = 1;
+  int dp_tail_layers = 2;
   bool master_stale = false;
   int mse_tiles = 0;   // loss partials written by the last MSE GEMM
   // data parallelism: RCCL communicator (not owned), its stream and events
@@ -355,6 +362,7 @@ int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, i
     h->side_prio_hi = mmad_knob(26);
     h->dp_shard = mmad_knob(28);
     h->graph_prio = mmad_knob(29);
+    h->dp_chunks = mmad_knob(30) < 1 ? 1 : (mmad_knob(30) > mmad_ae::kMaxChunks ? mmad_ae::kMaxChunks : mmad_knob(30));
     h->ev_flags_ = ev_flags(mmad_knob(27));
   }
   for (int side = 0; side < 2; ++side) {
@@ -530,6 +538,32 @@ static int prepare_ws(const mmad_ae* h, int B, int k, void* ws, int64_t ws_bytes
 enum { PROBE_FWD = 0, PROBE_DW = 64 };
 
 // GEMM dispatch with the split-K workspace of the stream it runs on
+// data-parallel weight buckets of layer l: row ranges [r0, r0 + rows) of
+// dW_l ([Np][Kp]), in row order.  One bucket, or (the last dp_tail_layers
+// layers of the backward, i.e. the lowest layer indices) dp_chunks chunks of
+// whole 128-row groups.  The step and mmad_ae_dp_sync_master use the same
+// partition: a sharded bucket's rank-r slice is [r * n / N, (r + 1) * n / N)
+// of the bucket's n = rows * Kp elements.
+static int dp_buckets(const mmad_ae* h, int l, int* r0, int* rows) {
+  const AeLayer& a = h->L[l];
+  const int groups = a.Np / 128;
+  int nch = l < h->dp_tail_layers ? h->dp_chunks : 1;
+  nch = nch < groups ? nch : (groups > 0 ? groups : 1);
+  if (nch <= 1) {
+    r0[0] = 0;
+    rows[0] = a.Np;
+    return 1;
+  }
+  const int per = (groups + nch - 1) / nch;    // 128-row groups per chunk
+  int n = 0;
+  for (int g0 = 0; g0 < groups; g0 += per) {
+    r0[n] = g0 * 128;
+    rows[n] = ((g0 + per < groups ? g0 + per : groups) - g0) * 128;
+    ++n;
+  }
+  return n;
+}
+
 static int ae_gemm(const mmad_ae* h, const AeWS& w, int dt, int epi, const void* A, int lda,
                    const void* B, int ldb, int Mp, int Np, int K, GemmEpi ep, hipStream_t s,
                    int* cfg = nullptr, int probe = -1) {
@@ -774,13 +808,30 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     const bool side_dw = adam && !dp && !ping && l >= w.dw_main;
     const bool rec = dp || (side_dw && (h->ev_every <= 1 || l == w.dw_main ||
                                         (l - w.dw_main) % h->ev_every == 0));
+    int br0[mmad_ae::kMaxChunks], brows[mmad_ae::kMaxChunks];
+    const int nb = dp ? dp_buckets(h, l, br0, brows) : 1;
     if (!adam || dp) {
       // fork: dz_l is complete on the main stream; dW_l overlaps the chain below
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
       MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
-      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
-                     nullptr, PROBE_DW + l));
-      if (dp) MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l], side));
+      if (nb == 1) {
+        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
+                       nullptr, PROBE_DW + l));
+        if (dp) MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l * mmad_ae::kMaxChunks], side));
+      } else {
+        // row chunks of dW_l = dz[:, r0:r0+rows]^T a, each bucket's exchange
+        // starting as soon as its rows are written
+        const size_t es = dt == MMAD_BF16 ? 2 : 4;
+        for (int b = 0; b < nb; ++b) {
+          GemmEpi ec = dwe;
+          ec.M = brows[b];
+          ec.out = h->grads + a.w_off + (int64_t)br0[b] * a.Kp;
+          if (ec.gb_src) ec.gb_src += br0[b];
+          RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, (const char*)dz + br0[b] * es, a.Np, in, a.Kp,
+                         brows[b], a.Kp, Mp, ec, side, nullptr, b == 0 ? PROBE_DW + l : -1));
+          MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l * mmad_ae::kMaxChunks + b], side));
+        }
+      }
     }
     if (l > 0) {
       const AeLayer& p = h->L[l - 1];
@@ -855,29 +906,33 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       // for the main stream's bwd-data of layer l)
       if (l == 0 || !(h->L[l - 1].bn) || (h->vib && l == h->n_enc))
         MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
-      MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_dw[l], 0));
       MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_data[l], 0));
-      const int64_t n = (int64_t)a.Np * a.Kp;
       const int nr = mmad_comm_size(h->comm) > 0 ? mmad_comm_size(h->comm) : 1;
-      if (h->dp_shard && n % nr == 0 && (n / nr) % 4 == 0) {
-        // ZeRO-1 form: reduce-scatter, Adam on this rank's shard, all-gather
-        // of the updated weights the next step reads (bf16 shadow / fp32 p)
-        const int64_t cnt = n / nr, off = a.w_off + (int64_t)mmad_comm_rank(h->comm) * cnt;
-        RET_IF(mmad_reduce_scatter_bucket(h->comm, h->grads + a.w_off, n, h->cstream));
-        void* sh = h->dtype == MMAD_BF16 ? (void*)((char*)h->shadow + off * 2) : nullptr;
-        RET_IF(mmad_adam(cnt, h->params + off, h->grads + off, h->m + off, h->v + off, adam->b1,
-                         adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt, sh,
-                         h->dtype == MMAD_BF16 ? cnt : 0, h->cstream));
-        if (h->dtype == MMAD_BF16)
-          RET_IF(mmad_all_gather_bucket(h->comm, (char*)h->shadow + a.w_off * 2, n, MMAD_BF16, h->cstream));
-        else
-          RET_IF(mmad_all_gather_bucket(h->comm, h->params + a.w_off, n, MMAD_F32, h->cstream));
-        if (nr > 1) h->master_stale = true;
-      } else {
-        RET_IF(mmad_allreduce_bucket(h->comm, h->grads + a.w_off, n, h->cstream));
-        RET_IF(mmad_adam(n, h->params + a.w_off, h->grads + a.w_off, h->m + a.w_off, h->v + a.w_off,
-                         adam->b1, adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt,
-                         adam_shadow(h, a, w.ping), h->dtype == MMAD_BF16 ? n : 0, h->cstream));
+      for (int b = 0; b < nb; ++b) {
+        MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_dw[l * mmad_ae::kMaxChunks + b], 0));
+        const int64_t n = (int64_t)brows[b] * a.Kp, boff = a.w_off + (int64_t)br0[b] * a.Kp;
+        if (h->dp_shard && n % nr == 0 && (n / nr) % 4 == 0) {
+          // ZeRO-1 form: reduce-scatter, Adam on this rank's shard, all-gather
+          // of the updated weights the next step reads (bf16 shadow / fp32 p)
+          const int64_t cnt = n / nr, off = boff + (int64_t)mmad_comm_rank(h->comm) * cnt;
+          RET_IF(mmad_reduce_scatter_bucket(h->comm, h->grads + boff, n, h->cstream));
+          void* sh = h->dtype == MMAD_BF16 ? (void*)((char*)h->shadow + off * 2) : nullptr;
+          RET_IF(mmad_adam(cnt, h->params + off, h->grads + off, h->m + off, h->v + off, adam->b1,
+                           adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt, sh,
+                           h->dtype == MMAD_BF16 ? cnt : 0, h->cstream));
+          if (h->dtype == MMAD_BF16)
+            RET_IF(mmad_all_gather_bucket(h->comm, (char*)h->shadow + boff * 2, n, MMAD_BF16, h->cstream));
+          else
+            RET_IF(mmad_all_gather_bucket(h->comm, h->params + boff, n, MMAD_F32, h->cstream));
+          if (nr > 1) h->master_stale = true;
+        } else {
+          RET_IF(mmad_allreduce_bucket(h->comm, h->grads + boff, n, h->cstream));
+          void* sh = adam_shadow(h, a, w.ping);
+          if (sh) sh = (char*)sh + (int64_t)br0[b] * a.Kp * 2;
+          RET_IF(mmad_adam(n, h->params + boff, h->grads + boff, h->m + boff, h->v + boff,
+                           adam->b1, adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt,
+                           sh, h->dtype == MMAD_BF16 ? n : 0, h->cstream));
+        }
       }
     } else if (adam) {
       // dW_l with this layer's Adam update fused into its epilogue.  It rewrites
@@ -1120,7 +1175,7 @@ int mmad_ae_set_comm(mmad_ae* h, mmad_comm* c) {
     int least = 0, greatest = 0;
     MMAD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     MMAD_HIP_CHECK(hipStreamCreateWithPriority(&h->cstream, hipStreamNonBlocking, greatest));
-    h->ev_dw.resize(h->L.size());
+    h->ev_dw.resize(h->L.size() * mmad_ae::kMaxChunks);
     for (auto& e : h->ev_dw) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, h->ev_flags_));
     MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_small, h->ev_flags_));
     MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_cdone, h->ev_flags_));
@@ -1136,12 +1191,17 @@ int mmad_ae_dp_sync_master(mmad_ae* h, void* stream) {
   if (!h->comm || !h->master_stale) return MMAD_OK;
   hipStream_t st = (hipStream_t)stream;
   const int nr = mmad_comm_size(h->comm);
-  for (const AeLayer& a : h->L) {
-    const int64_t n = (int64_t)a.Np * a.Kp;
-    if (!(n % nr == 0 && (n / nr) % 4 == 0)) continue;   // an all-reduced bucket: already current
-    if (h->dtype == MMAD_BF16) RET_IF(mmad_all_gather_bucket(h->comm, h->params + a.w_off, n, MMAD_F32, st));
-    RET_IF(mmad_all_gather_bucket(h->comm, h->m + a.w_off, n, MMAD_F32, st));
-    RET_IF(mmad_all_gather_bucket(h->comm, h->v + a.w_off, n, MMAD_F32, st));
+  for (int l = 0; l < (int)h->L.size(); ++l) {
+    const AeLayer& a = h->L[l];
+    int br0[mmad_ae::kMaxChunks], brows[mmad_ae::kMaxChunks];
+    const int nb = dp_buckets(h, l, br0, brows);
+    for (int b = 0; b < nb; ++b) {
+      const int64_t n = (int64_t)brows[b] * a.Kp, boff = a.w_off + (int64_t)br0[b] * a.Kp;
+      if (!(n % nr == 0 && (n / nr) % 4 == 0)) continue;   // an all-reduced bucket: already current
+      if (h->dtype == MMAD_BF16) RET_IF(mmad_all_gather_bucket(h->comm, h->params + boff, n, MMAD_F32, st));
+      RET_IF(mmad_all_gather_bucket(h->comm, h->m + boff, n, MMAD_F32, st));
+      RET_IF(mmad_all_gather_bucket(h->comm, h->v + boff, n, MMAD_F32, st));
+    }
   }
   h->master_stale = false;
   return MMAD_OK;

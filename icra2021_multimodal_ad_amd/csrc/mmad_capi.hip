@@ -32,7 +32,7 @@ int mmad_pad_granule(void) { return MMAD_PAD; }
 // Tuning knobs: ONE table, set only through mmad_tune_set (the library reads
 // no environment variables, so every rank of a job runs the same schedule
 // unless its code says otherwise).  GEMM knobs (0-11) are read per dispatch;
-// the executor's schedule knobs (16-29) are copied into a handle when it is
+// the executor's schedule knobs (16-30) are copied into a handle when it is
 // created (mmad_ae_create), so a handle keeps one schedule for its lifetime.
 namespace {
 int g_knob[MMAD_KNOB_COUNT] = {
@@ -63,6 +63,7 @@ int g_knob[MMAD_KNOB_COUNT] = {
     0,     // 27 executor events with the system-scope fence
     1,     // 28 DP: sharded weight buckets (reduce-scatter, Adam on 1/N, all-gather)
     0,     // 29 captured train-step graph instantiated with per-node (captured stream) priorities
+    1,     // 30 DP: row chunks per weight bucket of the last two layers of the backward
 };
 }  // namespace
 int mmad_knob(int k) { return g_knob[k]; }

@@ -45,7 +45,7 @@ int mmad_abi_version(void);
 int mmad_pad_granule(void);
 /* Tuning knobs (no reference counterpart).  One process-wide table, set only
  * through mmad_tune_set (the library reads no environment variables).  GEMM
- * knobs are read per dispatch; the executor's schedule knobs (16-29) are
+ * knobs are read per dispatch; the executor's schedule knobs (16-30) are
  * copied into a handle by mmad_ae_create, so set them before creating it.
  *   0  GEMM tile override (-1 autotuned; 0 = 128x128/512 thr, 1 = 256x128,
  *      2 = 128x256, 3 = 64x64/256 thr, 4 = 64x128, 5 = 128x128/256 thr,
@@ -79,8 +79,10 @@ int mmad_pad_granule(void);
  *   28 data parallel: sharded weight buckets (reduce-scatter, Adam on 1/N,
  *      all-gather; 1) or all-reduce + full Adam (0)
  *   29 the captured train-step graph keeps each node's stream priority
- *      (hipGraphInstantiateFlagUseNodePriority; 0) */
-#define MMAD_KNOB_COUNT 30
+ *      (hipGraphInstantiateFlagUseNodePriority; 0)
+ *   30 data parallel: row chunks (1-8) of the weight buckets of the last two
+ *      layers of the backward, each exchanged as its dW rows complete (1) */
+#define MMAD_KNOB_COUNT 31
 int mmad_tune_set(int knob, int value);
 int mmad_tune_get(int knob, int* value);
 /* The split-K factor the dispatcher picks for a padded GEMM shape (Mp x Np

@@ -117,13 +117,15 @@ def test_native_comm_single_rank_step_matches_fused():
         lib.mmad_comm_destroy(h)
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_native_exchange_schedule_loopback(dtype):
+@pytest.mark.parametrize("dtype,chunks", [("f32", 1), ("bf16", 1), ("bf16", 3), ("f32", 4)])
+def test_native_exchange_schedule_loopback(dtype, chunks):
     """Exchange schedule of the native DP step on one GPU: a loopback
     communicator whose all-reduce doubles each bucket (= 2 identical shards)
     after a delay.  Must equal: plain fwd+bwd, grads *= 2, loss *= 2, flat Adam
     -- i.e. every bucket is reduced after its producer finished and before its
-    Adam, and the small bucket + loss are reduced too."""
+    Adam, and the small bucket + loss are reduced too.  chunks > 1 (knob
+    dp_chunks): the last two layers' buckets go out as row chunks of their dW
+    GEMMs, each exchanged once its rows are written."""
     import ctypes
     import types as _t
     from icra2021_multimodal_ad_amd import _native
@@ -142,7 +144,9 @@ def test_native_exchange_schedule_loopback(dtype):
                            init_state_dict(700, 40, 5, seed=81).items()})
         return m
     try:
-        ma, mb = mk(), mk()
+        with _native.tune(dp_chunks=chunks):
+            ma = mk()
+        mb = mk()
         ma._native.set_comm(comm)
         for s in range(3):
             x = torch.from_numpy(synth_windows(384, 700, seed=90 + s)).cuda()
@@ -250,8 +254,20 @@ def test_native_comm_self_test_passes_and_catches_a_broken_exchange():
     lib.mmad_comm_destroy(hb)
 
 
-@pytest.mark.parametrize("dtype,rank", [("bf16", 0), ("bf16", 1), ("f32", 1)])
-def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank):
+def _dp_buckets(L, l, chunks):
+    """Row ranges of layer l's weight buckets (mirror of mmad_ae.hip dp_buckets:
+    the two lowest layers in `chunks` chunks of whole 128-row groups)."""
+    groups = L["Np"] // 128
+    nch = min(chunks if l < 2 else 1, max(groups, 1))
+    if nch <= 1:
+        return [(0, L["Np"])]
+    per = -(-groups // nch)
+    return [(g0 * 128, (min(g0 + per, groups) - g0) * 128) for g0 in range(0, groups, per)]
+
+
+@pytest.mark.parametrize("dtype,rank,chunks", [("bf16", 0, 1), ("bf16", 1, 1), ("f32", 1, 1),
+                                               ("bf16", 1, 4), ("f32", 0, 3)])
+def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank, chunks):
     """The sharded DP step (knob dp_shard: reduce-scatter, Adam on this rank's
     1/N of each weight bucket, all-gather of the updated weights) on one GPU,
     through a loopback communicator posing as rank `rank` of 2 (its
@@ -260,7 +276,9 @@ def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank):
     every weight bucket -- p, m, v and the bf16 shadow -- equals "grads x 2,
     then Adam" bit for bit; the other shard keeps its pre-step p / m / v;
     the small bucket is all-reduced and fully updated; the handle reports
-    stale master weights and refuses to detach until synced."""
+    stale master weights and refuses to detach until synced.  With chunks > 1
+    every row chunk of the last two layers is its own bucket with its own
+    shards."""
     import ctypes
     import types as _t
     from icra2021_multimodal_ad_amd import _native
@@ -280,7 +298,9 @@ def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank):
         m._native.sync_shadow(force=True)
         return m
     try:
-        ma, mb = mk(), mk()
+        with _native.tune(dp_chunks=chunks):
+            ma = mk()
+        mb = mk()
         a, b = ma._native, mb._native
         a.set_comm(comm)
         x = torch.from_numpy(synth_windows(384, 700, seed=95)).cuda()
@@ -292,17 +312,22 @@ def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank):
         torch.cuda.synchronize()
         assert abs(la - 2.0 * float(lb)) <= 1e-5 * abs(la)
         assert lib.mmad_ae_dp_master_stale(a._h) == 1
-        for L in a.layers:
-            n = L["Np"] * L["Kp"]
-            lo = L["w_off"] + rank * (n // 2)
-            own = slice(lo, lo + n // 2)
-            other = slice(L["w_off"] + (1 - rank) * (n // 2), L["w_off"] + (2 - rank) * (n // 2))
-            for name, ref0 in (("params", p0), ("exp_avg", m0), ("exp_avg_sq", v0)):
-                got, want = getattr(a, name), getattr(b, name)
-                assert torch.equal(got[own], want[own]), (name, L["w_off"])
-                assert torch.equal(got[other], ref0[other]), (name, "other shard changed")
-            if dtype == "bf16":
-                assert torch.equal(a.shadow[own], b.shadow[own])
+        nb = 0
+        for li, L in enumerate(a.layers):
+            for r0, rows in _dp_buckets(L, li, chunks):
+                nb += 1
+                n = rows * L["Kp"]
+                boff = L["w_off"] + r0 * L["Kp"]
+                lo = boff + rank * (n // 2)
+                own = slice(lo, lo + n // 2)
+                other = slice(boff + (1 - rank) * (n // 2), boff + (2 - rank) * (n // 2))
+                for name, ref0 in (("params", p0), ("exp_avg", m0), ("exp_avg_sq", v0)):
+                    got, want = getattr(a, name), getattr(b, name)
+                    assert torch.equal(got[own], want[own]), (name, L["w_off"], r0)
+                    assert torch.equal(got[other], ref0[other]), (name, "other shard changed", r0)
+                if dtype == "bf16":
+                    assert torch.equal(a.shadow[own], b.shadow[own])
+        assert nb > len(a.layers) or chunks == 1
         nw = a.n_weight
         for name in ("params", "exp_avg", "exp_avg_sq"):      # the small bucket: all-reduced
             assert torch.equal(getattr(a, name)[nw:], getattr(b, name)[nw:]), name

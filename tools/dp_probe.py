@@ -1,6 +1,7 @@
 """One DP-schedule variant alone, for a rocprofv3 kernel trace: the fused
 step driven through a loopback communicator posing as rank r of n, with the
-tune knob dp_shard = s.  Usage: python tools/dp_probe.py n r s [steps=20] [batch=1024]"""
+tune knob dp_shard = s.  Usage: python tools/dp_probe.py n r s [steps=20] [batch=1024] [chunks=1]
+(chunks: knob dp_chunks, row chunks of the last two layers' buckets)"""
 import ctypes
 import sys
 import time
@@ -15,12 +16,13 @@ from icra2021_multimodal_ad_amd.data import synth_windows_device
 n, r, shard = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
 steps = int(sys.argv[4]) if len(sys.argv) > 4 else 20
 batch = int(sys.argv[5]) if len(sys.argv) > 5 else 1024
+chunks = int(sys.argv[6]) if len(sys.argv) > 6 else 1
 dev = torch.device("cuda", 0)
 lib = _native.load()
 h = ctypes.c_void_p()
 assert lib.mmad_comm_create_loopback_ranks(ctypes.byref(h), 1.0, n, r) == 0
 cfg = types.SimpleNamespace(input_size=2048, btl_size=100, n_layers=5, gpu_id=0, dtype="bf16")
-with _native.tune(dp_shard=shard):
+with _native.tune(dp_shard=shard, dp_chunks=chunks):
     m = get_model(cfg)
 m._native.sync_shadow(force=True)
 m._native.set_comm(types.SimpleNamespace(handle=h))
@@ -32,7 +34,7 @@ t0 = time.perf_counter()
 for i in range(steps):
     m._native.train_step_fused(pool[i % 8])
 torch.cuda.synchronize()
-print(f"n={n} r={r} shard={shard}: {(time.perf_counter() - t0) / steps * 1e3:.4f} ms/step", flush=True)
+print(f"n={n} r={r} shard={shard} chunks={chunks} batch={batch}: {(time.perf_counter() - t0) / steps * 1e3:.4f} ms/step", flush=True)
 m._native.sync_master()
 m._native.set_comm(None)
 lib.mmad_comm_destroy(h)

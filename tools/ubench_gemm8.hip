@@ -61,15 +61,17 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int rbase, int kk, int l
 }
 
 // DI = 1: the next tile's LDS-DMA spread over the MFMAs of the following
-// k-step instead of issued in one burst after the barrier.  NOMMA: no MFMA
-// (fragment reads and the DMA ring only: the operand-feed ceiling)
-template <int BM, int BN, int WM, int WN, int NBUF, int STAG, int DI = 0, int NOMMA = 0>
-__global__ __launch_bounds__(512, 1) void gemm8(const bf16* __restrict__ A, const bf16* __restrict__ B,
+// k-step instead of issued in one burst after the barrier.  NOMMA: 1 = no MFMA
+// (fragment reads and the DMA ring only: the operand-feed ceiling); 2 = no
+// MFMA and no fragment reads either (the DMA ring and its barriers alone).
+// NW: waves per workgroup (8, or 4 for 128x64 / 128x128 wave tiles).
+template <int BM, int BN, int WM, int WN, int NBUF, int STAG, int DI = 0, int NOMMA = 0, int NW = 8>
+__global__ __launch_bounds__(64 * NW, 1) void gemm8(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                 bf16* __restrict__ C, int M, int N, int K, int tiles_n,
                                                 int group_m, int store) {
-  constexpr int NT = 512;
+  constexpr int NT = 64 * NW;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
-  static_assert(WM * WN == 8, "8 waves");
+  static_assert(WM * WN == NW, "wave grid");
   constexpr int ABYTES = BM * 128, SLOT = (BM + BN) * 128;
   constexpr int NL = SLOT / 16 / NT;                       // DMA per thread per K-tile
   static_assert(NBUF * SLOT <= 163840, "LDS");
@@ -127,6 +129,7 @@ __global__ __launch_bounds__(512, 1) void gemm8(const bf16* __restrict__ A, cons
   };
   bf16x8 fa[2][TM], fb[2][TN];
   auto rd = [&](int t, int kk, int s) {
+    if constexpr (NOMMA >= 2) return;
     const char* base = smem + (t % NBUF) * SLOT;
 #pragma unroll
     for (int i = 0; i < TM; ++i) fa[s][i] = frag(base, ra + i * 16, kk, lane);
@@ -166,12 +169,14 @@ __global__ __launch_bounds__(512, 1) void gemm8(const bf16* __restrict__ A, cons
 #pragma unroll
       for (int j = 0; j < TN; ++j) mfma(0, i, j);
       pend_issue(i);
-      if (i == 0) {
-        const char* base = smem + (t % NBUF) * SLOT;
+      if constexpr (NOMMA < 2) {
+        if (i == 0) {
+          const char* base = smem + (t % NBUF) * SLOT;
 #pragma unroll
-        for (int j = 0; j < TN; ++j) fb[1][j] = frag(base + ABYTES, rb + j * 16, 1, lane);
+          for (int j = 0; j < TN; ++j) fb[1][j] = frag(base + ABYTES, rb + j * 16, 1, lane);
+        }
+        fa[1][i] = frag(smem + (t % NBUF) * SLOT, ra + i * 16, 1, lane);
       }
-      fa[1][i] = frag(smem + (t % NBUF) * SLOT, ra + i * 16, 1, lane);
     }
     __builtin_amdgcn_s_setprio(0);
   };
@@ -261,13 +266,13 @@ __global__ void ref_k(const bf16* A, const bf16* B, float* C, int M, int N, int 
   C[(size_t)m * N + n] = s;
 }
 
-template <int BM, int BN, int WM, int WN, int NBUF, int STAG, int DI = 0, int NOMMA = 0>
+template <int BM, int BN, int WM, int WN, int NBUF, int STAG, int DI = 0, int NOMMA = 0, int NW = 8>
 static float run(const bf16* A, const bf16* B, bf16* C, int M, int N, int K, int store, int iters) {
   const int tiles_m = M / BM, tiles_n = N / BN, ntiles = tiles_m * tiles_n;
   int gm = (int)(sqrt(ntiles / 8.0 * BN / BM) + 0.5);
   gm = gm < 1 ? 1 : (gm > tiles_m ? tiles_m : gm);
   auto launch = [&]() {
-    gemm8<BM, BN, WM, WN, NBUF, STAG, DI, NOMMA><<<ntiles, 512>>>(A, B, C, M, N, K, tiles_n, gm, store);
+    gemm8<BM, BN, WM, WN, NBUF, STAG, DI, NOMMA, NW><<<ntiles, 64 * NW>>>(A, B, C, M, N, K, tiles_n, gm, store);
   };
   for (int i = 0; i < 3; ++i) launch();
   CK(hipGetLastError());
@@ -344,22 +349,22 @@ int main(int argc, char** argv) {
     }
     mmad_tune_set(0, -1);
   }
-#define RUN(BM_, BN_, WM_, WN_, NB_, ST_, DI_)                                                    \
+#define RUN(BM_, BN_, WM_, WN_, NB_, ST_, DI_, NW_)                                               \
   if (M % BM_ == 0 && N % BN_ == 0) {                                                           \
     char nm[64];                                                                                \
     snprintf(nm, sizeof nm, "gemm8 %dx%d w%dx%d nb%d st%d di%d", BM_, BN_, WM_, WN_, NB_, ST_, DI_); \
-    report(nm, run<BM_, BN_, WM_, WN_, NB_, ST_, DI_>(A, B, C, M, N, K, 1, iters), true);       \
+    report(nm, run<BM_, BN_, WM_, WN_, NB_, ST_, DI_, 0, NW_>(A, B, C, M, N, K, 1, iters), true); \
     snprintf(nm, sizeof nm, "  (no store)");                                                    \
-    report(nm, run<BM_, BN_, WM_, WN_, NB_, ST_, DI_>(A, B, C, M, N, K, 0, iters), false);      \
+    report(nm, run<BM_, BN_, WM_, WN_, NB_, ST_, DI_, 0, NW_>(A, B, C, M, N, K, 0, iters), false); \
     snprintf(nm, sizeof nm, "  (no MFMA: feed ceiling)");                                       \
-    report(nm, run<BM_, BN_, WM_, WN_, NB_, ST_, DI_, 1>(A, B, C, M, N, K, 0, iters), false);   \
+    report(nm, run<BM_, BN_, WM_, WN_, NB_, ST_, DI_, 1, NW_>(A, B, C, M, N, K, 0, iters), false); \
+    snprintf(nm, sizeof nm, "  (no MFMA, no reads: DMA ring)");                                 \
+    report(nm, run<BM_, BN_, WM_, WN_, NB_, ST_, DI_, 2, NW_>(A, B, C, M, N, K, 0, iters), false); \
   }
-  RUN(256, 128, 4, 2, 3, 0, 0)
-  RUN(256, 128, 4, 2, 3, 0, 1)
-  RUN(256, 128, 4, 2, 2, 1, 0)
-  RUN(256, 128, 4, 2, 2, 1, 1)
-  RUN(256, 128, 4, 2, 3, 1, 1)
-  RUN(256, 256, 2, 4, 2, 0, 0)
-  RUN(256, 256, 2, 4, 2, 0, 1)
+  RUN(256, 128, 4, 2, 3, 0, 1, 8)
+  RUN(256, 128, 2, 2, 3, 0, 1, 4)
+  RUN(256, 128, 2, 2, 3, 0, 0, 4)
+  RUN(256, 256, 2, 4, 2, 0, 1, 8)
+  RUN(256, 256, 2, 2, 2, 0, 1, 4)
   return 0;
 }
