@@ -66,16 +66,10 @@ template <> struct Cfg<5> { static constexpr int BM = 128, BN = 128, WM = 2, WN 
 // 16384 x 2048 x 1664 vs 0.33 for 256x128); its epilogue staging fills LDS
 constexpr int CFG_BIG = 6;
 template <> struct Cfg<6> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NS = 2, NT = 512; };
-// 256x128 with 4 waves (2 x 2, wave tile 128x64), one wave per SIMD: 25 %
-// fewer LDS fragment bytes per MFMA than cfg 1's 64x64 wave tiles (the LDS
-// port, shared by the ring's DMA writes and the fragment reads, is what
-// bounds the 8-wave loops: tools/ubench_gemm8.hip, profiles/r03w_*), and
-// 512 registers per lane for the accumulators, fragments and epilogue state
-template <> struct Cfg<7> { static constexpr int BM = 256, BN = 128, WM = 2, WN = 2, NS = 3, NT = 256; };
-constexpr int NCFG = 8;
-constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256, 256};
-constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256, 128};
-constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512, 256};
+constexpr int NCFG = 7;
+constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256};
+constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256};
+constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512};
 // the 256x256 tile: bf16 operands, forward-type epilogues, no fused BN
 template <typename T, int EPI>
 constexpr bool big_ok() {
@@ -1348,7 +1342,6 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
 static bool cfg_fits(int cfg, int Mp, int Np, int epi, int dtype) {
   if (Mp % CFG_BM[cfg] || Np % CFG_BN[cfg]) return false;
   if (cfg == CFG_BIG && !big_ok_rt(dtype, epi)) return false;
-  if (cfg == 7 && dtype != MMAD_BF16) return false;   // fp32 operands spill at 128x64 per wave
   // the score epilogue reduces rows over 128-column groups inside one tile
   if (epi == GEMM_EPI_SCORE && CFG_BN[cfg] < 128) return false;
   return true;
@@ -1405,14 +1398,6 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
     case 3: mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
     case 4: mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
     case 5: mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
-    case 7:
-      if constexpr (sizeof(T) == 2) {
-        mmad_gemm_kernel<T, TO, AK, BK_, 7, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep);
-      } else {
-        mmad_set_error("gemm: tile configuration 7 is bf16 only");
-        return MMAD_EUNSUPPORTED;
-      }
-      break;
     default:
       if constexpr (big_ok<T, EPI>()) {
         mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep);
@@ -1436,9 +1421,6 @@ static const void* kernel_ptr(int cfg) {
     case 3: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI>;
     case 4: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI>;
     case 5: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI>;
-    case 7:
-      if constexpr (sizeof(T) == 2) return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 7, EPI>;
-      return nullptr;
     default:
       if constexpr (big_ok<T, EPI>()) return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI>;
       return nullptr;

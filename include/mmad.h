@@ -50,8 +50,7 @@ int mmad_pad_granule(void);
  *   0  GEMM tile override (-1 autotuned; 0 = 128x128/512 thr, 1 = 256x128,
  *      2 = 128x256, 3 = 64x64/256 thr, 4 = 64x128, 5 = 128x128/256 thr,
  *      6 = 256x256/512 thr (bf16 forward / MSE / score GEMMs without fused BN
- *      or split-K), 7 = 256x128/256 thr (4 waves of 128x64, bf16); a tile that does
- *      not fit a shape falls back to the tuned one)
+ *      or split-K); a tile that does not fit a shape falls back to the tuned one)
  *   1  XCD tile-group height override (-1 rule)
  *   2  per-shape autotune on first dispatch (1, default) or static heuristic (0)
  *   3  diagnostics bits (tools/gemm_phase; 4 = force the split-K combine's

@@ -330,7 +330,7 @@ int main(int argc, char** argv) {
     float* bias;
     CK(hipMalloc(&bias, N * 4));
     CK(hipMemset(bias, 0, N * 4));
-    for (int tile : {-1, 0, 1, 2, 6, 7}) {
+    for (int tile : {-1, 0, 1, 2, 6}) {
       mmad_tune_set(0, tile);
       auto f = [&]() { return mmad_fc_fwd(MMAD_BF16, M, N, K, M, N, K, A, B, bias, 0, 0.f, nullptr, nullptr, C, nullptr, 0); };
       for (int i = 0; i < 3; ++i)
