@@ -79,14 +79,10 @@ struct mmad_ae {
   // bf16 model's fp32 master weights / every model's Adam moments are
   // current only on their owning rank since the last mmad_ae_dp_sync_master
   int dp_shard = 1;
-  int graph_prio = 0;   // knob 29
-  // data-parallel step: the weight buckets of the last dp_tail_layers layers
-  // of the backward (their exchange is what the step waits for at its end)
-  // go out in dp_chunks row chunks, each exchanged as soon as its piece of the
-  // dW GEMM is done (knob 30; 1 = one bucket per layer)
-  static constexpr int kMaxChunks = 8;
-  int dp_chunks = 1;
-  int dp_tail_layers = 2;
+  // data-parallel step: consecutive layers' weight gradients (backward
+  // order) share one exchange bucket until it holds at least dp_bucket_mib
+  // MiB of fp32 gradient (knob 30; 0 = one bucket per layer)
+  int dp_bucket_mib = 8;
   bool master_stale = false;
   int mse_tiles = 0;   // loss partials written by the last MSE GEMM
   // data parallelism: RCCL communicator (not owned), its stream and events
@@ -361,8 +357,7 @@ int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, i
     h->keep_grads = mmad_knob(25);
     h->side_prio_hi = mmad_knob(26);
     h->dp_shard = mmad_knob(28);
-    h->graph_prio = mmad_knob(29);
-    h->dp_chunks = mmad_knob(30) < 1 ? 1 : (mmad_knob(30) > mmad_ae::kMaxChunks ? mmad_ae::kMaxChunks : mmad_knob(30));
+    h->dp_bucket_mib = mmad_knob(30) < 0 ? 0 : mmad_knob(30);
     h->ev_flags_ = ev_flags(mmad_knob(27));
   }
   for (int side = 0; side < 2; ++side) {
@@ -538,30 +533,34 @@ static int prepare_ws(const mmad_ae* h, int B, int k, void* ws, int64_t ws_bytes
 enum { PROBE_FWD = 0, PROBE_DW = 64 };
 
 // GEMM dispatch with the split-K workspace of the stream it runs on
-// data-parallel weight buckets of layer l: row ranges [r0, r0 + rows) of
-// dW_l ([Np][Kp]), in row order.  One bucket, or (the last dp_tail_layers
-// layers of the backward, i.e. the lowest layer indices) dp_chunks chunks of
-// whole 128-row groups.  The step and mmad_ae_dp_sync_master use the same
-// partition: a sharded bucket's rank-r slice is [r * n / N, (r + 1) * n / N)
-// of the bucket's n = rows * Kp elements.
-static int dp_buckets(const mmad_ae* h, int l, int* r0, int* rows) {
-  const AeLayer& a = h->L[l];
-  const int groups = a.Np / 128;
-  int nch = l < h->dp_tail_layers ? h->dp_chunks : 1;
-  nch = nch < groups ? nch : (groups > 0 ? groups : 1);
-  if (nch <= 1) {
-    r0[0] = 0;
-    rows[0] = a.Np;
-    return 1;
+// data-parallel weight buckets: walking the layers in backward order,
+// consecutive layers join one bucket until it holds >= dp_bucket_mib MiB of
+// fp32 gradient (layer 0 always closes the last).  The weights are one
+// contiguous buffer in layer order, so a bucket of layers l_lo..l_hi is the
+// range [w_off(l_lo), w_off(l_hi) + Np * Kp).  Fewer, larger buckets: fewer
+// exchange calls and events on the host (the DP step was host-bound with one
+// bucket per layer, profiles/r03z_*) and larger collectives.  The step and
+// mmad_ae_dp_sync_master use the same plan; a sharded bucket's rank-r slice is
+// [r * n / N, (r + 1) * n / N).  last_of[l] = the bucket whose lowest layer is
+// l (-1 if none).
+struct DpBucket {
+  int l_hi, l_lo;
+  int64_t off, n;
+};
+static void dp_plan(const mmad_ae* h, std::vector<DpBucket>& out) {
+  out.clear();
+  const int nL = (int)h->L.size();
+  const int64_t min_n = (int64_t)h->dp_bucket_mib * (1 << 20) / 4;
+  int hi = nL - 1;
+  int64_t acc = 0;
+  for (int l = nL - 1; l >= 0; --l) {
+    acc += (int64_t)h->L[l].Np * h->L[l].Kp;
+    if (acc >= min_n || l == 0) {
+      out.push_back(DpBucket{hi, l, h->L[l].w_off, acc});
+      hi = l - 1;
+      acc = 0;
+    }
   }
-  const int per = (groups + nch - 1) / nch;    // 128-row groups per chunk
-  int n = 0;
-  for (int g0 = 0; g0 < groups; g0 += per) {
-    r0[n] = g0 * 128;
-    rows[n] = ((g0 + per < groups ? g0 + per : groups) - g0) * 128;
-    ++n;
-  }
-  return n;
 }
 
 static int ae_gemm(const mmad_ae* h, const AeWS& w, int dt, int epi, const void* A, int lda,
@@ -743,6 +742,9 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
   const int nL = (int)h->L.size();
   hipStream_t side = h->side;
   std::vector<PendingDW> pending;   // side-stream dW GEMMs waiting for a recorded event
+  std::vector<DpBucket> plan;       // data parallel: the exchange buckets (dp_plan)
+  int next_bucket = 0;
+  if (adam && h->comm) dp_plan(h, plan);
   // layer l's Adam terms for a dW epilogue: the weight tile's (ad_*, unless
   // weights_too is false) and the small segment [bias | gamma | beta]'s
   auto fill_adam = [&](GemmEpi& e, int l, bool weights_too) {
@@ -796,6 +798,9 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       dwe.gb_stride = gs.stride;
     }
     const bool dp = adam && h->comm;
+    // the exchange bucket this layer closes (data parallel), if any
+    const DpBucket* bk = nullptr;
+    if (dp && next_bucket < (int)plan.size() && plan[next_bucket].l_lo == l) bk = &plan[next_bucket++];
     // ping-pong shadows (bf16): the fused Adam of dW_l writes the other
     // shadow, so dW_l may start as soon as dz_l is complete
     const bool ping = adam && !dp && w.ping && l >= w.dw_main;
@@ -806,32 +811,28 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     // the DP exchange and by side-stream dW GEMMs (every ev_every-th layer;
     // the lowest side layer always records, flushing the deferred ones)
     const bool side_dw = adam && !dp && !ping && l >= w.dw_main;
-    const bool rec = dp || (side_dw && (h->ev_every <= 1 || l == w.dw_main ||
+    const bool rec = bk || (side_dw && (h->ev_every <= 1 || l == w.dw_main ||
                                         (l - w.dw_main) % h->ev_every == 0));
-    int br0[mmad_ae::kMaxChunks], brows[mmad_ae::kMaxChunks];
-    const int nb = dp ? dp_buckets(h, l, br0, brows) : 1;
-    if (!adam || dp) {
+    if (dp) {
+      // data parallel: the dW GEMMs of a bucket's layers are issued together
+      // once the layer that closes it has its dz (one fork per bucket: the
+      // step is host-bound, every event call counts), then the bucket's event
+      pending.push_back(PendingDW{dz, in, a.Np, a.Kp, a.Np, a.Kp, Mp, dwe, l});
+      if (bk) {
+        MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
+        MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
+        for (const PendingDW& q : pending)
+          RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, q.dz, q.lda, q.in, q.ldb, q.M, q.N, q.K, q.ep,
+                         side, nullptr, PROBE_DW + q.layer));
+        pending.clear();
+        MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l], side));
+      }
+    } else if (!adam) {
       // fork: dz_l is complete on the main stream; dW_l overlaps the chain below
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
       MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
-      if (nb == 1) {
-        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
-                       nullptr, PROBE_DW + l));
-        if (dp) MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l * mmad_ae::kMaxChunks], side));
-      } else {
-        // row chunks of dW_l = dz[:, r0:r0+rows]^T a, each bucket's exchange
-        // starting as soon as its rows are written
-        const size_t es = dt == MMAD_BF16 ? 2 : 4;
-        for (int b = 0; b < nb; ++b) {
-          GemmEpi ec = dwe;
-          ec.M = brows[b];
-          ec.out = h->grads + a.w_off + (int64_t)br0[b] * a.Kp;
-          if (ec.gb_src) ec.gb_src += br0[b];
-          RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, (const char*)dz + br0[b] * es, a.Np, in, a.Kp,
-                         brows[b], a.Kp, Mp, ec, side, nullptr, b == 0 ? PROBE_DW + l : -1));
-          MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l * mmad_ae::kMaxChunks + b], side));
-        }
-      }
+      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
+                     nullptr, PROBE_DW + l));
     }
     if (l > 0) {
       const AeLayer& p = h->L[l - 1];
@@ -900,17 +901,19 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
                        h->v + h->n_weight, adam->b1, adam->b2, adam->eps, adam->step_size,
                        adam->bc2_sqrt, nullptr, 0, h->cstream));
     }
-    if (dp) {
-      // data parallel: all-reduce dW_l on the comm stream as soon as it is
-      // complete, then its Adam update (which rewrites W_l, so it also waits
-      // for the main stream's bwd-data of layer l)
+    if (bk) {
+      // data parallel: exchange the bucket this layer closes (layers
+      // bk->l_hi .. l, one contiguous weight range) on the comm stream as soon
+      // as its last dW GEMM is complete, then its Adam update (which rewrites
+      // the bucket's weights, so it also waits for the main stream's bwd-data
+      // of layer l, the last GEMM of the chain that reads them)
       if (l == 0 || !(h->L[l - 1].bn) || (h->vib && l == h->n_enc))
         MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
       MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_data[l], 0));
       const int nr = mmad_comm_size(h->comm) > 0 ? mmad_comm_size(h->comm) : 1;
-      for (int b = 0; b < nb; ++b) {
-        MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_dw[l * mmad_ae::kMaxChunks + b], 0));
-        const int64_t n = (int64_t)brows[b] * a.Kp, boff = a.w_off + (int64_t)br0[b] * a.Kp;
+      MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_dw[l], 0));
+      {
+        const int64_t n = bk->n, boff = bk->off;
         if (h->dp_shard && n % nr == 0 && (n / nr) % 4 == 0) {
           // ZeRO-1 form: reduce-scatter, Adam on this rank's shard, all-gather
           // of the updated weights the next step reads (bf16 shadow / fp32 p)
@@ -928,13 +931,12 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
         } else {
           RET_IF(mmad_allreduce_bucket(h->comm, h->grads + boff, n, h->cstream));
           void* sh = adam_shadow(h, a, w.ping);
-          if (sh) sh = (char*)sh + (int64_t)br0[b] * a.Kp * 2;
           RET_IF(mmad_adam(n, h->params + boff, h->grads + boff, h->m + boff, h->v + boff,
                            adam->b1, adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt,
                            sh, h->dtype == MMAD_BF16 ? n : 0, h->cstream));
         }
       }
-    } else if (adam) {
+    } else if (adam && !dp) {
       // dW_l with this layer's Adam update fused into its epilogue.  It rewrites
       // W_l, so it starts only once the main stream has finished reading W_l
       // (bwd-data of l); the rest of the chain keeps overlapping it.
@@ -1144,8 +1146,7 @@ int mmad_ae_train_step_graph(mmad_ae* h, const float* x, int ld_x, int B, int k,
   hipGraphExec_t exec = nullptr;
   hipError_t ei = hipErrorUnknown;
   if (rc == MMAD_OK && ec == hipSuccess && graph)
-    ei = hipGraphInstantiateWithFlags(&exec, graph,
-                                      h->graph_prio ? hipGraphInstantiateFlagUseNodePriority : 0);
+    ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
   if (graph) (void)hipGraphDestroy(graph);
   if (rc != MMAD_OK || ec != hipSuccess || ei != hipSuccess) {
     // this step already ran eagerly; later calls stay eager
@@ -1175,7 +1176,7 @@ int mmad_ae_set_comm(mmad_ae* h, mmad_comm* c) {
     int least = 0, greatest = 0;
     MMAD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     MMAD_HIP_CHECK(hipStreamCreateWithPriority(&h->cstream, hipStreamNonBlocking, greatest));
-    h->ev_dw.resize(h->L.size() * mmad_ae::kMaxChunks);
+    h->ev_dw.resize(h->L.size());
     for (auto& e : h->ev_dw) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, h->ev_flags_));
     MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_small, h->ev_flags_));
     MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_cdone, h->ev_flags_));
@@ -1191,17 +1192,14 @@ int mmad_ae_dp_sync_master(mmad_ae* h, void* stream) {
   if (!h->comm || !h->master_stale) return MMAD_OK;
   hipStream_t st = (hipStream_t)stream;
   const int nr = mmad_comm_size(h->comm);
-  for (int l = 0; l < (int)h->L.size(); ++l) {
-    const AeLayer& a = h->L[l];
-    int br0[mmad_ae::kMaxChunks], brows[mmad_ae::kMaxChunks];
-    const int nb = dp_buckets(h, l, br0, brows);
-    for (int b = 0; b < nb; ++b) {
-      const int64_t n = (int64_t)brows[b] * a.Kp, boff = a.w_off + (int64_t)br0[b] * a.Kp;
-      if (!(n % nr == 0 && (n / nr) % 4 == 0)) continue;   // an all-reduced bucket: already current
-      if (h->dtype == MMAD_BF16) RET_IF(mmad_all_gather_bucket(h->comm, h->params + boff, n, MMAD_F32, st));
-      RET_IF(mmad_all_gather_bucket(h->comm, h->m + boff, n, MMAD_F32, st));
-      RET_IF(mmad_all_gather_bucket(h->comm, h->v + boff, n, MMAD_F32, st));
-    }
+  std::vector<DpBucket> plan;
+  dp_plan(h, plan);
+  for (const DpBucket& b : plan) {
+    const int64_t n = b.n, boff = b.off;
+    if (!(n % nr == 0 && (n / nr) % 4 == 0)) continue;   // an all-reduced bucket: already current
+    if (h->dtype == MMAD_BF16) RET_IF(mmad_all_gather_bucket(h->comm, h->params + boff, n, MMAD_F32, st));
+    RET_IF(mmad_all_gather_bucket(h->comm, h->m + boff, n, MMAD_F32, st));
+    RET_IF(mmad_all_gather_bucket(h->comm, h->v + boff, n, MMAD_F32, st));
   }
   h->master_stale = false;
   return MMAD_OK;

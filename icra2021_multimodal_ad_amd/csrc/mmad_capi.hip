@@ -62,8 +62,8 @@ int g_knob[MMAD_KNOB_COUNT] = {
     0,     // 26 side stream at the highest priority (schedule sweeps)
     0,     // 27 executor events with the system-scope fence
     1,     // 28 DP: sharded weight buckets (reduce-scatter, Adam on 1/N, all-gather)
-    0,     // 29 captured train-step graph instantiated with per-node (captured stream) priorities
-    1,     // 30 DP: row chunks per weight bucket of the last two layers of the backward
+    0,     // 29 retired (graph node priorities: no effect, profiles/r03w_graph_priority.txt)
+    8,     // 30 DP: minimum exchange bucket (MiB of fp32 gradient; consecutive layers merge)
 };
 }  // namespace
 int mmad_knob(int k) { return g_knob[k]; }
@@ -102,7 +102,7 @@ int mmad_tile_epi_override(int epi) {
 }
 
 static bool knob_valid(int knob) {
-  return knob >= 0 && knob < MMAD_KNOB_COUNT && !(knob >= 12 && knob <= 15);
+  return knob >= 0 && knob < MMAD_KNOB_COUNT && !(knob >= 12 && knob <= 15) && knob != 29;
 }
 int mmad_tune_set(int knob, int value) {
   if (!knob_valid(knob)) {

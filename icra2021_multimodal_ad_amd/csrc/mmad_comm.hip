@@ -58,15 +58,14 @@ struct mmad_comm {
 
 namespace {
 // loopback "all-reduce": buf *= s, after a short delay so that a missing
-// dependency on the producer of buf shows up as a wrong result.  The delay is
-// one sleeping wave of its own launch ahead of the scaling (same stream): a
-// spin in every block of the scaling grid would hold CUs for the delay and
-// stand in for an exchange far heavier than RCCL's few channel workgroups.
-__global__ void loopback_delay_k() {
+// dependency on the producer of buf shows up as a wrong result.  A small grid
+// (<= 256 workgroups, one per CU) whose waves sleep through the delay (s_sleep, no issue
+// pressure) and then scale: one launch, like an RCCL call, and it does not
+// hold the chip the way a spin in every block of a full grid did (that stood
+// in for an exchange far heavier than RCCL's few channel workgroups)
+__global__ void loopback_k(float* __restrict__ buf, int64_t n, float s) {
   const long long t0 = clock64();
   while (clock64() - t0 < 20000) __builtin_amdgcn_s_sleep(8);
-}
-__global__ void loopback_k(float* __restrict__ buf, int64_t n, float s) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     buf[i] *= s;
 }
@@ -137,9 +136,7 @@ int mmad_allreduce_bucket(mmad_comm* c, float* buf, int64_t n, void* stream) {
   MMAD_CHECK_ARG(c && (buf || n == 0) && n >= 0, "allreduce_bucket: bad arguments");
   if (n == 0) return MMAD_OK;
   if (c->loopback > 0.f) {
-    const int64_t blocks = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
-    loopback_delay_k<<<1, 64, 0, (hipStream_t)stream>>>();
-    MMAD_LAUNCH_CHECK();
+    const int64_t blocks = (n + 255) / 256 < 256 ? (n + 255) / 256 : 256;
     loopback_k<<<(int)blocks, 256, 0, (hipStream_t)stream>>>(buf, n, c->loopback);
     MMAD_LAUNCH_CHECK();
     return MMAD_OK;
@@ -160,8 +157,10 @@ int mmad_reduce_scatter_bucket(mmad_comm* c, float* buf, int64_t n, void* stream
   MMAD_CHECK_ARG(n % c->nranks == 0, "reduce_scatter_bucket: n=%lld not divisible by %d ranks",
                  (long long)n, c->nranks);
   if (n == 0) return MMAD_OK;
-  if (c->loopback > 0.f) return mmad_allreduce_bucket(c, buf, n, stream);   // one rank: shard = all
   const size_t cnt = (size_t)(n / c->nranks);
+  // loopback posing as rank r of N: like RCCL's in-place reduce-scatter, only
+  // this rank's slice [r * n / N, (r + 1) * n / N) receives the reduced values
+  if (c->loopback > 0.f) return mmad_allreduce_bucket(c, buf + (size_t)c->rank * cnt, (int64_t)cnt, stream);
   MMAD_RCCL_CHECK(rccl().reduce_scatter(buf, buf + (size_t)c->rank * cnt, cnt, ncclFloat32, ncclSum,
                                         c->comm, (hipStream_t)stream));
   return MMAD_OK;

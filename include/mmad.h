@@ -78,10 +78,10 @@ int mmad_pad_granule(void);
  *   27 executor events with the system-scope fence (0)
  *   28 data parallel: sharded weight buckets (reduce-scatter, Adam on 1/N,
  *      all-gather; 1) or all-reduce + full Adam (0)
- *   29 the captured train-step graph keeps each node's stream priority
- *      (hipGraphInstantiateFlagUseNodePriority; 0)
- *   30 data parallel: row chunks (1-8) of the weight buckets of the last two
- *      layers of the backward, each exchanged as its dW rows complete (1) */
+ *   29 retired (EINVAL)
+ *   30 data parallel: minimum exchange bucket in MiB of fp32 gradient;
+ *      consecutive layers (backward order) share a bucket until it holds this
+ *      much (8; 0 = one bucket per layer) */
 #define MMAD_KNOB_COUNT 31
 int mmad_tune_set(int knob, int value);
 int mmad_tune_get(int knob, int* value);
@@ -383,7 +383,8 @@ int mmad_comm_create(mmad_comm** out, const void* unique_id, int nranks, int ran
  * shards) after a short delay */
 int mmad_comm_create_loopback(mmad_comm** out, float scale);
 /* ... posing as rank `rank` of `nranks` (tests of the sharded step's shard
- * arithmetic on one GPU: its reduce-scatter scales the whole bucket, its
+ * arithmetic on one GPU: its reduce-scatter scales this rank's slice of the
+ * bucket -- the slice RCCL's in-place reduce-scatter writes -- and its
  * all-gather leaves the other ranks' shards untouched) */
 int mmad_comm_create_loopback_ranks(mmad_comm** out, float scale, int nranks, int rank);
 void mmad_comm_destroy(mmad_comm* c);

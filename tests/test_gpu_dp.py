@@ -117,15 +117,15 @@ def test_native_comm_single_rank_step_matches_fused():
         lib.mmad_comm_destroy(h)
 
 
-@pytest.mark.parametrize("dtype,chunks", [("f32", 1), ("bf16", 1), ("bf16", 3), ("f32", 4)])
-def test_native_exchange_schedule_loopback(dtype, chunks):
+@pytest.mark.parametrize("dtype,mib", [("f32", 8), ("bf16", 8), ("bf16", 0), ("f32", 1000)])
+def test_native_exchange_schedule_loopback(dtype, mib):
     """Exchange schedule of the native DP step on one GPU: a loopback
     communicator whose all-reduce doubles each bucket (= 2 identical shards)
     after a delay.  Must equal: plain fwd+bwd, grads *= 2, loss *= 2, flat Adam
     -- i.e. every bucket is reduced after its producer finished and before its
-    Adam, and the small bucket + loss are reduced too.  chunks > 1 (knob
-    dp_chunks): the last two layers' buckets go out as row chunks of their dW
-    GEMMs, each exchanged once its rows are written."""
+    Adam, and the small bucket + loss are reduced too -- whatever the bucket
+    plan (knob dp_bucket_mib: 0 = one bucket per layer, 1000 = all weights in
+    one bucket closed by layer 0)."""
     import ctypes
     import types as _t
     from icra2021_multimodal_ad_amd import _native
@@ -144,7 +144,7 @@ def test_native_exchange_schedule_loopback(dtype, chunks):
                            init_state_dict(700, 40, 5, seed=81).items()})
         return m
     try:
-        with _native.tune(dp_chunks=chunks):
+        with _native.tune(dp_bucket_mib=mib):
             ma = mk()
         mb = mk()
         ma._native.set_comm(comm)
@@ -254,31 +254,33 @@ def test_native_comm_self_test_passes_and_catches_a_broken_exchange():
     lib.mmad_comm_destroy(hb)
 
 
-def _dp_buckets(L, l, chunks):
-    """Row ranges of layer l's weight buckets (mirror of mmad_ae.hip dp_buckets:
-    the two lowest layers in `chunks` chunks of whole 128-row groups)."""
-    groups = L["Np"] // 128
-    nch = min(chunks if l < 2 else 1, max(groups, 1))
-    if nch <= 1:
-        return [(0, L["Np"])]
-    per = -(-groups // nch)
-    return [(g0 * 128, (min(g0 + per, groups) - g0) * 128) for g0 in range(0, groups, per)]
+def _dp_plan(layers, mib):
+    """(offset, n) of every weight exchange bucket (mirror of mmad_ae.hip
+    dp_plan: consecutive layers in backward order until >= mib MiB of fp32)."""
+    out, acc = [], 0
+    for l in range(len(layers) - 1, -1, -1):
+        acc += layers[l]["Np"] * layers[l]["Kp"]
+        if acc * 4 >= mib * (1 << 20) or l == 0:
+            out.append((layers[l]["w_off"], acc))
+            acc = 0
+    return out
 
 
-@pytest.mark.parametrize("dtype,rank,chunks", [("bf16", 0, 1), ("bf16", 1, 1), ("f32", 1, 1),
-                                               ("bf16", 1, 4), ("f32", 0, 3)])
-def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank, chunks):
+@pytest.mark.parametrize("dtype,rank,mib", [("bf16", 0, 8), ("bf16", 1, 8), ("f32", 1, 8),
+                                            ("bf16", 1, 0), ("f32", 0, 2)])
+def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank, mib):
     """The sharded DP step (knob dp_shard: reduce-scatter, Adam on this rank's
     1/N of each weight bucket, all-gather of the updated weights) on one GPU,
     through a loopback communicator posing as rank `rank` of 2 (its
-    reduce-scatter doubles the whole bucket = 2 identical shards, its
-    all-gather leaves the other rank's shard alone).  This rank's shard of
+    reduce-scatter doubles this rank's slice = 2 identical shards summed into
+    the slice RCCL's in-place reduce-scatter writes, its all-gather leaves the
+    other rank's shard alone).  This rank's shard of
     every weight bucket -- p, m, v and the bf16 shadow -- equals "grads x 2,
     then Adam" bit for bit; the other shard keeps its pre-step p / m / v;
     the small bucket is all-reduced and fully updated; the handle reports
-    stale master weights and refuses to detach until synced.  With chunks > 1
-    every row chunk of the last two layers is its own bucket with its own
-    shards."""
+    stale master weights and refuses to detach until synced.  The shards
+    follow the bucket plan (knob dp_bucket_mib: consecutive layers share a
+    bucket, split once over the ranks)."""
     import ctypes
     import types as _t
     from icra2021_multimodal_ad_amd import _native
@@ -298,7 +300,7 @@ def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank, chunks):
         m._native.sync_shadow(force=True)
         return m
     try:
-        with _native.tune(dp_chunks=chunks):
+        with _native.tune(dp_bucket_mib=mib):
             ma = mk()
         mb = mk()
         a, b = ma._native, mb._native
@@ -312,22 +314,18 @@ def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank, chunks):
         torch.cuda.synchronize()
         assert abs(la - 2.0 * float(lb)) <= 1e-5 * abs(la)
         assert lib.mmad_ae_dp_master_stale(a._h) == 1
-        nb = 0
-        for li, L in enumerate(a.layers):
-            for r0, rows in _dp_buckets(L, li, chunks):
-                nb += 1
-                n = rows * L["Kp"]
-                boff = L["w_off"] + r0 * L["Kp"]
-                lo = boff + rank * (n // 2)
-                own = slice(lo, lo + n // 2)
-                other = slice(boff + (1 - rank) * (n // 2), boff + (2 - rank) * (n // 2))
-                for name, ref0 in (("params", p0), ("exp_avg", m0), ("exp_avg_sq", v0)):
-                    got, want = getattr(a, name), getattr(b, name)
-                    assert torch.equal(got[own], want[own]), (name, L["w_off"], r0)
-                    assert torch.equal(got[other], ref0[other]), (name, "other shard changed", r0)
-                if dtype == "bf16":
-                    assert torch.equal(a.shadow[own], b.shadow[own])
-        assert nb > len(a.layers) or chunks == 1
+        plan = _dp_plan(a.layers, mib)
+        assert (len(plan) == len(a.layers)) == (mib == 0)
+        for boff, n in plan:
+            lo = boff + rank * (n // 2)
+            own = slice(lo, lo + n // 2)
+            other = slice(boff + (1 - rank) * (n // 2), boff + (2 - rank) * (n // 2))
+            for name, ref0 in (("params", p0), ("exp_avg", m0), ("exp_avg_sq", v0)):
+                got, want = getattr(a, name), getattr(b, name)
+                assert torch.equal(got[own], want[own]), (name, boff)
+                assert torch.equal(got[other], ref0[other]), (name, "other shard changed", boff)
+            if dtype == "bf16":
+                assert torch.equal(a.shadow[own], b.shadow[own])
         nw = a.n_weight
         for name in ("params", "exp_avg", "exp_avg_sq"):      # the small bucket: all-reduced
             assert torch.equal(getattr(a, name)[nw:], getattr(b, name)[nw:]), name

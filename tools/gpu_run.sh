@@ -9,6 +9,7 @@
 #   py:<script,args> python <script> <args>          (tools/*.py helpers)
 #   bin:<path,args>  a prebuilt binary (tools/ubench_*)
 #   trace:<script,args>  rocprofv3 --kernel-trace --stats of python <script> <args>
+#   htrace:<script,args> rocprofv3 --hip-trace --kernel-trace (host API timeline)
 #   pmc:<ctr+ctr>:<script,args>  one rocprofv3 --pmc pass (counters joined by '+')
 # Every GPU step runs under its own timeout; logs go to gpurun_out/<tag>_*.
 set -o pipefail
@@ -49,6 +50,15 @@ for step in "$@"; do
     trace)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_${i}_trace -o run -- \
         python3 ${arg//,/ } > "$log" 2>&1 ;;
+    htrace)
+      # summarised on the box (the raw trace is large), then removed
+      timeout -k 10 400 rocprofv3 --hip-trace --kernel-trace -d /tmp/${T}_${i}_htrace -o run -- \
+        python3 ${arg//,/ } > "$log" 2>&1 &&
+        python3 tools/hip_api_stats.py /tmp/${T}_${i}_htrace --steps 20 > gpurun_out/${T}_${i}_api.txt 2>&1 &&
+        python3 tools/host_gaps.py /tmp/${T}_${i}_htrace > gpurun_out/${T}_${i}_gaps.txt 2>&1 &&
+        python3 tools/prof_step.py "$(ls /tmp/${T}_${i}_htrace/*/*.db /tmp/${T}_${i}_htrace/*.db 2>/dev/null | head -1)" \
+          --last 15 > gpurun_out/${T}_${i}_timeline.txt 2>&1
+      rm -rf /tmp/${T}_${i}_htrace ;;
     pmc)
       ctr=${arg%%:*}
       cmd=${arg#*:}

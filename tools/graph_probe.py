@@ -1,6 +1,5 @@
 """The c2 train step, eager or as one captured hipGraph per step, for a
-rocprofv3 kernel trace.  Usage: python tools/graph_probe.py eager|graph|graphp [steps=30]
-(graphp: the graph instantiated with per-node stream priorities, knob graph_prio)"""
+rocprofv3 kernel trace.  Usage: python tools/graph_probe.py eager|graph [steps=30]"""
 import sys
 import time
 import types
@@ -14,7 +13,7 @@ from icra2021_multimodal_ad_amd.data import synth_windows_device
 mode = sys.argv[1]
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 dev = torch.device("cuda", 0)
-with _native.tune(train_graph=mode.startswith("graph"), graph_prio=int(mode == "graphp")):
+with _native.tune(train_graph=mode == "graph"):
     m = get_model(types.SimpleNamespace(input_size=2048, btl_size=100, n_layers=5, gpu_id=0, dtype="bf16"))
 m._native.sync_shadow(force=True)
 opt = torch.optim.Adam(m.parameters(), lr=1e-3)
