@@ -819,13 +819,20 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       // step is host-bound, every event call counts), then the bucket's event
       pending.push_back(PendingDW{dz, in, a.Np, a.Kp, a.Np, a.Kp, Mp, dwe, l});
       if (bk) {
-        MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
-        MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
+        // a bucket made only of the last dw_main layers of the chain runs its
+        // dW GEMMs on the main stream, idle by then, instead of behind the
+        // side stream's backlog (the exchange tail waits for them)
+        const bool on_main = bk->l_hi < w.dw_main;
+        hipStream_t ds = on_main ? st : side;
+        if (!on_main) {
+          MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
+          MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
+        }
         for (const PendingDW& q : pending)
           RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, q.dz, q.lda, q.in, q.ldb, q.M, q.N, q.K, q.ep,
-                         side, nullptr, PROBE_DW + q.layer));
+                         ds, nullptr, PROBE_DW + q.layer));
         pending.clear();
-        MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l], side));
+        MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l], ds));
       }
     } else if (!adam) {
       // fork: dz_l is complete on the main stream; dW_l overlaps the chain below

@@ -2,7 +2,7 @@
 # time limit) for the two roofline kernels bench.py reports, at c2 and c3:
 #   encoder-layer-1 forward GEMM (tools/gemm_one.py) -> gpurun_out/<tag>_{c2,c3}e_pmc_{fetch,write,hit}
 #   Adam-fused dW GEMM (tools/dw_one.py)             -> gpurun_out/<tag>_{c2,c3}w_pmc_{fetch,write,hit,mfma}
-# then: python tools/pmc_traffic.py <tag>_c2e 1024 ae ; python tools/pmc_traffic.py <tag>_c3e 4096 vib_ae
+# summarised at the end (below): python tools/pmc_traffic.py <tag>_c2e 1024 ae ; python tools/pmc_traffic.py <tag>_c3e 4096 vib_ae
 #       python tools/pmc_dw.py <tag>_c2w 1024 1658 2048 0 ae <tile> ; ... <tag>_c3w 4096 1678 2048 0 vib_ae <tile>
 # Usage: bash tools/gpu_pmc_round.sh <tag> [c2 dW tile] [c3 dW tile]   (-2 = the production shape rule)
 set -o pipefail
@@ -23,3 +23,14 @@ for p in "fetch FETCH_SIZE" "write WRITE_SIZE" "hit TCC_HIT_sum TCC_MISS_sum" "m
   pass ${T}_c2w_pmc_$n "$*" python3 tools/dw_one.py 1024 1658 2048 40 $W2 || exit 1
   pass ${T}_c3w_pmc_$n "$*" python3 tools/dw_one.py 4096 1678 2048 40 $W3 || exit 1
 done
+# summarise on the box (the per-pass databases are tens of MB each and gpurun
+# copies back at most 64 MiB) and keep only the JSON summaries + pass logs
+python3 tools/pmc_traffic.py ${T}_c2e 1024 ae &&
+  python3 tools/pmc_traffic.py ${T}_c3e 4096 vib_ae &&
+  python3 tools/pmc_dw.py ${T}_c2w 1024 1658 2048 0 ae 64x64 &&
+  python3 tools/pmc_dw.py ${T}_c3w 4096 1678 2048 0 vib_ae 128x128 &&
+  cp profiles/${T}_*pmc_*.json gpurun_out/
+rc=$?
+rm -rf gpurun_out/${T}_c2e_pmc_*/ gpurun_out/${T}_c3e_pmc_*/ gpurun_out/${T}_c2w_pmc_*/ gpurun_out/${T}_c3w_pmc_*/
+ls gpurun_out/${T}_* 2>/dev/null
+exit $rc

@@ -41,8 +41,14 @@ for step in "$@"; do
     bench)
       timeout -k 10 400 python -u bench.py ${arg//,/ } > "$log" 2>&1 ;;
     prof)
-      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_${i}_prof -o run -- \
-        python3 bench.py ${arg//,/ } > "$log" 2>&1 ;;
+      # keep the --stats CSVs and a per-grid summary; the trace database stays on the box
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/${T}_${i}_prof -o run -- \
+        python3 bench.py ${arg//,/ } > "$log" 2>&1 &&
+        mkdir -p gpurun_out/${T}_${i}_prof &&
+        cp $(find /tmp/${T}_${i}_prof -name "*_stats.csv") gpurun_out/${T}_${i}_prof/ &&
+        python3 tools/prof_db.py "$(find /tmp/${T}_${i}_prof -name '*.db' | head -1)" --by-grid \
+          > gpurun_out/${T}_${i}_prof/kstats_bygrid.txt 2>&1
+      rc_=$?; rm -rf /tmp/${T}_${i}_prof; (exit $rc_) ;;
     py)
       timeout -k 10 400 python -u ${arg//,/ } > "$log" 2>&1 ;;
     bin)
@@ -58,7 +64,7 @@ for step in "$@"; do
         python3 tools/host_gaps.py /tmp/${T}_${i}_htrace > gpurun_out/${T}_${i}_gaps.txt 2>&1 &&
         python3 tools/prof_step.py "$(ls /tmp/${T}_${i}_htrace/*/*.db /tmp/${T}_${i}_htrace/*.db 2>/dev/null | head -1)" \
           --last 15 > gpurun_out/${T}_${i}_timeline.txt 2>&1
-      rm -rf /tmp/${T}_${i}_htrace ;;
+      rc_=$?; rm -rf /tmp/${T}_${i}_htrace; (exit $rc_) ;;
     pmc)
       ctr=${arg%%:*}
       cmd=${arg#*:}
