@@ -45,7 +45,9 @@ for step in "$@"; do
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/${T}_${i}_prof -o run -- \
         python3 bench.py ${arg//,/ } > "$log" 2>&1 &&
         mkdir -p gpurun_out/${T}_${i}_prof &&
-        cp $(find /tmp/${T}_${i}_prof -name "*_stats.csv") gpurun_out/${T}_${i}_prof/ &&
+        { find /tmp/${T}_${i}_prof -name "*stats*.csv" -exec cp {} gpurun_out/${T}_${i}_prof/ \; ; true; } &&
+        python3 tools/prof_db.py "$(find /tmp/${T}_${i}_prof -name '*.db' | head -1)" \
+          > gpurun_out/${T}_${i}_prof/kstats.txt 2>&1 &&
         python3 tools/prof_db.py "$(find /tmp/${T}_${i}_prof -name '*.db' | head -1)" --by-grid \
           > gpurun_out/${T}_${i}_prof/kstats_bygrid.txt 2>&1
       rc_=$?; rm -rf /tmp/${T}_${i}_prof; (exit $rc_) ;;
