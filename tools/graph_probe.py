@@ -1,5 +1,6 @@
 """The c2 train step, eager or as one captured hipGraph per step, for a
-rocprofv3 kernel trace.  Usage: python tools/graph_probe.py eager|graph [steps=30]"""
+rocprofv3 kernel trace.  Usage: python tools/graph_probe.py eager|graph [steps=30] [knob=value ...]
+(extra tune-table knobs, e.g. bn_mode=0 side_prio=1, applied while the model is built)"""
 import sys
 import time
 import types
@@ -13,7 +14,8 @@ from icra2021_multimodal_ad_amd.data import synth_windows_device
 mode = sys.argv[1]
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
 dev = torch.device("cuda", 0)
-with _native.tune(train_graph=mode == "graph"):
+extra = {k: int(v) for k, v in (a.split("=") for a in sys.argv[3:])}
+with _native.tune(train_graph=mode == "graph", **extra):
     m = get_model(types.SimpleNamespace(input_size=2048, btl_size=100, n_layers=5, gpu_id=0, dtype="bf16"))
 m._native.sync_shadow(force=True)
 opt = torch.optim.Adam(m.parameters(), lr=1e-3)
@@ -27,5 +29,5 @@ for i in range(steps):
 th = time.perf_counter() - t0
 torch.cuda.synchronize()
 tw = time.perf_counter() - t0
-print(f"{mode}: host {th / steps * 1e6:.1f} us/step, wall {tw / steps * 1e6:.1f} us/step, "
+print(f"{mode} {extra}: host {th / steps * 1e6:.1f} us/step, wall {tw / steps * 1e6:.1f} us/step, "
       f"graphs {m._native._lib.mmad_ae_train_graph_count(m._native._h)}", flush=True)
