@@ -5,8 +5,9 @@ Workloads (``--config``; ``auto`` = c2 on one GPU, c4 on several):
   c2  BASELINE configs[1]: FC-AE, D=2048, 1024 windows, bf16, 1 GPU
   c3  BASELINE configs[2]: VIB-AE (k=1, beta_kl=1), D=2048, 4096 windows, bf16
   c4  BASELINE configs[3]: the c3 model, 4096 windows PER GPU (global 4096*N),
-      one process per GPU, per-layer RCCL all-reduce of the gradients over xGMI
-      overlapped with the backward (weak scaling)
+      one process per GPU, RCCL reduce-scatter / sharded Adam / all-gather of the
+      weight gradients in buckets of consecutive layers over xGMI, overlapped with
+      the backward (weak scaling)
   c5  BASELINE configs[4]: RaPP scoring (get_diffs + BASE + SAP) over 1,048,576
       windows resident in HBM, D=2048, one hipGraph-captured pass per step
       (bench_score.run_c5; metric: scored windows/s)
@@ -350,7 +351,7 @@ def run(args):
     fpw, _ = ae_flops_per_window(nat.enc_widths, nat.dec_widths)
     windows = args.steps * batch * world
     value = windows / el
-    exchange = ("native RCCL per-layer buckets overlapped with backward"
+    exchange = ("native RCCL buckets (reduce-scatter, sharded Adam, all-gather) overlapped with backward"
                 if model.dist is not None and model.dist.native else
                 ("torch.distributed flat all-reduce" if world > 1 else "none"))
     res = {

@@ -122,7 +122,8 @@ class NativeAE:
 
     def set_comm(self, comm):
         """Attach a dist.NativeComm (or None): mmad_ae_train_step then exchanges
-        each layer's gradients on the executor's comm stream before its Adam
+        the weight gradients in buckets of consecutive layers (tune knob
+        dp_bucket_mib) on the executor's comm stream before their Adam
         (sharded: reduce-scatter, Adam on this rank's 1/N, all-gather).
         Detaching first all-gathers the sharded master weights / Adam moments
         (sync_master: collective, so detach on every rank at the same point)."""
