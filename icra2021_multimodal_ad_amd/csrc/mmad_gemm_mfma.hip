@@ -288,6 +288,17 @@ __device__ __forceinline__ void wait_tail(int rem) {
   else wait_vmcnt<0>();
 }
 
+// the same with X more (younger) loads allowed in flight: the dW GEMM's Adam
+// state prefetch, issued after the last ring DMA
+template <int NL, int X>
+__device__ __forceinline__ void wait_tail_x(int rem) {
+  static_assert(3 * NL + X <= 63, "vmcnt range");
+  if (rem >= 3) wait_vmcnt<3 * NL + X>();
+  else if (rem == 2) wait_vmcnt<2 * NL + X>();
+  else if (rem == 1) wait_vmcnt<NL + X>();
+  else wait_vmcnt<X>();
+}
+
 __device__ __forceinline__ void block_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -527,6 +538,29 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   // hipcc's lgkmcnt bookkeeping stays exact, and sched_barriers pin the order.
   using FR = typename SubFrag<T>::F;
   const int ra = wm * 16 * TM, rb = wn * 16 * TN;
+  // Adam-fused dW: the first chunk group of the tile's p / m / v is loaded
+  // right after the ring's last DMA issue, so its HBM round trip runs under
+  // the K loop's last NS-1 stages instead of after the loop (the tail waits
+  // let these APF younger loads stay in flight; APF = 0: not prefetched)
+  constexpr int A_CPR = BN * (int)sizeof(TO) / 16;
+  constexpr int A_ITERS = BM * A_CPR / NT;
+  constexpr int A_AG = A_ITERS < 4 ? A_ITERS : 4;
+  // (not for the 8-wave 256x128 / 128x256 tiles: their 48 prefetch registers
+  // spill beside the larger accumulator set)
+  constexpr bool APF_OK = EPI == GEMM_EPI_BWD_WEIGHT && !BIG && CFG != 1 && CFG != 2 &&
+                          3 * NL + 3 * A_AG <= 63;
+  floatx4 pf_p[A_AG], pf_m[A_AG], pf_v[A_AG];
+  bool pf = false;
+  auto adam_prefetch = [&]() {
+#pragma unroll
+    for (int u = 0; u < A_AG; ++u) {
+      const int idx = u * NT + tid;
+      const size_t off = (size_t)(m0 + idx / A_CPR) * ep.ldo + n0 + (idx % A_CPR) * (16 / (int)sizeof(TO));
+      pf_p[u] = *(const floatx4*)(ep.ad_p + off);
+      pf_m[u] = *(const floatx4*)(ep.ad_m + off);
+      pf_v[u] = *(const floatx4*)(ep.ad_v + off);
+    }
+  };
   if constexpr (BIG) {
     // 256x256 tile (bf16, both operands K-major): a 2-slot ring, one barrier
     // per stage after both 32-deep sub-steps; the fragment registers of a
@@ -594,8 +628,9 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
     FR f0a[TM], f0b[TN], f1a[TM], f1b[TN];
     read_sub<T, AK, BK_, NAT, BM, BN, TM, TN>(smem, smem + IA::BYTES, ra, rb, 0, lane, f0a, f0b);
     wait_lgkm0();
-    auto step = [&](int t, auto issue_c, auto last_c) {
+    auto step = [&](int t, auto issue_c, auto last_c, auto pf_c) {
       constexpr bool ISSUE = decltype(issue_c)::value, LAST = decltype(last_c)::value;
+      constexpr bool PF = decltype(pf_c)::value;   // the Adam prefetch is in flight
       const char* sa = smem + (t % NS) * SLOT;
       mma_half<T, TM, TN, 0>(acc, f0a, f0b);
       MMAD_SB();
@@ -606,6 +641,8 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       if constexpr (!LAST) {
         if constexpr (ISSUE) {
           wait_vmcnt<(NS - 2) * NL>();
+        } else if constexpr (PF && APF_OK) {
+          wait_tail_x<NL, 3 * A_AG>(nt - t - 2);
         } else {
           wait_tail<NL>(nt - t - 2);
         }
@@ -634,9 +671,23 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
     using T_ = std::true_type;
     using F_ = std::false_type;
     int t = 0;
-    for (; t < nt - NS; ++t) step(t, T_{}, F_{});
-    for (; t < nt - 1; ++t) step(t, F_{}, F_{});
-    step(nt - 1, F_{}, T_{});
+    bool apf = false;
+    if constexpr (APF_OK) apf = ep.ad_p != nullptr && nt > NS;
+    if (apf) {
+      // the last issuing stage, then the prefetch behind its DMA
+      for (; t < nt - NS - 1; ++t) step(t, T_{}, F_{}, F_{});
+      step(t++, T_{}, F_{}, F_{});
+      MMAD_SB();
+      adam_prefetch();
+      MMAD_SB();
+      pf = true;
+      for (; t < nt - 1; ++t) step(t, F_{}, F_{}, T_{});
+      step(nt - 1, F_{}, T_{}, T_{});
+    } else {
+      for (; t < nt - NS; ++t) step(t, T_{}, F_{}, F_{});
+      for (; t < nt - 1; ++t) step(t, F_{}, F_{}, F_{});
+      step(nt - 1, F_{}, T_{}, F_{});
+    }
   }
 
   // ---- split-K combine (ticket first, no spin on a block that has not run):
@@ -956,9 +1007,23 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         const int idx = (i0 + u) * NT + tid;
         const int rl = idx / CPR, ch = idx % CPR;
         off[u] = (size_t)(m0 + rl) * ep.ldo + n0 + ch * OEPC;
-        P[u] = *(const floatx4*)(ep.ad_p + off[u]);
-        Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
-        Vv[u] = *(const floatx4*)(ep.ad_v + off[u]);
+      }
+      static_assert(AG == A_AG && CPR == A_CPR, "prefetch group = first epilogue group");
+      if (i0 == 0 && pf) {
+        // the first group was loaded under the K loop (adam_prefetch)
+#pragma unroll
+        for (int u = 0; u < AG; ++u) {
+          P[u] = pf_p[u];
+          Mm[u] = pf_m[u];
+          Vv[u] = pf_v[u];
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < AG; ++u) {
+          P[u] = *(const floatx4*)(ep.ad_p + off[u]);
+          Mm[u] = *(const floatx4*)(ep.ad_m + off[u]);
+          Vv[u] = *(const floatx4*)(ep.ad_v + off[u]);
+        }
       }
 #pragma unroll
       for (int u = 0; u < AG; ++u) {
