@@ -902,8 +902,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       MMAD_HIP_CHECK(hipEventRecord(h->ev_small, st));
       MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_small, 0));
       const int64_t ns = h->n_params - h->n_weight;
-      RET_IF(mmad_allreduce_bucket(h->comm, h->grads + h->n_weight, ns, h->cstream));
-      RET_IF(mmad_allreduce_bucket(h->comm, dp_loss, 1, h->cstream));
+      RET_IF(mmad_allreduce_pair(h->comm, h->grads + h->n_weight, ns, dp_loss, 1, h->cstream));
       RET_IF(mmad_adam(ns, h->params + h->n_weight, h->grads + h->n_weight, h->m + h->n_weight,
                        h->v + h->n_weight, adam->b1, adam->b2, adam->eps, adam->step_size,
                        adam->bc2_sqrt, nullptr, 0, h->cstream));

@@ -25,6 +25,8 @@ struct RcclApi {
   ncclResult_t (*reduce_scatter)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                                  hipStream_t);
   ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+  ncclResult_t (*group_start)();
+  ncclResult_t (*group_end)();
   const char* (*error_string)(ncclResult_t);
   bool ok;
 };
@@ -43,8 +45,11 @@ const RcclApi& rccl() {
     api.reduce_scatter = (decltype(api.reduce_scatter))dlsym(h, "ncclReduceScatter");
     api.all_gather = (decltype(api.all_gather))dlsym(h, "ncclAllGather");
     api.error_string = (decltype(api.error_string))dlsym(h, "ncclGetErrorString");
+    api.group_start = (decltype(api.group_start))dlsym(h, "ncclGroupStart");
+    api.group_end = (decltype(api.group_end))dlsym(h, "ncclGroupEnd");
     api.ok = api.get_unique_id && api.comm_init_rank && api.comm_destroy && api.all_reduce &&
-             api.reduce_scatter && api.all_gather && api.error_string;
+             api.reduce_scatter && api.all_gather && api.error_string && api.group_start &&
+             api.group_end;
   });
   return api;
 }
@@ -143,6 +148,23 @@ int mmad_allreduce_bucket(mmad_comm* c, float* buf, int64_t n, void* stream) {
   }
   MMAD_RCCL_CHECK(rccl().all_reduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, c->comm,
                                     (hipStream_t)stream));
+  return MMAD_OK;
+}
+
+int mmad_allreduce_pair(mmad_comm* c, float* a, int64_t na, float* b, int64_t nb, void* stream) {
+  MMAD_CHECK_ARG(c && (a || na == 0) && (b || nb == 0) && na >= 0 && nb >= 0, "allreduce_pair: bad arguments");
+  if (c->loopback > 0.f) {
+    const int rc = mmad_allreduce_bucket(c, a, na, stream);
+    return rc != MMAD_OK ? rc : mmad_allreduce_bucket(c, b, nb, stream);
+  }
+  MMAD_RCCL_CHECK(rccl().group_start());
+  ncclResult_t r = na ? rccl().all_reduce(a, a, (size_t)na, ncclFloat32, ncclSum, c->comm, (hipStream_t)stream)
+                      : ncclSuccess;
+  if (r == ncclSuccess && nb)
+    r = rccl().all_reduce(b, b, (size_t)nb, ncclFloat32, ncclSum, c->comm, (hipStream_t)stream);
+  const ncclResult_t e = rccl().group_end();   // always close the group
+  MMAD_RCCL_CHECK(r);
+  MMAD_RCCL_CHECK(e);
   return MMAD_OK;
 }
 
