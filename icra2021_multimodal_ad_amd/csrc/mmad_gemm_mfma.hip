@@ -561,6 +561,24 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       pf_v[u] = *(const floatx4*)(ep.ad_v + off);
     }
   };
+  // bwd-data with the BatchNorm-backward partials: this thread's pre-BN
+  // activations a (16 rows x PPT pieces of one column, the epilogue's own
+  // pattern) prefetched the same way, raw (converted only where used)
+  constexpr int B_NG = NT / BN, B_PIECES = BM / 16;
+  constexpr int B_PPT = (B_PIECES + B_NG - 1) / B_NG;
+  constexpr bool BPF_OK = EPI == GEMM_EPI_BWD_DATA && !BIG && B_PIECES % B_NG == 0 && B_PPT <= 2 &&
+                          3 * NL + 16 * B_PPT <= 63;
+  TO pf_a[BPF_OK ? B_PPT : 1][16];
+  bool pfa = false;
+  auto bn_a_prefetch = [&]() {
+    const TO* an = (const TO*)ep.bn_a;
+    const int cc = tid % BN, grp = tid / BN;
+#pragma unroll
+    for (int u = 0; u < B_PPT; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        pf_a[u][r] = an[(size_t)(m0 + (grp + u * B_NG) * 16 + r) * ep.ldo + n0 + cc];
+  };
   if constexpr (BIG) {
     // 256x256 tile (bf16, both operands K-major): a 2-slot ring, one barrier
     // per stage after both 32-deep sub-steps; the fragment registers of a
@@ -643,6 +661,8 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
           wait_vmcnt<(NS - 2) * NL>();
         } else if constexpr (PF && APF_OK) {
           wait_tail_x<NL, 3 * A_AG>(nt - t - 2);
+        } else if constexpr (PF && BPF_OK) {
+          wait_tail_x<NL, 16 * B_PPT>(nt - t - 2);
         } else {
           wait_tail<NL>(nt - t - 2);
         }
@@ -673,14 +693,21 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
     int t = 0;
     bool apf = false;
     if constexpr (APF_OK) apf = ep.ad_p != nullptr && nt > NS;
+    if constexpr (BPF_OK) apf = ep.bn_part != nullptr && ep.bn_a != nullptr && nt > NS;
     if (apf) {
       // the last issuing stage, then the prefetch behind its DMA
       for (; t < nt - NS - 1; ++t) step(t, T_{}, F_{}, F_{});
       step(t++, T_{}, F_{}, F_{});
       MMAD_SB();
-      adam_prefetch();
+      if constexpr (APF_OK) {
+        adam_prefetch();
+        pf = true;
+      }
+      if constexpr (BPF_OK) {
+        bn_a_prefetch();
+        pfa = true;
+      }
       MMAD_SB();
-      pf = true;
       for (; t < nt - 1; ++t) step(t, F_{}, F_{}, T_{});
       step(nt - 1, F_{}, T_{}, T_{});
     } else {
@@ -887,8 +914,11 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
           v = valid ? v : 0.f;
           s1[i >> 1] += v;
         } else if (EPI == GEMM_EPI_MSE) {
-          float d = 0.f;
-          if (valid) d = v + bias - tgt[(size_t)(row % ep.tmod) * ep.ldt + col];
+          // unconditional load at a clamped column (row % tmod is always a
+          // target row): a load guarded per element makes hipcc branch around
+          // each one and wait for it, one round trip per element
+          const float tv = tgt[(size_t)(row % ep.tmod) * ep.ldt + (col < ep.N ? col : ep.N - 1)];
+          const float d = valid ? v + bias - tv : 0.f;
           v = ep.gscale * d;
           s1[i >> 1] += v;
           s2[i >> 1] += d * d;
@@ -1047,12 +1077,33 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
     // null = 0 (NAP run: sum of squared outputs); colw: per-column weights
     uint4v rvs[EPI == GEMM_EPI_SCORE ? ITERS : 1];
     if constexpr (EPI == GEMM_EPI_SCORE) {
+      // one branch around the whole group (a per-chunk "ref ? load : 0"
+      // became a branch per load and a wait after the first one)
+      if (ep.ref) {
 #pragma unroll
-      for (int it = 0; it < ITERS; ++it) {
-        const int idx = it * NT + tid;
-        const int rl = idx / CPR, ch = idx % CPR;
-        rvs[it] = ep.ref ? *(const uint4v*)((const TO*)ep.ref + (size_t)(m0 + rl) * ep.ldref + n0 + ch * OEPC)
-                         : uint4v{0u, 0u, 0u, 0u};
+        for (int it = 0; it < ITERS; ++it) {
+          const int idx = it * NT + tid;
+          const int rl = idx / CPR, ch = idx % CPR;
+          rvs[it] = *(const uint4v*)((const TO*)ep.ref + (size_t)(m0 + rl) * ep.ldref + n0 + ch * OEPC);
+        }
+      } else {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) rvs[it] = uint4v{0u, 0u, 0u, 0u};
+      }
+    }
+    // SCORE per-column weights of this thread's columns (NAP run; 1 without)
+    float wcol[EPI == GEMM_EPI_SCORE ? OEPC : 1];
+    if constexpr (EPI == GEMM_EPI_SCORE && NT % CPR == 0) {
+      const int col0 = n0 + (tid % CPR) * OEPC;
+      if (ep.colw) {
+#pragma unroll
+        for (int e = 0; e < OEPC; e += 4) {
+          const floatx4 w4 = *(const floatx4*)(ep.colw + col0 + e);
+          wcol[e] = w4[0]; wcol[e + 1] = w4[1]; wcol[e + 2] = w4[2]; wcol[e + 3] = w4[3];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < OEPC; ++e) wcol[e] = 1.f;
       }
     }
 #pragma unroll
@@ -1072,10 +1123,16 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         float sq = 0.f;
         float dd[OEPC];
         float wv[OEPC];
+        if constexpr (NT % CPR == 0) {
+          // this thread's columns are the same in every iteration: loaded once
 #pragma unroll
-        for (int e = 0; e < OEPC; e += 4) {
-          const floatx4 w4 = ep.colw ? *(const floatx4*)(ep.colw + col + e) : floatx4{1.f, 1.f, 1.f, 1.f};
-          wv[e] = w4[0]; wv[e + 1] = w4[1]; wv[e + 2] = w4[2]; wv[e + 3] = w4[3];
+          for (int e = 0; e < OEPC; ++e) wv[e] = wcol[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < OEPC; e += 4) {
+            const floatx4 w4 = ep.colw ? *(const floatx4*)(ep.colw + col + e) : floatx4{1.f, 1.f, 1.f, 1.f};
+            wv[e] = w4[0]; wv[e + 1] = w4[1]; wv[e + 2] = w4[2]; wv[e + 3] = w4[3];
+          }
         }
 #pragma unroll
         for (int e = 0; e < OEPC; ++e) {
@@ -1254,6 +1311,29 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       // registers; the 8-wave 256-row / 256-column tiles reload them instead)
       constexpr bool AREG = PPT <= 2;
       float areg[AREG ? PPT : 1][16];
+      // this thread's a values: the ones prefetched under the K loop, or all
+      // loaded here in one block (issued together, one round trip)
+      TO araw[PPT][16];
+      bool have_a = false;
+      if constexpr (BPF_OK && PPT == B_PPT) {
+        if (pfa) {
+#pragma unroll
+          for (int u = 0; u < PPT; ++u)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) araw[u][r] = pf_a[u][r];
+          have_a = true;
+        }
+      }
+      if (!have_a) {
+#pragma unroll
+        for (int u = 0; u < PPT; ++u) {
+          const int pc = grp + u * NG;
+          if (pc < PIECES) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) araw[u][r] = an[(size_t)(m0 + pc * 16 + r) * ep.ldo + col];
+          }
+        }
+      }
 #pragma unroll
       for (int u = 0; u < PPT; ++u) {
         const int pc = grp + u * NG;
@@ -1263,7 +1343,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
           for (int r = 0; r < 16; ++r) {
             const int rl = pc * 16 + r;
             const double dy = to_f32<TO>(*(const TO*)(smem + rl * OSTRIDE + cc * (int)sizeof(TO)));
-            const float avf = to_f32<TO>(an[(size_t)(m0 + rl) * ep.ldo + col]);
+            const float avf = to_f32<TO>(araw[u][r]);
             if constexpr (AREG) areg[u][r] = avf;   // kept for the fused dz below
             const double av = avf;
             s1 += dy;
