@@ -489,6 +489,30 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   if constexpr (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_BWD_DATA) {
     if (ep.bn_sync && tid == 0) gen0 = col_gen(ep.bn_sync + tn);
   }
+  // BatchNorm parameters / statistics of this thread's column (tid % BN, the
+  // epilogues' column), read before the main loop: their round trip hides
+  // under it instead of following the loop or the column barrier
+  float bnp_g = 0.f, bnp_b = 0.f, bnp_rm = 0.f, bnp_rv = 0.f, bnp_mu = 0.f, bnp_rs = 0.f;
+  if constexpr ((EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_BWD_DATA) && !BIG) {
+    const int bc = n0 + tid % BN;
+    const int bcc = bc < ep.N ? bc : ep.N - 1;   // clamped: an unconditional load
+    if constexpr (EPI == GEMM_EPI_FWD) {
+      if (ep.bn_sync) {
+        bnp_g = ep.bn_gamma[bcc];
+        bnp_b = ep.bn_beta[bcc];
+        if (ep.bn_rmean && tm == 0) {
+          bnp_rm = ep.bn_rmean[bcc];
+          bnp_rv = ep.bn_rvar[bcc];
+        }
+      }
+    } else {
+      if (ep.bn_part) {
+        bnp_mu = ep.bn_mean[bc];
+        bnp_rs = ep.bn_rstd[bc];
+      }
+      if (ep.bn_sync) bnp_g = ep.bn_gamma[bcc];
+    }
+  }
   float e_g[QG];
   // db[n] (bias gradient of this layer's output n) is needed by the dW fix-up
   // (BN producer) and by the fused bias Adam (column-tile-0 blocks)
@@ -1219,15 +1243,15 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         float sc = 0.f, sh = 0.f;
         if (c < ep.N) {
           const float rstd = (float)(1.0 / sqrt((double)var + (double)ep.bn_eps));
-          sc = ep.bn_gamma[c] * rstd;
-          sh = ep.bn_beta[c] - mu * sc;
+          sc = bnp_g * rstd;                 // gamma / beta of column c (prefetched)
+          sh = bnp_b - mu * sc;
           if (tm == 0) {
             ep.bn_save_mean[c] = mu;
             ep.bn_save_rstd[c] = rstd;
             if (ep.bn_rmean) {
               const float unb = ep.M > 1 ? var * (float)ep.M / (float)(ep.M - 1) : var;
-              ep.bn_rmean[c] = (1.f - ep.bn_mom) * ep.bn_rmean[c] + ep.bn_mom * mu;
-              ep.bn_rvar[c] = (1.f - ep.bn_mom) * ep.bn_rvar[c] + ep.bn_mom * unb;
+              ep.bn_rmean[c] = (1.f - ep.bn_mom) * bnp_rm + ep.bn_mom * mu;
+              ep.bn_rvar[c] = (1.f - ep.bn_mom) * bnp_rv + ep.bn_mom * unb;
             }
           }
         } else if (tm == 0) {
@@ -1303,7 +1327,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       constexpr int PPT = (PIECES + NG - 1) / NG;   // pieces per thread
       const int cc = tid % BN, grp = tid / BN;
       const int col = n0 + cc;
-      const double mu = ep.bn_mean[col], rs = ep.bn_rstd[col];
+      const double mu = bnp_mu, rs = bnp_rs;   // bn_mean / bn_rstd[col] (prefetched)
       const TO* an = (const TO*)ep.bn_a;
       double* scr = (double*)(smem + BM * OSTRIDE);    // [PIECES][BN]
       double ps1[PPT], ps2[PPT];
@@ -1425,7 +1449,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         }
         __syncthreads();
         const double t1 = s_t1[cc], t2 = s_t2[cc];
-        const double cf = col < ep.N ? (double)ep.bn_gamma[col] * rs / (double)ep.M : 0.0;
+        const double cf = col < ep.N ? (double)bnp_g * rs / (double)ep.M : 0.0;
         const double Md = (double)ep.M;
         // (the piece sums go straight to the fp64 piece scratch: its group-sum
         // use above is finished)
