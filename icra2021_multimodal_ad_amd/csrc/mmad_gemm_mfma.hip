@@ -585,6 +585,30 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       pf_v[u] = *(const floatx4*)(ep.ad_v + off);
     }
   };
+  // the layer's small Adam segment [bias | gamma | beta] this block updates in
+  // its epilogue (bias: the column-tile-0 blocks, one row per thread; gamma |
+  // beta: 4 per thread of the first tiles): read before the main loop, as
+  // nothing else writes it during this launch and its gradients are final
+  float smp_p = 0.f, smp_m = 0.f, smp_v = 0.f;
+  floatx4 smq_g{}, smq_p{}, smq_m{}, smq_v{};
+  bool smq = false;
+  if constexpr (APF_OK) {
+    if (ep.sm_p) {
+      if (tn == 0 && tid < BM && m0 + tid < ep.sm_bNp) {
+        smp_p = ep.sm_p[m0 + tid];
+        smp_m = ep.sm_m[m0 + tid];
+        smp_v = ep.sm_v[m0 + tid];
+      }
+      const int i4 = ep.sm_bNp + (tile * NT + tid) * 4;
+      if (i4 < ep.sm_n) {
+        smq_g = *(const floatx4*)(ep.sm_g + i4);
+        smq_p = *(const floatx4*)(ep.sm_p + i4);
+        smq_m = *(const floatx4*)(ep.sm_m + i4);
+        smq_v = *(const floatx4*)(ep.sm_v + i4);
+        smq = true;
+      }
+    }
+  }
   // bwd-data with the BatchNorm-backward partials: this thread's pre-BN
   // activations a (16 rows x PPT pieces of one column, the epilogue's own
   // pattern) prefetched the same way, raw (converted only where used)
@@ -1295,14 +1319,34 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         const int n = m0 + tid;
         float g = ep.gb_src ? (n < ep.sm_bN ? db_own : 0.f) : ep.sm_g[n];
         if (ep.gb_src) ep.sm_g[n] = g;
-        float pp = ep.sm_p[n], mm = ep.sm_m[n], vv = ep.sm_v[n];
+        float pp, mm, vv;
+        if constexpr (APF_OK) {
+          pp = smp_p;                        // prefetched before the main loop
+          mm = smp_m;
+          vv = smp_v;
+        } else {
+          pp = ep.sm_p[n];
+          mm = ep.sm_m[n];
+          vv = ep.sm_v[n];
+        }
         adam_elem(pp, mm, vv, g, ep.ad_b1, ep.ad_b2, ep.ad_eps, ad_step, ad_bc2);
         ep.sm_p[n] = pp;
         ep.sm_m[n] = mm;
         ep.sm_v[n] = vv;
       }
       // gamma | beta (grads already final), 4 per thread over all tiles
-      for (int q = tile * NT + tid; ep.sm_bNp + q * 4 < ep.sm_n; q += ntl * NT) {
+      int q = tile * NT + tid;
+      if (smq) {
+        // the first chunk was read before the main loop
+        const int i4 = ep.sm_bNp + q * 4;
+        floatx4 pp = smq_p, mm = smq_m, vv = smq_v;
+        adam4(pp, mm, vv, smq_g, ep.ad_b1, ep.ad_b2, ep.ad_eps, ad_step, ad_bc2);
+        *(floatx4*)(ep.sm_p + i4) = pp;
+        *(floatx4*)(ep.sm_m + i4) = mm;
+        *(floatx4*)(ep.sm_v + i4) = vv;
+        q += ntl * NT;
+      }
+      for (; ep.sm_bNp + q * 4 < ep.sm_n; q += ntl * NT) {
         const int i4 = ep.sm_bNp + q * 4;
         const floatx4 gg = *(const floatx4*)(ep.sm_g + i4);
         floatx4 pp = *(floatx4*)(ep.sm_p + i4), mm = *(floatx4*)(ep.sm_m + i4);
