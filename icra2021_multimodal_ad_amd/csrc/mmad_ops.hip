@@ -559,30 +559,48 @@ __global__ __launch_bounds__(1024) void sum2d_k(int rows, int cols, const float*
   }
 }
 
-template <typename T>
+// PU output chunks per thread (chunk u of the block at blockIdx*256*PU +
+// u*256 + tid): every chunk's loads are issued before the first conversion,
+// PU x V/4 16-B loads in flight per thread
+template <typename T, int PU>
 __global__ void pack_input_k(int M, int K, int Mp, int Kp, const float* __restrict__ x, int ldx,
                              int vec, T* __restrict__ out, const MmadDyn* __restrict__ dyn) {
   constexpr int V = Vec<T>::N;
   if (dyn) x = dyn->x;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int cpr = Kp / V;
-  if (idx >= (int64_t)Mp * cpr) return;
-  const int row = (int)(idx / cpr), c0 = (int)(idx % cpr) * V;
-  uint4v r;
-  T* p = (T*)&r;
-  const float* src = x + (size_t)row * ldx + c0;
-  if (vec && row < M && c0 + V <= K) {
-    // 16-B aligned rows (checked by the launcher): V/4 dwordx4 loads
-    floatx4 f[V / 4];
+  const int64_t total = (int64_t)Mp * cpr;
+  const int64_t base = (int64_t)blockIdx.x * blockDim.x * PU + threadIdx.x;
+  floatx4 f[PU][V / 4];
+  bool full[PU];
 #pragma unroll
-    for (int q = 0; q < V / 4; ++q) f[q] = *(const floatx4*)(src + 4 * q);
+  for (int u = 0; u < PU; ++u) {
+    const int64_t idx = base + (int64_t)u * blockDim.x;
+    const int row = (int)(idx / cpr), c0 = (int)(idx % cpr) * V;
+    full[u] = vec && idx < total && row < M && c0 + V <= K;
+    if (full[u]) {
+      // 16-B aligned rows (checked by the launcher): V/4 dwordx4 loads
+      const float* src = x + (size_t)row * ldx + c0;
 #pragma unroll
-    for (int k = 0; k < V; ++k) p[k] = from_f32<T>(f[k / 4][k % 4]);
-  } else {
-#pragma unroll
-    for (int k = 0; k < V; ++k) p[k] = from_f32<T>((row < M && c0 + k < K) ? src[k] : 0.f);
+      for (int q = 0; q < V / 4; ++q) f[u][q] = *(const floatx4*)(src + 4 * q);
+    }
   }
-  *(uint4v*)(out + (size_t)row * Kp + c0) = r;
+#pragma unroll
+  for (int u = 0; u < PU; ++u) {
+    const int64_t idx = base + (int64_t)u * blockDim.x;
+    if (idx >= total) continue;
+    const int row = (int)(idx / cpr), c0 = (int)(idx % cpr) * V;
+    uint4v r;
+    T* p = (T*)&r;
+    if (full[u]) {
+#pragma unroll
+      for (int k = 0; k < V; ++k) p[k] = from_f32<T>(f[u][k / 4][k % 4]);
+    } else {
+      const float* src = x + (size_t)row * ldx + c0;
+#pragma unroll
+      for (int k = 0; k < V; ++k) p[k] = from_f32<T>((row < M && c0 + k < K) ? src[k] : 0.f);
+    }
+    *(uint4v*)(out + (size_t)row * Kp + c0) = r;
+  }
 }
 
 template <typename T>
@@ -1032,10 +1050,10 @@ int mmad_pack_input_dyn(int dtype, int M, int K, int Mp, int Kp, const float* x,
   const int vec = ((uintptr_t)x % 16 == 0 && ld_x % 4 == 0) ? 1 : 0;
   if (dtype == MMAD_BF16) {
     const int64_t n = (int64_t)Mp * (Kp / 8);
-    pack_input_k<bf16><<<nblk(n, 256), 256, 0, s>>>(M, K, Mp, Kp, x, ld_x, vec, (bf16*)out, dyn);
+    pack_input_k<bf16, 4><<<nblk(n, 256 * 4), 256, 0, s>>>(M, K, Mp, Kp, x, ld_x, vec, (bf16*)out, dyn);
   } else {
     const int64_t n = (int64_t)Mp * (Kp / 4);
-    pack_input_k<float><<<nblk(n, 256), 256, 0, s>>>(M, K, Mp, Kp, x, ld_x, vec, (float*)out, dyn);
+    pack_input_k<float, 4><<<nblk(n, 256 * 4), 256, 0, s>>>(M, K, Mp, Kp, x, ld_x, vec, (float*)out, dyn);
   }
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;

@@ -49,7 +49,9 @@ for step in "$@"; do
         python3 tools/prof_db.py "$(find /tmp/${T}_${i}_prof -name '*.db' | head -1)" \
           > gpurun_out/${T}_${i}_prof/kstats.txt 2>&1 &&
         python3 tools/prof_db.py "$(find /tmp/${T}_${i}_prof -name '*.db' | head -1)" --by-grid \
-          > gpurun_out/${T}_${i}_prof/kstats_bygrid.txt 2>&1
+          > gpurun_out/${T}_${i}_prof/kstats_bygrid.txt 2>&1 &&
+        python3 tools/prof_step.py "$(find /tmp/${T}_${i}_prof -name '*.db' | head -1)" --last 20 \
+          > gpurun_out/${T}_${i}_prof/timeline.txt 2>&1
       rc_=$?; rm -rf /tmp/${T}_${i}_prof; (exit $rc_) ;;
     py)
       timeout -k 10 400 python -u ${arg//,/ } > "$log" 2>&1 ;;

@@ -1,6 +1,6 @@
 """Tile x split-K sweep of the bench GEMM shapes (D=2048 AE, bf16) with the
 K loop on and off (tuning knob 3 bit 0 skips it: prologue + epilogue only).
-Usage: python tools/splitk_sweep.py [batch=1024] [kinds=fwd,bwd_data,bwd_w] [layers=0,1]"""
+Usage: python tools/splitk_sweep.py [batch=1024] [kinds=fwd,bwd_data,bwd_w] [layers=0,1]  (lists: "," or "+")"""
 import json
 import sys
 
@@ -10,8 +10,8 @@ from icra2021_multimodal_ad_amd import _native
 from icra2021_multimodal_ad_amd._native import call, ptr, stream_ptr, pad
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
-kinds = (sys.argv[2] if len(sys.argv) > 2 else "fwd,bwd_data,bwd_w").split(",")
-layers = [int(v) for v in (sys.argv[3] if len(sys.argv) > 3 else "0,1").split(",")]
+kinds = (sys.argv[2] if len(sys.argv) > 2 else "fwd,bwd_data,bwd_w").replace("+", ",").split(",")
+layers = [int(v) for v in (sys.argv[3] if len(sys.argv) > 3 else "0,1").replace("+", ",").split(",")]
 widths = [2048, 1658, 1268, 879, 489, 100, 489, 879, 1268, 1658, 2048]
 dev = torch.device("cuda", 0)
 lib = _native.load()
