@@ -415,10 +415,10 @@ def run(args):
         model.dist = mdl_dist
     durs, n_probe, probe_layers = [], 0, None
     if not args.no_probe and rank == 0:
-        # the timed steps replay one captured hipGraph each, so the dominant
-        # kernel is timed by the executor's probe on EAGER steps of the same
-        # state and inputs right after the timed region (HIP event pair around
-        # that one launch, on the stream it is launched on)
+        # the dominant kernel is timed by the executor's probe on eager steps
+        # of the same state and inputs right after the timed region (a HIP
+        # event pair around that one launch, on the stream it is launched on;
+        # the probe's events stay out of the timed steps)
         import ctypes
         n_probe = max(20, args.steps // 4)
         graph_mode = nat.use_graph

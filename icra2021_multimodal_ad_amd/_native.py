@@ -187,10 +187,14 @@ def load():
     return lib
 
 
+def last_error():
+    """This thread's last libmmad error string."""
+    return load().mmad_last_error_string().decode(errors="replace")
+
+
 def check(status, what=""):
     if status != MMAD_OK:
-        msg = load().mmad_last_error_string().decode(errors="replace")
-        raise NativeError(f"{what}: status {status}: {msg}")
+        raise NativeError(f"{what}: status {status}: {last_error()}")
 
 
 def call(name, *args):

@@ -68,15 +68,28 @@ class _AEFunction(torch.autograd.Function):
         return (None, None, *grads)
 
 
-def _check_status_all(model):
+# under data parallelism the status flag is exchanged every STATUS_EVERY calls
+# (and at every epoch end, dist.DataParallel.epoch_end), not per step: the
+# exchange is one more collective plus a host round trip on a sub-millisecond
+# step.  A timed-out barrier only invalidates results -- every rank still
+# issues the same collectives -- so deferring the check cannot hang a rank.
+STATUS_EVERY = 16
+
+
+def _check_status_all(model, force=False):
     """model._native.check_status() (a kernel barrier / split-K combine that
     timed out leaves that call's outputs unwritten).  Under data parallelism
     the failure is local to one GPU, so the flag is MAX-all-reduced and every
-    rank raises together instead of the others blocking in the next
-    collective."""
+    rank raises together instead of one rank stopping alone; that exchange
+    runs every STATUS_EVERY-th call (or when ``force``d), the same count on
+    every rank."""
     d = getattr(model, "dist", None)
     if d is None or getattr(d, "world", 1) <= 1:
         model._native.check_status()
+        return
+    n = model.__dict__.get("_status_calls", 0) + 1
+    model.__dict__["_status_calls"] = n
+    if not force and n % STATUS_EVERY:
         return
     import torch.distributed as tdist
     err = None
@@ -269,10 +282,12 @@ class AutoEncoder(AbstractModel):
         bwd [+ grad all-reduce] + Adam) with the loss left on the device."""
         if not self.training:
             self.train()
-        if self.dist is not None and self.dist.world > 1:
+        nat = self._native
+        # a step enters collectives whenever the executor holds a communicator
+        # (whatever model.dist says) or the torch exchange is attached
+        if getattr(nat, "_comm", None) is not None or (self.dist is not None and self.dist.world > 1):
             from .dist import assert_collective_context
             assert_collective_context("train_step_async with the data-parallel exchange attached")
-        nat = self._native
         seed = 0x9E3779B97F4A7C15 & ((1 << 63) - 1)
         if self.dist is None or self.dist.native:
             # single process, or data parallel with the native RCCL exchange

@@ -1,21 +1,25 @@
 """Data parallelism for the train step: one process per GPU, windows sharded by
-rows, weights/Adam state replicated, ONE exchange per step = sum all-reduce of
-the flat fp32 gradient buffer over RCCL (torch.distributed 'nccl' backend is
-RCCL on ROCm; xGMI between the GPUs of a node).  Sum, not mean: the reference
-loss is sum-reduced (model_builder.py:42), so the global gradient of the
-concatenated batch is the sum of the shard gradients.  BatchNorm statistics
-stay per shard (DDP semantics).  The grad buffer is one
-contiguous tensor.
+rows, BatchNorm statistics per shard (DDP semantics).  Sum, not
+mean: the reference loss is sum-reduced (model_builder.py:42), so the global
+gradient of the concatenated batch is the sum of the shard gradients.
 
 Two exchange paths:
-* native (GPU, 'nccl' process group): an RCCL communicator of our own
-  (mmad_comm_*, unique id broadcast over the torch process group) attached to
-  the executor; each layer's weight gradient is all-reduced on the executor's
-  comm stream as soon as its dW GEMM completes -- overlapped with the rest of
-  the backward -- then Adam-updated there; biases/gamma/beta + the loss follow
-  in one small bucket.  One host call per step, no host sync.
+* native (GPU, 'nccl' process group, the default): an RCCL communicator of our
+  own (mmad_comm_*, unique id broadcast over the torch process group) attached
+  to the executor.  The backward's weight gradients are grouped into buckets
+  of >= 8 MiB (consecutive layers, one contiguous range each); as soon as a
+  bucket's dW GEMMs complete, the comm stream REDUCE-SCATTERS its fp32
+  gradient, runs Adam on this rank's 1/N slice of p / m / v only (ZeRO-1:
+  optimizer state sharded, the bf16 weight shadow written for that slice), and
+  ALL-GATHERS the updated shadow -- overlapped with the rest of the backward.
+  Biases / gamma / beta + the loss follow in one small all-reduced bucket.  A
+  bucket the ranks do not divide into 16-B slices keeps all-reduce + full
+  Adam.  The fp32 master and m / v are then current only on their owner:
+  ``epoch_end`` all-gathers them (mmad_ae_dp_sync_master) before anything
+  reads the state_dict.  One host call per step, no host sync.
 * torch (gloo / fallback): train_fwd_bwd, then one torch.distributed
-  all-reduce of the flat gradient buffer, then the flat Adam.
+  all-reduce of the flat gradient buffer, then the flat Adam (weights and
+  Adam state replicated).
 
 Around the step (NoveltyDetecter under data parallelism): each
 rank trains on its rows of every global batch (data_loaders.BatchLoader with
@@ -138,35 +142,47 @@ class NativeComm:
         self.handle = h
 
     def self_test(self, n=4096):
-        """One sum all-reduce through the library's communicator on a fresh
-        stream-ordered buffer (rank r contributes r + 1), checked on the host:
-        a communicator that builds but cannot exchange fails here, before any
-        train step depends on it (the ranks then fall back together)."""
+        """Every collective the step uses, through the library's communicator,
+        on fresh stream-ordered buffers, checked on the host: sum all-reduce
+        (rank r contributes r + 1), in-place reduce-scatter (fp32) and
+        all-gather (fp32, bf16).  A communicator that builds but cannot
+        exchange fails here, before any train step depends on it.  Every rank
+        issues EVERY collective whatever an earlier check found (a rank that
+        stopped at its first failure would leave its peers blocked in the next
+        collective); the failures are raised only after the last one."""
         from . import _native
         from ._native import ptr, stream_ptr
-        buf = torch.full((n,), float(self.rank + 1), device="cuda", dtype=torch.float32)
-        _native.check(self._lib.mmad_allreduce_bucket(self.handle, ptr(buf), n, stream_ptr()),
-                      "mmad_allreduce_bucket")
+        errors = []
+
+        def issue(rc, what):
+            # a failed enqueue is recorded, not raised: the peers still issue theirs
+            if rc != 0:
+                errors.append(f"{what}: {_native.last_error()}")
+                return False
+            return True
+
         want = self.world * (self.world + 1) / 2.0
-        if not bool(torch.all(buf == want)):
-            raise RuntimeError(f"native all-reduce self-test: got {float(buf[0])}, want {want}")
-        # every collective the sharded step uses: reduce-scatter (fp32) and
-        # all-gather (fp32 and bf16), in place
-        n = 4096 * self.world
         buf = torch.full((n,), float(self.rank + 1), device="cuda", dtype=torch.float32)
-        _native.check(self._lib.mmad_reduce_scatter_bucket(self.handle, ptr(buf), n, stream_ptr()),
-                      "mmad_reduce_scatter_bucket")
-        shard = buf[self.rank * 4096:(self.rank + 1) * 4096]
-        if not bool(torch.all(shard == want)):
-            raise RuntimeError(f"native reduce-scatter self-test: got {float(shard[0])}, want {want}")
+        if issue(self._lib.mmad_allreduce_bucket(self.handle, ptr(buf), n, stream_ptr()),
+                 "mmad_allreduce_bucket") and not bool(torch.all(buf == want)):
+            errors.append(f"all-reduce: got {float(buf[0])}, want {want}")
+        m = 4096 * self.world
+        buf = torch.full((m,), float(self.rank + 1), device="cuda", dtype=torch.float32)
+        if issue(self._lib.mmad_reduce_scatter_bucket(self.handle, ptr(buf), m, stream_ptr()),
+                 "mmad_reduce_scatter_bucket"):
+            shard = buf[self.rank * 4096:(self.rank + 1) * 4096]
+            if not bool(torch.all(shard == want)):
+                errors.append(f"reduce-scatter: got {float(shard[0])}, want {want}")
         owners = torch.arange(self.world, device="cuda").repeat_interleave(4096).float() + 1.0
         for dt, code in ((torch.float32, _native.F32), (torch.bfloat16, _native.BF16)):
-            g = torch.zeros(n, device="cuda", dtype=dt)
+            g = torch.zeros(m, device="cuda", dtype=dt)
             g[self.rank * 4096:(self.rank + 1) * 4096] = float(self.rank + 1)
-            _native.check(self._lib.mmad_all_gather_bucket(self.handle, ptr(g), n, code, stream_ptr()),
-                          "mmad_all_gather_bucket")
-            if not bool(torch.all(g.float() == owners)):
-                raise RuntimeError(f"native all-gather self-test ({dt}) failed")
+            if issue(self._lib.mmad_all_gather_bucket(self.handle, ptr(g), m, code, stream_ptr()),
+                     f"mmad_all_gather_bucket({dt})") and not bool(torch.all(g.float() == owners)):
+                errors.append(f"all-gather ({dt}) failed")
+        torch.cuda.synchronize()
+        if errors:
+            raise RuntimeError("native RCCL self-test: " + "; ".join(errors))
 
     def close(self):
         if self.handle is not None and self.handle.value:
@@ -265,6 +281,8 @@ class DataParallel:
         if self.native:
             model._native.sync_master()
         self.average_running_stats(model)
+        from .auto_encoder import _check_status_all
+        _check_status_all(model, force=True)
 
     def average_running_stats(self, model):
         """BatchNorm running mean / var averaged over the ranks (SURVEY

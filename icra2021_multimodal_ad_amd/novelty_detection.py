@@ -176,6 +176,10 @@ class NoveltyDetecter:
             trainer.add_event_handler(Events.EPOCH_COMPLETED,
                                       lambda engine: model.dist.epoch_end(model))
         trainer.add_event_handler(Events.EPOCH_COMPLETED, run_validation, evaluator, valid_loader)
+        # every mini-batch's loss (the reference's step output), for trajectory checks
+        self.step_losses = []
+        trainer.add_event_handler(Events.ITERATION_COMPLETED,
+                                  lambda engine: self.step_losses.append(float(engine.state.output[0])))
 
         @trainer.on(Events.EPOCH_COMPLETED)
         def append_train_loss_history(engine):

@@ -390,13 +390,16 @@ int mmad_comm_create_loopback_ranks(mmad_comm** out, float scale, int nranks, in
 void mmad_comm_destroy(mmad_comm* c);
 /* in-place fp32 sum all-reduce of buf[n] on stream */
 int mmad_allreduce_bucket(mmad_comm* c, float* buf, int64_t n, void* stream);
-/* this communicator's rank / number of ranks (a loopback communicator: 0 / 1) */
+/* this communicator's rank / number of ranks (a loopback communicator: the
+ * rank / nranks given to its create call; 0 / 1 for mmad_comm_create_loopback) */
 int mmad_comm_rank(const mmad_comm* c);
 int mmad_comm_size(const mmad_comm* c);
 /* sharded exchange, in place (n divisible by the rank count): sum
  * reduce-scatter of fp32 buf[n] leaving rank r's sum in buf[r*n/N, (r+1)*n/N);
  * all-gather of every rank's shard of buf[n] (dtype MMAD_F32 or MMAD_BF16).
- * Loopback: the reduce-scatter is its all-reduce, the all-gather a no-op. */
+ * Loopback: the reduce-scatter scales only this rank's slice
+ * [r*n/N, (r+1)*n/N) by the loopback's scale (after the same short delay),
+ * the all-gather does nothing. */
 int mmad_reduce_scatter_bucket(mmad_comm* c, float* buf, int64_t n, void* stream);
 int mmad_all_gather_bucket(mmad_comm* c, void* buf, int64_t n, int dtype, void* stream);
 /* Attach (c != NULL) or detach a communicator.  With one attached,

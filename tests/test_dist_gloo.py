@@ -184,4 +184,7 @@ def test_rank_local_guard():
     mdist.assert_collective_context("outside again")
     import inspect
     from icra2021_multimodal_ad_amd.auto_encoder import AutoEncoder
-    assert "assert_collective_context" in inspect.getsource(AutoEncoder.train_step_async)
+    src = inspect.getsource(AutoEncoder.train_step_async)
+    # the guard follows the executor's communicator, not only model.dist
+    # (tests/test_gpu_dp.py::test_rank_local_guard_follows_the_attached_communicator)
+    assert "assert_collective_context" in src and "nat, \"_comm\"" in src

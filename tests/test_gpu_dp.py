@@ -231,7 +231,10 @@ def test_native_comm_self_test_passes_and_catches_a_broken_exchange():
     """dist.NativeComm.self_test (run before the native exchange is used, the
     ranks fall back to torch.distributed together if it fails): a one-rank
     RCCL communicator sums correctly; a loopback communicator that doubles
-    its buffer (a wrong exchange) is rejected."""
+    its buffer (a wrong exchange) is rejected -- after issuing every
+    collective of the test (the failure of the first check is reported
+    together with the later ones: a rank that stopped at its first failure
+    would leave its peers blocked in the next collective)."""
     import ctypes
     import types as _t
     from icra2021_multimodal_ad_amd import _native
@@ -249,8 +252,9 @@ def test_native_comm_self_test_passes_and_catches_a_broken_exchange():
     hb = ctypes.c_void_p()
     assert lib.mmad_comm_create_loopback(ctypes.byref(hb), 2.0) == 0
     bad = _t.SimpleNamespace(_lib=lib, handle=hb, rank=0, world=1)
-    with pytest.raises(RuntimeError, match="self-test"):
+    with pytest.raises(RuntimeError, match="self-test") as ei:
         NativeComm.self_test(bad)
+    assert "all-reduce" in str(ei.value) and "reduce-scatter" in str(ei.value), str(ei.value)
     lib.mmad_comm_destroy(hb)
 
 
@@ -335,5 +339,36 @@ def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank, mib):
         a.sync_master()                                        # loopback all-gather: a no-op
         assert not a.master_stale
         a.set_comm(None)
+    finally:
+        lib.mmad_comm_destroy(h)
+
+
+def test_rank_local_guard_follows_the_attached_communicator():
+    """A step whose executor still holds a communicator enters collectives
+    even when model.dist has been cleared (bench.py's rank-0 probe does
+    exactly that): inside dist.rank_local() it must raise, not run the
+    exchange on one rank; detached, the same call runs."""
+    import ctypes
+    import types as _t
+    from icra2021_multimodal_ad_amd import _native
+    from icra2021_multimodal_ad_amd import dist as mdist
+    from icra2021_multimodal_ad_amd.data import synth_windows
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    lib = _native.load()
+    h = ctypes.c_void_p()
+    assert lib.mmad_comm_create_loopback(ctypes.byref(h), 1.0) == 0
+    try:
+        m = get_model(_t.SimpleNamespace(input_size=256, btl_size=20, n_layers=5, gpu_id=0, dtype="bf16"))
+        x = torch.from_numpy(synth_windows(256, 256, seed=3)).cuda()
+        m._native.set_comm(_t.SimpleNamespace(handle=h))
+        assert m.dist is None
+        with mdist.rank_local():
+            with pytest.raises(RuntimeError, match="rank-local"):
+                m.train_step_async(x)
+        m._native.sync_master()
+        m._native.set_comm(None)
+        with mdist.rank_local():
+            m.train_step_async(x)                  # no exchange attached: allowed
+        torch.cuda.synchronize()
     finally:
         lib.mmad_comm_destroy(h)
