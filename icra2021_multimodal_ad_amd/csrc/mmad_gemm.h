@@ -2,10 +2,11 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-// split-K control block: per-launch arrival counters + flags use at most
-// 1920 words; this word records a combine that timed out (sticky until read
+// split-K control block: per-launch arrival counters + flags use fewer than
+// MMAD_SK_ERR_WORD words (mmad_gemm_splitk checks); this word records a combine that timed out (sticky until read
 // by mmad_gemm_status / mmad_ae_status)
-#define MMAD_SK_ERR_WORD 2047
+#define MMAD_SK_ERR_WORD 8191
+#define MMAD_SK_SLAB_TILES 832
 
 enum GemmEpiKind {
   GEMM_EPI_FWD = 0,         // y = BNaffine(act(acc + bias)); optional Welford partials

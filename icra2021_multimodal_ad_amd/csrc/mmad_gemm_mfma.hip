@@ -62,14 +62,24 @@ template <> struct Cfg<5> { static constexpr int BM = 128, BN = 128, WM = 2, WN 
 // 256x256, 8 waves (2 x 4, wave tile 128x64), a 2-slot ring: twice the
 // operand reuse of 256x128 (128 FLOP per staged byte), for the large-row
 // bf16 GEMMs of the forward / score / MSE epilogues without the fused BN
-// (C5 scoring at 65,536 rows; tools/ubench_gemm8.hip: 0.47-0.55 of peak at
+// (C5 scoring at 65,536 rows; a round-3 stand-alone loop study, since removed: 0.47-0.55 of peak at
 // 16384 x 2048 x 1664 vs 0.33 for 256x128); its epilogue staging fills LDS
 constexpr int CFG_BIG = 6;
 template <> struct Cfg<6> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NS = 2, NT = 512; };
-constexpr int NCFG = 7;
-constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256};
-constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256};
-constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512};
+// 64x64 dW tiles for the Adam-fused backward-weight GEMM at higher occupancy:
+// a 3-slot ring with <= 168 VGPRs (3 blocks per CU) and a 2-slot ring with
+// <= 128 (4 per CU), so the K loops of some blocks run beside the Adam
+// streams of others instead of the resident blocks alternating in step
+template <> struct Cfg<7> { static constexpr int BM = 64, BN = 64, WM = 2, WN = 2, NS = 3, NT = 256; };
+template <> struct Cfg<8> { static constexpr int BM = 64, BN = 64, WM = 2, WN = 2, NS = 2, NT = 256; };
+constexpr int NCFG = 9;
+constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256, 64, 64};
+constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256, 64, 64};
+constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512, 256, 256};
+// minimum resident blocks per CU the compiler must allow (launch bounds)
+template <int CFG> constexpr int cfg_minb() { return CFG == 7 ? 3 : CFG == 8 ? 4 : 1; }
+// the occupancy tiles exist for the dW epilogue only
+constexpr bool cfg_dw_only(int cfg) { return cfg == 7 || cfg == 8; }
 // the 256x256 tile: bf16 operands, forward-type epilogues, no fused BN
 template <typename T, int EPI>
 constexpr bool big_ok() {
@@ -252,7 +262,7 @@ __device__ __forceinline__ void read_sub(const char* sa, const char* sb, int ra,
 // two such groups with the next fragment reads between them
 // row_hook(i) runs after the MFMAs of fragment row i: the next stage's
 // LDS-DMA is spread over them (a burst of DMA issues right after the barrier
-// delays the MFMAs behind it; tools/ubench_gemm8.hip "di1": +10-12 %)
+// delays the MFMAs behind it: +10-12 % in the round-3 loop study, profiles/r03c_*)
 struct NoHook {
   __device__ __forceinline__ void operator()(int) const {}
 };
@@ -409,7 +419,9 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   // prefetched bias partials per lane (none for the 256x256 tile: its
   // 128 accumulator registers leave no room to hold them across the loop)
   constexpr int QB = BIG ? 0 : 8;
-  constexpr int QG = 32;                               // prefetched dW row-sum partials
+  // prefetched dW row-sum partials (none for the occupancy tiles 7 / 8: their
+  // register budget is the point; occupancy hides those loads instead)
+  constexpr int QG = cfg_dw_only(CFG) ? 0 : 32;
   constexpr int OSTRIDE = BN * (int)sizeof(TO) + 16;
   constexpr int OBYTES = BM * OSTRIDE + (EPI == GEMM_EPI_BWD_DATA ? BM * BN / 2 : 0);   // + fp64 [BM/16][BN]
   // fused train-mode BN: per-column merge results (2 x fp64 [BN]) + a flag word
@@ -513,7 +525,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       if (ep.bn_sync) bnp_g = ep.bn_gamma[bcc];
     }
   }
-  float e_g[QG];
+  float e_g[QG > 0 ? QG : 1];
   // db[n] (bias gradient of this layer's output n) is needed by the dW fix-up
   // (BN producer) and by the fused bias Adam (column-tile-0 blocks)
   const bool need_db = EPI == GEMM_EPI_BWD_WEIGHT && ep.gb_src &&
@@ -572,7 +584,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   // (not for the 8-wave 256x128 / 128x256 tiles: their 48 prefetch registers
   // spill beside the larger accumulator set)
   constexpr bool APF_OK = EPI == GEMM_EPI_BWD_WEIGHT && !BIG && CFG != 1 && CFG != 2 &&
-                          3 * NL + 3 * A_AG <= 63;
+                          !cfg_dw_only(CFG) && 3 * NL + 3 * A_AG <= 63;
   floatx4 pf_p[A_AG], pf_m[A_AG], pf_v[A_AG];
   bool pf = false;
   auto adam_prefetch = [&]() {
@@ -633,7 +645,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
     // sub-step are re-read row by row under the MFMAs that free them (their
     // lifetimes do not overlap, so the 128 accumulators fit beside them), and
     // stage t+2 is issued over the MFMA rows of stage t+1's first sub-step
-    // (tools/ubench_gemm8.hip "256x256 nb2 st0 di1")
+    // (the round-3 loop study's "256x256 nb2 st0 di1", profiles/r03d_*)
     if (nt > 0) {
       FR fa[2][TM], fb[2][TN];
       auto rd = [&](int t, int kk, int sl) {
@@ -1543,7 +1555,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
 }
 
 template <typename T, typename TO, bool AK, bool BK_, int CFG, int EPI>
-__global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __restrict__ A, int lda,
+__global__ __launch_bounds__(Cfg<CFG>::NT, cfg_minb<CFG>()) void mmad_gemm_kernel(const T* __restrict__ A, int lda,
                                                            const T* __restrict__ B, int ldb, int K,
                                                            GemmEpi ep) {
   gemm_body<T, TO, AK, BK_, CFG, EPI>(A, lda, B, ldb, K, ep, blockIdx.x, gridDim.x);
@@ -1555,6 +1567,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
 static bool cfg_fits(int cfg, int Mp, int Np, int epi, int dtype) {
   if (Mp % CFG_BM[cfg] || Np % CFG_BN[cfg]) return false;
   if (cfg == CFG_BIG && !big_ok_rt(dtype, epi)) return false;
+  if (cfg_dw_only(cfg) && epi != GEMM_EPI_BWD_WEIGHT) return false;
   // the score epilogue reduces rows over 128-column groups inside one tile
   if (epi == GEMM_EPI_SCORE && CFG_BN[cfg] < 128) return false;
   return true;
@@ -1611,6 +1624,16 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
     case 3: mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
     case 4: mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
     case 5: mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
+    case 7:
+    case 8:
+      if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
+        if (cfg == 7) mmad_gemm_kernel<T, TO, AK, BK_, 7, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep);
+        else mmad_gemm_kernel<T, TO, AK, BK_, 8, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep);
+      } else {
+        mmad_set_error("gemm: tile configuration %d is for the dW epilogue only", cfg);
+        return MMAD_EUNSUPPORTED;
+      }
+      break;
     default:
       if constexpr (big_ok<T, EPI>()) {
         mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep);
@@ -1634,6 +1657,8 @@ static const void* kernel_ptr(int cfg) {
     case 3: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI>;
     case 4: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI>;
     case 5: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI>;
+    case 7:
+    case 8: return nullptr;   // dW-only tiles: never a fused-BN candidate
     default:
       if constexpr (big_ok<T, EPI>()) return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI>;
       return nullptr;
@@ -1692,7 +1717,9 @@ bool mmad_gemm_bn_fusable(int dtype, int epi, int Mp, int Np) {
   if (epi != GEMM_EPI_FWD && epi != GEMM_EPI_BWD_DATA) return false;
   if (Mp % 128 || Np % 128 || Np / 64 > MMAD_BN_EXIT) return false;
   for (int c = 0; c < NCFG; ++c)
-    if (cfg_fits(c, Mp, Np, epi, dtype) && c != CFG_BIG && coresident(dtype, epi, c, Mp, Np)) return true;
+    if (cfg_fits(c, Mp, Np, epi, dtype) && c != CFG_BIG && !cfg_dw_only(c) &&
+        coresident(dtype, epi, c, Mp, Np))
+      return true;
   return false;
 }
 
@@ -1751,6 +1778,7 @@ static int tune_cfg(int dtype, int epi, const void* A, int lda, const void* B, i
   for (int c = 0; c < NCFG && rc == MMAD_OK; ++c) {
     if (!cfg_fits(c, Mp, Np, epi, dtype)) continue;
     if (c == CFG_BIG && (ep.bn_sync || ep.splitk > 1)) continue;   // no fused BN / split on 256x256
+    if (cfg_dw_only(c)) continue;   // picked by the Adam tile rule / knobs, not timed without Adam
     if (ep.bn_sync && !coresident(dtype, epi, c, Mp, Np)) continue;
     rc = launch_cfg(dtype, epi, A, lda, B, ldb, Mp, Np, K, et, c, s);   // warm
     if (rc != MMAD_OK) break;
@@ -1787,10 +1815,10 @@ int mmad_gemm_splitk(int Mp, int Np, int K, int dtype, int epi) {
   const int bk = dtype == MMAD_BF16 ? 64 : 32;            // K per stage
   const int t128 = (Mp / 128) * (Np / 128);              // 128x128 output tiles
   const int t64 = (Mp / 64) * (Np / 64);                 // 64x64 output tiles
-  // workspace bounds (mmad_gemm_splitk_bytes): S * t128 <= 320 slab tiles,
+  // workspace bounds (mmad_gemm_splitk_bytes): S * t128 <= MMAD_SK_SLAB_TILES slab tiles,
   // (1 + S) control words per tile of the smallest configuration
   auto ok = [&](int S) {
-    return K % (S * bk) == 0 && K / S >= 4 * bk && S * t128 <= 320 && t64 * (1 + S) < MMAD_SK_ERR_WORD;
+    return K % (S * bk) == 0 && K / S >= 4 * bk && S * t128 <= MMAD_SK_SLAB_TILES && t64 * (1 + S) < MMAD_SK_ERR_WORD;
   };
   auto valid = [](int S) { return S == 1 || S == 2 || S == 4 || S == 8 || S == 16; };
   const int env = mmad_splitk_override();
@@ -1819,13 +1847,14 @@ int mmad_gemm_splitk(int Mp, int Np, int K, int dtype, int epi) {
   return 1;
 }
 
-// shape-independent bound: S * Mp * Np <= 320 * 128 * 128 slab floats; per
-// launch (1 + S) control words per 64x64 tile <= 1920
+// shape-independent bound: S * Mp * Np <= MMAD_SK_SLAB_TILES * 128 * 128 slab
+// floats (832: split-K 4 of c2's largest forward / bwd-data GEMMs at 128x128);
+// per launch (1 + S) control words per 64x64 tile < MMAD_SK_ERR_WORD
 void mmad_gemm_splitk_bytes(int Mp, int Np, size_t* slab_bytes, size_t* ctl_bytes) {
   (void)Mp;
   (void)Np;
-  if (slab_bytes) *slab_bytes = (size_t)320 * 128 * 128 * 4;
-  if (ctl_bytes) *ctl_bytes = (size_t)2048 * 4;
+  if (slab_bytes) *slab_bytes = (size_t)MMAD_SK_SLAB_TILES * 128 * 128 * 4;
+  if (ctl_bytes) *ctl_bytes = (size_t)(MMAD_SK_ERR_WORD + 1) * 4;
 }
 
 int mmad_gemm_read_status(unsigned* ctl, hipStream_t s, const char* who) {

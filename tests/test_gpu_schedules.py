@@ -45,3 +45,34 @@ def test_schedule_knobs_match_default(knobs):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
     assert torch.equal(a.shadow, b.shadow)
     assert torch.equal(a.shadow, a.params[: a.n_weight].bfloat16())
+
+
+@pytest.mark.parametrize("tile", [0, 7, 8])
+def test_adam_fused_dw_tiles_match_default(tile):
+    """The Adam-fused dW GEMM on any of its tiles -- the default 64x64 (cfg 3,
+    2 blocks per CU), 128x128 (cfg 0) and the occupancy tiles (cfg 7: 3-slot
+    ring, 3 blocks per CU; cfg 8: 2-slot ring, 4 per CU) forced through knob 5
+    for every call -- gives the default schedule's bits: parameters, Adam
+    moments, BN statistics, the bf16 shadow and the losses."""
+    import types
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    cfg = types.SimpleNamespace(input_size=2048, btl_size=100, n_layers=5, gpu_id=0, dtype="bf16",
+                                models="ae")
+    torch.manual_seed(8)
+    ma = get_model(cfg)
+    mb = get_model(cfg)
+    mb.load_state_dict(ma.state_dict())
+    for m in (ma, mb):
+        m._native.sync_shadow(force=True)
+    for s in range(3):
+        x = torch.from_numpy(synth_windows(1024, 2048, seed=40 + s)).cuda()
+        la = float(ma._native.train_step_fused(x))
+        with _native.tune(tile_adam=tile):
+            lb = float(mb._native.train_step_fused(x))
+        assert la == lb, (s, la, lb)
+    for m in (ma, mb):
+        m._native.check_status()
+    a, b = ma._native, mb._native
+    for name in ("params", "exp_avg", "exp_avg_sq", "running"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert torch.equal(a.shadow, b.shadow)
