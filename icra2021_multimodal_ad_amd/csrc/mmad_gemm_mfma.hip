@@ -66,20 +66,10 @@ template <> struct Cfg<5> { static constexpr int BM = 128, BN = 128, WM = 2, WN 
 // 16384 x 2048 x 1664 vs 0.33 for 256x128); its epilogue staging fills LDS
 constexpr int CFG_BIG = 6;
 template <> struct Cfg<6> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NS = 2, NT = 512; };
-// 64x64 dW tiles for the Adam-fused backward-weight GEMM at higher occupancy:
-// a 3-slot ring with <= 168 VGPRs (3 blocks per CU) and a 2-slot ring with
-// <= 128 (4 per CU), so the K loops of some blocks run beside the Adam
-// streams of others instead of the resident blocks alternating in step
-template <> struct Cfg<7> { static constexpr int BM = 64, BN = 64, WM = 2, WN = 2, NS = 3, NT = 256; };
-template <> struct Cfg<8> { static constexpr int BM = 64, BN = 64, WM = 2, WN = 2, NS = 2, NT = 256; };
-constexpr int NCFG = 9;
-constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256, 64, 64};
-constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256, 64, 64};
-constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512, 256, 256};
-// minimum resident blocks per CU the compiler must allow (launch bounds)
-template <int CFG> constexpr int cfg_minb() { return CFG == 7 ? 3 : CFG == 8 ? 4 : 1; }
-// the occupancy tiles exist for the dW epilogue only
-constexpr bool cfg_dw_only(int cfg) { return cfg == 7 || cfg == 8; }
+constexpr int NCFG = 7;
+constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256};
+constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256};
+constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512};
 // the 256x256 tile: bf16 operands, forward-type epilogues, no fused BN
 template <typename T, int EPI>
 constexpr bool big_ok() {
@@ -419,9 +409,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   // prefetched bias partials per lane (none for the 256x256 tile: its
   // 128 accumulator registers leave no room to hold them across the loop)
   constexpr int QB = BIG ? 0 : 8;
-  // prefetched dW row-sum partials (none for the occupancy tiles 7 / 8: their
-  // register budget is the point; occupancy hides those loads instead)
-  constexpr int QG = cfg_dw_only(CFG) ? 0 : 32;
+  constexpr int QG = 32;                               // prefetched dW row-sum partials
   constexpr int OSTRIDE = BN * (int)sizeof(TO) + 16;
   constexpr int OBYTES = BM * OSTRIDE + (EPI == GEMM_EPI_BWD_DATA ? BM * BN / 2 : 0);   // + fp64 [BM/16][BN]
   // fused train-mode BN: per-column merge results (2 x fp64 [BN]) + a flag word
@@ -525,7 +513,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       if (ep.bn_sync) bnp_g = ep.bn_gamma[bcc];
     }
   }
-  float e_g[QG > 0 ? QG : 1];
+  float e_g[QG];
   // db[n] (bias gradient of this layer's output n) is needed by the dW fix-up
   // (BN producer) and by the fused bias Adam (column-tile-0 blocks)
   const bool need_db = EPI == GEMM_EPI_BWD_WEIGHT && ep.gb_src &&
@@ -584,7 +572,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   // (not for the 8-wave 256x128 / 128x256 tiles: their 48 prefetch registers
   // spill beside the larger accumulator set)
   constexpr bool APF_OK = EPI == GEMM_EPI_BWD_WEIGHT && !BIG && CFG != 1 && CFG != 2 &&
-                          !cfg_dw_only(CFG) && 3 * NL + 3 * A_AG <= 63;
+                          3 * NL + 3 * A_AG <= 63;
   floatx4 pf_p[A_AG], pf_m[A_AG], pf_v[A_AG];
   bool pf = false;
   auto adam_prefetch = [&]() {
@@ -1555,7 +1543,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
 }
 
 template <typename T, typename TO, bool AK, bool BK_, int CFG, int EPI>
-__global__ __launch_bounds__(Cfg<CFG>::NT, cfg_minb<CFG>()) void mmad_gemm_kernel(const T* __restrict__ A, int lda,
+__global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __restrict__ A, int lda,
                                                            const T* __restrict__ B, int ldb, int K,
                                                            GemmEpi ep) {
   gemm_body<T, TO, AK, BK_, CFG, EPI>(A, lda, B, ldb, K, ep, blockIdx.x, gridDim.x);
@@ -1567,7 +1555,6 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, cfg_minb<CFG>()) void mmad_gemm_kerne
 static bool cfg_fits(int cfg, int Mp, int Np, int epi, int dtype) {
   if (Mp % CFG_BM[cfg] || Np % CFG_BN[cfg]) return false;
   if (cfg == CFG_BIG && !big_ok_rt(dtype, epi)) return false;
-  if (cfg_dw_only(cfg) && epi != GEMM_EPI_BWD_WEIGHT) return false;
   // the score epilogue reduces rows over 128-column groups inside one tile
   if (epi == GEMM_EPI_SCORE && CFG_BN[cfg] < 128) return false;
   return true;
@@ -1624,16 +1611,6 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
     case 3: mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
     case 4: mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
     case 5: mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
-    case 7:
-    case 8:
-      if constexpr (EPI == GEMM_EPI_BWD_WEIGHT) {
-        if (cfg == 7) mmad_gemm_kernel<T, TO, AK, BK_, 7, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep);
-        else mmad_gemm_kernel<T, TO, AK, BK_, 8, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep);
-      } else {
-        mmad_set_error("gemm: tile configuration %d is for the dW epilogue only", cfg);
-        return MMAD_EUNSUPPORTED;
-      }
-      break;
     default:
       if constexpr (big_ok<T, EPI>()) {
         mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep);
@@ -1657,8 +1634,6 @@ static const void* kernel_ptr(int cfg) {
     case 3: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI>;
     case 4: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI>;
     case 5: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI>;
-    case 7:
-    case 8: return nullptr;   // dW-only tiles: never a fused-BN candidate
     default:
       if constexpr (big_ok<T, EPI>()) return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI>;
       return nullptr;
@@ -1717,9 +1692,7 @@ bool mmad_gemm_bn_fusable(int dtype, int epi, int Mp, int Np) {
   if (epi != GEMM_EPI_FWD && epi != GEMM_EPI_BWD_DATA) return false;
   if (Mp % 128 || Np % 128 || Np / 64 > MMAD_BN_EXIT) return false;
   for (int c = 0; c < NCFG; ++c)
-    if (cfg_fits(c, Mp, Np, epi, dtype) && c != CFG_BIG && !cfg_dw_only(c) &&
-        coresident(dtype, epi, c, Mp, Np))
-      return true;
+    if (cfg_fits(c, Mp, Np, epi, dtype) && c != CFG_BIG && coresident(dtype, epi, c, Mp, Np)) return true;
   return false;
 }
 
@@ -1778,7 +1751,6 @@ static int tune_cfg(int dtype, int epi, const void* A, int lda, const void* B, i
   for (int c = 0; c < NCFG && rc == MMAD_OK; ++c) {
     if (!cfg_fits(c, Mp, Np, epi, dtype)) continue;
     if (c == CFG_BIG && (ep.bn_sync || ep.splitk > 1)) continue;   // no fused BN / split on 256x256
-    if (cfg_dw_only(c)) continue;   // picked by the Adam tile rule / knobs, not timed without Adam
     if (ep.bn_sync && !coresident(dtype, epi, c, Mp, Np)) continue;
     rc = launch_cfg(dtype, epi, A, lda, B, ldb, Mp, Np, K, et, c, s);   // warm
     if (rc != MMAD_OK) break;

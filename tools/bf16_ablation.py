@@ -36,13 +36,11 @@ from sklearn import metrics as skm
 from icra2021_multimodal_ad_amd.common_utils import ae_widths, init_state_dict
 from icra2021_multimodal_ad_amd.data_loaders import get_loaders
 
-dev = torch.device("cuda", 0)
+dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
 torch.backends.cuda.matmul.allow_tf32 = False
 torch.backends.cudnn.allow_tf32 = False
 G = np.load("tests/golden/e2e.npz")
-seeds = [int(s) for s in (sys.argv[1] if len(sys.argv) > 1 else "0+1+2").split("+")]
-variants = (sys.argv[2] if len(sys.argv) > 2 else "fp32+act+dz+w+all").split("+")
-nap_epochs = [int(e) for e in (sys.argv[3] if len(sys.argv) > 3 else "6+12+18+24").split("+")]
+nap_epochs = [6, 12, 18, 24]
 
 
 def bf(x):
@@ -164,10 +162,11 @@ def nap_auroc(tr, te, lab):
     return auroc((st ** 2).mean(1).cpu().numpy(), lab)
 
 
-def run(seed, mode):
+def run(seed, mode, override=None):
     c = types.SimpleNamespace(**{k[5:]: G[k].item() for k in G.files
                                  if k.startswith("meta/") and k not in ("meta/torch", "meta/seeds",
                                                                         "meta/floor_threads")})
+    c.__dict__.update(override or {})
     c.gpu_id, c.dtype = 0, "f32"
     c.data_seed, c.sampler_seed, c.model_seed = 100 + seed, 200 + seed, 300 + seed
     enc, dec = ae_widths(c.input_size, c.btl_size, c.n_layers)
@@ -215,13 +214,23 @@ def run(seed, mode):
     return out
 
 
-summary = {}
-for s in seeds:
-    for v in variants:
-        o = run(s, v)
-        print(json.dumps(o), flush=True)
-        for k in ("base", "sap", "nap"):
-            summary.setdefault(v, {}).setdefault(k, []).append(o[f"{k}_mean_abs_delta_same_epoch"])
-for v, d in summary.items():
-    print(json.dumps({"variant": v, **{f"{k}_mean_abs_delta": float(np.mean(x)) for k, x in d.items()},
-                      "seeds": seeds}), flush=True)
+def main():
+    global nap_epochs
+    seeds = [int(s) for s in (sys.argv[1] if len(sys.argv) > 1 else "0+1+2").split("+")]
+    variants = (sys.argv[2] if len(sys.argv) > 2 else "fp32+act+dz+w+all").split("+")
+    if len(sys.argv) > 3:
+        nap_epochs = [int(e) for e in sys.argv[3].split("+")]
+    summary = {}
+    for s in seeds:
+        for v in variants:
+            o = run(s, v)
+            print(json.dumps(o), flush=True)
+            for k in ("base", "sap", "nap"):
+                summary.setdefault(v, {}).setdefault(k, []).append(o[f"{k}_mean_abs_delta_same_epoch"])
+    for v, d in summary.items():
+        print(json.dumps({"variant": v, **{f"{k}_mean_abs_delta": float(np.mean(x)) for k, x in d.items()},
+                          "seeds": seeds}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
