@@ -122,7 +122,8 @@ def test_nap_scoring_parity_on_reference_weights(wc):
     assert n_ranges >= 3, "the fixture must hold well-conditioned NAP ranges"
 
 
-def test_nap_end_to_end_training(wc):
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_nap_end_to_end_training(wc, dtype):
     """After training, NAP AUROC is a property of the trajectory as much as
     of the scorer: the reference's own 8- and 1-thread trainings of these
     models land 0.012 apart on average over the 36 (seed, range) pairs (90th
@@ -131,7 +132,10 @@ def test_nap_end_to_end_training(wc):
     same way) is held to that floor in aggregate: mean |ours - ref8| <= 2 x
     mean |ref1 - ref8| and the 90th percentile <= 2 x the floor's, over every
     seed and well-conditioned range; every value is recorded
-    (gpurun_out/nap_wc.json)."""
+    (gpurun_out/nap_wc.json).  bf16: the throughput path's training (bf16
+    activations, dz and weight shadow; NAP scored from the fp32 twin of the
+    master weights) under the same bars -- on these resolvable ranges the
+    bf16 trajectory must stay inside the reference's own fp32 floor too."""
     from icra2021_multimodal_ad_amd.data_loaders import get_loaders
     from icra2021_multimodal_ad_amd.common_utils import init_state_dict
     from icra2021_multimodal_ad_amd.model_builder import get_model
@@ -141,7 +145,7 @@ def test_nap_end_to_end_training(wc):
     ours_d, ref_d = [], []
     for seed in [int(s) for s in g["meta/seeds"]]:
         p = f"s{seed}/"
-        cfg = _cfg(g, seed)
+        cfg = _cfg(g, seed, dtype)
         model = get_model(cfg)
         sd0 = init_state_dict(cfg.input_size, cfg.btl_size, cfg.n_layers, seed=cfg.model_seed)
         model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd0.items()})
@@ -166,7 +170,7 @@ def test_nap_end_to_end_training(wc):
            "ref_floor_mean": float(np.mean(ref_d)), "ref_floor_p90": float(np.quantile(ref_d, 0.9)),
            "pairs": len(ours_d)}
     rec["aggregate"] = agg
-    _REC["end_to_end_training"] = rec
+    _REC[f"end_to_end_training_{dtype}"] = rec
     _record(_REC)
     print(f"\naggregate {agg}")
     assert agg["product_mean"] <= 2.0 * agg["ref_floor_mean"], agg

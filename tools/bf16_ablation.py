@@ -12,7 +12,8 @@ the product's bf16 step rounds:
   w   : the weight operand of every GEMM (the bf16 shadow of the fp32 master;
         gradients flow to the fp32 master, biases / gamma / beta stay fp32);
   all : the three together (= the product's bf16 path);
-  fp32: none (another fp32 implementation: the ablation's own floor).
+  fp32: none (another fp32 implementation: the ablation's own floor);
+  <v>_sr: variant v with stochastic instead of round-to-nearest rounding.
 
 Every variant trains the e2e configuration (tests/golden/e2e.npz meta: D=1728,
 btl 100, 24 epochs of 12 batches of 500) from the seed's initial weights on
@@ -22,6 +23,8 @@ fp32 SVD as utils/normalize.py does); each score is compared with the
 REFERENCE's AUROC at the same epoch (e2e.npz, 8-thread run).  Prints one JSON
 line per (seed, variant) and a summary per variant.
 Usage: python tools/bf16_ablation.py [seeds=0+1+2] [variants=fp32+act+dz+w+all] [nap_epochs=6+12+18+24]
+       python tools/bf16_ablation.py wc [seeds=0+1+2] [variants=fp32+act+w+all+all_sr]
+         (the well-conditioned NAP fixture, tests/golden/nap_wc.npz: NAP per resolvable layer range)
 """
 import json
 import sys
@@ -43,8 +46,17 @@ G = np.load("tests/golden/e2e.npz")
 nap_epochs = [6, 12, 18, 24]
 
 
+SR = {"on": False}
+
+
 def bf(x):
-    return x.bfloat16().float()
+    """fp32 -> bf16 -> fp32: round to nearest even, or (SR["on"]) stochastic
+    rounding: uniform random low 16 bits added before truncation."""
+    if not SR["on"]:
+        return x.bfloat16().float()
+    i = x.contiguous().view(torch.int32)
+    r = torch.randint(0, 1 << 16, i.shape, device=i.device, dtype=torch.int32)
+    return ((i + r) & ~0xFFFF).view(torch.float32)
 
 
 class RoundAct(torch.autograd.Function):
@@ -171,7 +183,10 @@ def run(seed, mode, override=None):
     c.data_seed, c.sampler_seed, c.model_seed = 100 + seed, 200 + seed, 300 + seed
     enc, dec = ae_widths(c.input_size, c.btl_size, c.n_layers)
     torch.manual_seed(0)
-    m = AE(enc, dec, set() if mode == "fp32" else ({"act", "dz", "w"} if mode == "all" else {mode})).to(dev)
+    SR["on"] = mode.endswith("_sr")
+    base_mode = mode[:-3] if SR["on"] else mode
+    m = AE(enc, dec, set() if base_mode == "fp32" else
+           ({"act", "dz", "w"} if base_mode == "all" else {base_mode})).to(dev)
     m.load_ref(init_state_dict(c.input_size, c.btl_size, c.n_layers, seed=c.model_seed))
     dset, trl, val, tel = get_loaders(c, device=dev)
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
@@ -214,8 +229,74 @@ def run(seed, mode, override=None):
     return out
 
 
+def run_wc(seed, mode):
+    """The well-conditioned NAP fixture (tests/golden/nap_wc.npz, D=256):
+    train the variant for the fixture's epochs from the seed's initial
+    weights, keep the best-on-valid state, and score NAP on every
+    well-conditioned layer range; |AUROC - reference (8 threads)| per range
+    next to the reference's own |ref1 - ref8|."""
+    W = np.load("tests/golden/nap_wc.npz")
+    skip = ("meta/torch", "meta/seeds", "meta/min_var_ratio")
+    c = types.SimpleNamespace(**{k[5:]: W[k].item() for k in W.files if k.startswith("meta/") and k not in skip})
+    c.gpu_id, c.dtype = 0, "f32"
+    c.data_seed, c.sampler_seed, c.model_seed = 500 + seed, 600 + seed, 700 + seed
+    enc, dec = ae_widths(c.input_size, c.btl_size, c.n_layers)
+    torch.manual_seed(0)
+    SR["on"] = mode.endswith("_sr")
+    base_mode = mode[:-3] if SR["on"] else mode
+    m = AE(enc, dec, set() if base_mode == "fp32" else
+           ({"act", "dz", "w"} if base_mode == "all" else {base_mode})).to(dev)
+    m.load_ref(init_state_dict(c.input_size, c.btl_size, c.n_layers, seed=c.model_seed))
+    dset, trl, val, tel = get_loaders(c, device=dev)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    st = trl.sampler.rng.bit_generator.state
+    tr_x, _ = dset.get_transformed_data(trl)
+    trl.sampler.rng.bit_generator.state = st
+    te_x, te_y = dset.get_transformed_data(tel)
+    lab = np.isin(np.asarray(te_y.cpu() if torch.is_tensor(te_y) else te_y), [c.target_class])
+    best, lowest = None, np.inf
+    for ep in range(1, c.n_epochs + 1):
+        m.train()
+        for x, _ in trl:
+            opt.zero_grad()
+            ((m(x, train_round=True) - x) ** 2).sum().backward()
+            opt.step()
+        m.eval()
+        with torch.no_grad():
+            vema = None
+            for x, _ in val:
+                lv = float(((m(x) - x) ** 2).sum())
+                vema = lv if vema is None else 0.98 * vema + 0.02 * lv
+        if vema < lowest:
+            lowest, best = vema, {k: v.clone() for k, v in m.state_dict().items()}
+    m.load_state_dict(best)
+    tr, te = diffs(m, tr_x, c.batch_size), diffs(m, te_x)
+    out, d, f = {"fixture": "nap_wc", "seed": seed, "variant": mode}, [], []
+    for s_, e_ in np.asarray(W[f"s{seed}/ranges"]).reshape(-1, 2):
+        a = nap_auroc(tr[s_:e_], te[s_:e_], lab)
+        r8 = float(W[f"s{seed}/nap_{s_}_{e_}/auroc"])
+        r1 = float(W[f"s{seed}/ref1/nap_{s_}_{e_}/auroc"])
+        d.append(abs(a - r8))
+        f.append(abs(r1 - r8))
+    out.update(nap_mean_abs_delta=float(np.mean(d)), nap_p90=float(np.quantile(d, 0.9)),
+               ref_floor_mean=float(np.mean(f)), ref_floor_p90=float(np.quantile(f, 0.9)))
+    return out
+
+
 def main():
     global nap_epochs
+    if len(sys.argv) > 1 and sys.argv[1] == "wc":
+        seeds = [int(s) for s in (sys.argv[2] if len(sys.argv) > 2 else "0+1+2").split("+")]
+        variants = (sys.argv[3] if len(sys.argv) > 3 else "fp32+act+w+all+all_sr").split("+")
+        agg = {}
+        for v in variants:
+            for s in seeds:
+                o = run_wc(s, v)
+                print(json.dumps(o), flush=True)
+                agg.setdefault(v, []).append(o["nap_mean_abs_delta"])
+            print(json.dumps({"fixture": "nap_wc", "variant": v, "nap_mean_abs_delta": float(np.mean(agg[v])),
+                              "seeds": seeds}), flush=True)
+        return
     seeds = [int(s) for s in (sys.argv[1] if len(sys.argv) > 1 else "0+1+2").split("+")]
     variants = (sys.argv[2] if len(sys.argv) > 2 else "fp32+act+dz+w+all").split("+")
     if len(sys.argv) > 3:
