@@ -36,6 +36,10 @@ import torch
 pytestmark = pytest.mark.gpu
 
 METHODS = ("base", "sap", "nap")
+# scored by every reference run at every epoch (NAP at each run's best epoch
+# only: its per-epoch SVDs would dominate the fixture's cost, and on this
+# model NAP is rounding-noise dominated -- see NAP_ILL_CONDITIONED_BAR)
+SAME_EPOCH = ("base", "sap")
 N_EARLY = 50          # steps of the early-trajectory check
 
 
@@ -248,8 +252,9 @@ def test_e2e_reported_auroc_vs_reference_ensemble(e2e):
 
 
 def test_e2e_training_parity_fp32(e2e):
-    """The product's AUROC at the epoch IT selects against the reference's
-    AUROC at that epoch (both reference-side numbers from its 8-thread run).
+    """The product's BASE / SAP AUROC at the epoch IT selects against the
+    reference's AUROC at that epoch (both reference-side numbers from its
+    8-thread run; NAP is compared as reported, in the ensemble test above).
 
     Two effects move any other fp32 implementation off the reference: the
     trajectory (at the same epoch the reference's own runs differ by the
@@ -276,7 +281,7 @@ def test_e2e_training_parity_fp32(e2e):
         row = {"best_epoch": e, "ref_best_epoch": int(g[p + "best_epoch"]),
                "ref_valid_at_ours_over_min": float(vref[e - 1] / vref.min()),
                "train_ema_max_rel_dev": th_dev, "valid_ema_max_rel_dev": vh_dev}
-        for m in METHODS:
+        for m in SAME_EPOCH:
             a = det.last_row[f"{m}_auroc"]
             r_e = float(g[p + f"epoch_auroc/{m}"][e - 1])
             deltas[m].append(abs(a - r_e))
@@ -285,17 +290,17 @@ def test_e2e_training_parity_fp32(e2e):
         print(f"\nseed {seed} fp32: best epoch {e} (ref {row['ref_best_epoch']}; ref valid there "
               f"{row['ref_valid_at_ours_over_min']:.4f} x min); loss EMA dev {th_dev:.2e}/{vh_dev:.2e}; "
               + "; ".join(f"{m} ours {row[m]['auroc']:.4f} ref@{e} {row[m]['ref_auroc_same_epoch']:.4f}"
-                          for m in METHODS))
+                          for m in SAME_EPOCH))
         assert e == int(np.argmin(np.asarray(vh))) + 1, (e, vh)    # selection logic
         assert row["ref_valid_at_ours_over_min"] <= 1.03, (seed, e, vref.tolist())
         assert th_dev < 0.05 and vh_dev < 0.05, (seed, th, vh)
-    for m in METHODS:
+    for m in SAME_EPOCH:
         fl = _epoch_floor(g, m)
         rec[m] = {"deltas_same_epoch": deltas[m], "mean_abs_delta": float(np.mean(deltas[m])),
                   "floor_mean": float(np.mean(fl)), "floor_p90": float(np.quantile(fl, 0.9)),
                   "floor_max": float(np.max(fl))}
     _record("fp32_training", rec)
-    for m in METHODS:
+    for m in SAME_EPOCH:
         fl = _epoch_floor(g, m)
         assert np.mean(deltas[m]) <= max(0.002, 2.0 * np.mean(fl)), (m, deltas[m], rec[m])
         assert np.max(deltas[m]) <= max(0.002, 3.0 * np.quantile(fl, 0.9)), (m, deltas[m], rec[m])
@@ -412,8 +417,11 @@ def test_e2e_bf16_scoring_and_training(e2e):
         e = int(det.best_epoch)
         epochs.append(e)
         for m in METHODS:
-            diffs[m].append(det.last_row[f"{m}_auroc"] - float(g[f"s{seed}/epoch_auroc/{m}"][e - 1]))
-    rec = {"what": "bf16-trained product AUROC - reference (8 threads) at the product's selected epoch",
+            # BASE / SAP at the product's epoch; NAP as reported (own best epoch each)
+            r = float(g[f"s{seed}/epoch_auroc/{m}"][e - 1]) if m in SAME_EPOCH else float(g[f"s{seed}/{m}/auroc"])
+            diffs[m].append(det.last_row[f"{m}_auroc"] - r)
+    rec = {"what": "bf16-trained product AUROC - reference (8 threads): BASE / SAP at the product's "
+                   "selected epoch, NAP as reported; floors: pairwise over the reference's 4 runs",
            "best_epochs": epochs, "seed0_fp32_model_scored": scoring16}
     for m in METHODS:
         fl = _epoch_floor(g, m)

@@ -198,7 +198,8 @@ def run(seed, mode, override=None):
     va_x, _ = dset.get_transformed_data(val)
     te_x, te_y = dset.get_transformed_data(tel)
     lab = np.isin(np.asarray(te_y.cpu() if torch.is_tensor(te_y) else te_y), [c.target_class])
-    ref = {k: np.asarray(G[f"s{seed}/epoch_auroc/{k}"]) for k in ("base", "sap", "nap")}
+    ref = {k: np.asarray(G[f"s{seed}/epoch_auroc/{k}"]) for k in ("base", "sap", "nap")
+           if f"s{seed}/epoch_auroc/{k}" in G.files}
     rows, best, lowest = [], None, np.inf
     for ep in range(1, c.n_epochs + 1):
         m.train()
@@ -216,7 +217,7 @@ def run(seed, mode, override=None):
         te = diffs(m, te_x)
         r = {"epoch": ep, "valid": vema, "base": auroc((te[0] ** 2).mean(1).cpu().numpy(), lab),
              "sap": auroc((torch.cat(te, 1) ** 2).mean(1).cpu().numpy(), lab)}
-        if ep in nap_epochs:
+        if ep in nap_epochs and "nap" in ref:
             r["nap"] = nap_auroc(diffs(m, tr_x, c.batch_size), te, lab)
         rows.append(r)
         if vema < lowest:
@@ -224,7 +225,7 @@ def run(seed, mode, override=None):
     out = {"seed": seed, "variant": mode, "best_epoch": best}
     for k in ("base", "sap", "nap"):
         d = [r[k] - ref[k][r["epoch"] - 1] for r in rows if k in r]
-        out[f"{k}_mean_abs_delta_same_epoch"] = float(np.mean(np.abs(d)))
+        out[f"{k}_mean_abs_delta_same_epoch"] = float(np.mean(np.abs(d))) if d else None
         out[f"{k}_deltas"] = [round(v, 5) for v in d]
     return out
 

@@ -7,6 +7,7 @@
 # Usage: bash tools/gpu_pmc_round.sh <tag> [c2 dW tile] [c3 dW tile]   (-2 = the production shape rule)
 set -o pipefail
 T=$1; W2=${2:--2}; W3=${3:--2}
+lab() { case $1 in 0) echo 128x128;; 3) echo 64x64;; 5) echo 128x128-4w;; *) echo "rule$1";; esac; }
 mkdir -p gpurun_out && export TMPDIR=/tmp
 pass() {   # pass <dir> <counters> <cmd...>
   local d=$1 c=$2; shift 2
@@ -27,8 +28,8 @@ done
 # copies back at most 64 MiB) and keep only the JSON summaries + pass logs
 python3 tools/pmc_traffic.py ${T}_c2e 1024 ae &&
   python3 tools/pmc_traffic.py ${T}_c3e 4096 vib_ae &&
-  python3 tools/pmc_dw.py ${T}_c2w 1024 1658 2048 0 ae 64x64 &&
-  python3 tools/pmc_dw.py ${T}_c3w 4096 1678 2048 0 vib_ae 128x128 &&
+  python3 tools/pmc_dw.py ${T}_c2w 1024 1658 2048 0 ae $(lab $W2) &&
+  python3 tools/pmc_dw.py ${T}_c3w 4096 1678 2048 0 vib_ae $(lab $W3) &&
   cp profiles/${T}_*pmc_*.json gpurun_out/
 rc=$?
 rm -rf gpurun_out/${T}_c2e_pmc_*/ gpurun_out/${T}_c3e_pmc_*/ gpurun_out/${T}_c2w_pmc_*/ gpurun_out/${T}_c3w_pmc_*/
