@@ -262,6 +262,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-probe", action="store_true", help="skip the in-situ kernel probe")
+    ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
+                    help="set a tune-table knob for the whole run (A/B of schedules; "
+                         "icra2021_multimodal_ad_amd._native.KNOB names)")
     return ap.parse_args(argv)
 
 
@@ -295,6 +298,9 @@ def run(args):
             raise SystemExit("c5 (scoring) is a one-GPU configuration")
         bench_score.run_c5(args)
         return
+    for kv in args.tune:
+        k, v = kv.split("=", 1)
+        _native.tune_set(k, int(v))
     cfgd = dict(CONFIGS[cname])
     for k in ("model", "dim", "batch"):
         if getattr(args, k) is not None:
@@ -377,6 +383,8 @@ def run(args):
         "host_enqueue_ms_per_step": round(t_host / args.steps * 1e3, 4),
         "final_loss": loss_v,
     }
+    if args.tune:
+        res["tune"] = args.tune
     # per-step spread: the same number of steps again, a HIP event after each
     # (on the caller's stream, which joins the side streams at every step end)
     evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]

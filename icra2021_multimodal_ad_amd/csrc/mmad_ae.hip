@@ -953,7 +953,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       // by then, instead of queueing behind the side stream's backlog
       const bool on_main = l < w.dw_main;
       if (on_main) {
-        dwe.tile_force = mmad_tile_adam_main_override() + 1;
+        dwe.tile_force = mmad_tile_adam_main_for(a.Np, a.Kp, Mp) + 1;
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st,
                        nullptr, PROBE_DW + l));
       } else if (ping) {

@@ -129,6 +129,7 @@ int mmad_splitk_dw_min_stages();   // dW split rule: minimum K stages per slice 
 int mmad_tile_adam_override();  // >= 0: tile of the Adam-fused dW GEMMs (-2: shape rule)
 int mmad_tile_adam_for(int Mp, int Np, int K);   // ... for a shape
 int mmad_tile_adam_main_override();  // >= 0: ... of those on the main stream
+int mmad_tile_adam_main_for(int Mp, int Np, int K);   // ... for a shape (-2: rule)
 int mmad_tile_epi_override(int epi);  // >= 0: tile of this epilogue's GEMMs
 
 // tile configuration a problem will run with (autotuned on first dispatch of
