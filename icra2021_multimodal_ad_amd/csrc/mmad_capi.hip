@@ -44,7 +44,7 @@ int g_knob[MMAD_KNOB_COUNT] = {
     -2,    // 5  tile of the Adam-fused dW GEMMs (-2 = shape rule, -1 = autotuned)
     -1,    // 6  tile of the bwd-data GEMMs
     -1,    // 7  tile of the forward GEMMs
-    -2,    // 8  tile of the main-stream Adam-fused dW GEMMs (-2 = rule, -1 = knob 5)
+    0,     // 8  tile of the main-stream Adam-fused dW GEMMs (-2 = rule, -1 = knob 5)
     0,     // 9  split-K override of the dW GEMMs
     0,     // 10 dW split rule: target 64x64-tile blocks (0 = no split)
     8,     // 11 dW split rule: minimum K stages per slice
@@ -92,13 +92,14 @@ int mmad_tile_adam_for(int Mp, int Np, int K) {
   return (K >= 2048 && (long)Mp * Np >= 1500000L) ? 0 : 3;
 }
 // tile of the Adam-fused dW GEMMs that run on the main stream at the end of
-// the backward (nothing else on the GPU then; -1 = same as knob 5).  Default
-// (-2) = a rule: 128x128 (cfg 0) when that grid still covers >= 200 of the
-// 256 CUs, otherwise knob 5's.  c2: layer 0 (1664x2048, 208 tiles) takes
-// 27.1 us on 128x128 vs 32.6 on 64x64 under rocprofv3, layer 1 (1280x1664,
-// 130 tiles) 28.3 vs 25.7 (profiles/r05q_prof_c2/, r04r_prof_c2/); the step
-// with both on 128x128: 0.4314-0.4326 vs 0.4335-0.4339 ms on two boxes
-// (profiles/r05h_main_tail_dw_tile_ab.txt).
+// the backward (nothing else on the GPU then; -1 = same as knob 5, -2 = a
+// rule: 128x128 where that grid covers >= 200 of the 256 CUs).  Default 0:
+// 128x128 for both (c2 layer 0, 208 tiles: 27.1 vs 32.6 us under rocprofv3;
+// layer 1, 130 tiles: 28.3 vs 25.7 -- yet the step is fastest with both on
+// 128x128: 0.4314 / 0.4321-0.4326 / 0.4351 vs 0.4335-0.4339 / 0.4372 ms with
+// the knob-5 tiles and 0.4372-0.4378 with the rule on three boxes,
+// profiles/r05h_main_tail_dw_tile_ab.txt, r05t_main_tail_dw_tile_ab.txt; at
+// 4096 rows knob 5's rule already picks 128x128 for these layers).
 int mmad_tile_adam_main_override() { return g_knob[8]; }
 int mmad_tile_adam_main_for(int Mp, int Np, int K) {
   if (g_knob[8] != -2) return g_knob[8];

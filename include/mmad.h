@@ -60,8 +60,9 @@ int mmad_pad_granule(void);
  *      split rule's target number of 64x64-tile blocks (0 = no split, default)
  *      and minimum K stages per slice (8)
  *   5  tile of the Adam-fused dW GEMMs (-2 shape rule, -1 autotuned); 8 = of
- *      those on the main stream at the end of the backward (-2 default:
- *      128x128 when its grid covers >= 200 CUs, else knob 5; -1 = knob 5);
+ *      those on the main stream at the end of the backward (default 0 =
+ *      128x128; -2 = 128x128 where its grid covers >= 200 CUs, else knob 5;
+ *      -1 = knob 5);
  *      6 / 7 = tile of the bwd-data / forward GEMMs (-1 autotuned)
  *   12-15 retired (EINVAL)
  *   16 train-mode BN schedule (-1 dtype default: bf16 fused, fp32 apply;

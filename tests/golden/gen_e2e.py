@@ -193,34 +193,52 @@ def run_reference(seed, per_epoch_nap=True, state_out=None):
 
 def run_oracle(seed):
     """The same training + scoring with the CPU oracle (oracle/ae_oracle.py, an
-    independent fp32 restatement pinned to the reference's goldens): how far
-    ANY independent fp32 implementation lands from the reference after
-    n_epochs of Adam (summation-order noise amplified by training)."""
+    independent numpy fp32 restatement pinned to the reference's goldens; its
+    GEMMs are OpenBLAS's, not oneDNN's): how far a FOREIGN fp32
+    implementation lands from the reference -- the reference's own thread
+    counts share most of their summation order (oneDNN partitions rows, not
+    the K loop), so they agree with each other more closely than any other
+    implementation can.  Keys ``oracle/...``: per-step losses, per-epoch BASE /
+    SAP AUROC, the best-on-valid epoch and its BASE / SAP / NAP AUROC (NAP fit
+    with an fp64 SVD)."""
     from oracle import ae_oracle as O
-    from oracle.model_io import model_from_state_dict
     cfg = config_for(seed)
+    from oracle.model_io import model_from_state_dict
     m = model_from_state_dict(init_state_dict(cfg.input_size, cfg.btl_size, cfg.n_layers,
                                               seed=cfg.model_seed))
     dset, train_loader, valid_loader, test_loader = get_loaders(cfg, device="cpu")
-    st, train_hist, lowest, best = {}, [], np.inf, None
+    rng_state = train_loader.sampler.rng.bit_generator.state
+    te_x, te_y = dset.get_transformed_data(test_loader)
+    lab = np.isin(np.asarray(te_y), [cfg.target_class])
+    train_loader.sampler.rng.bit_generator.state = rng_state
+    st, train_hist, valid_hist, steps, lowest, best, best_epoch = {}, [], [], [], np.inf, None, 0
+    ep_auc = {"base": [], "sap": []}
     for epoch in range(1, cfg.n_epochs + 1):
         ema = None
         for x, _ in train_loader:
-            ema = ema_update(ema, O.train_step(x.numpy(), m, st))
+            lv = float(O.train_step(x.numpy(), m, st))
+            steps.append(lv)
+            ema = ema_update(ema, lv)
         train_hist.append(ema)
         vema = None
         for x, _ in valid_loader:
             xh, _ = O.ae_forward(x.numpy(), m, train=False)
             vema = ema_update(vema, O.mse_sum(xh, x.numpy()))
+        valid_hist.append(vema)
+        te = O.get_diffs(te_x.numpy(), m)
+        ep_auc["base"].append(O.auroc(O.base_score(te), lab))
+        ep_auc["sap"].append(O.auroc(O.sap_score(te), lab))
         if vema < lowest:
-            lowest, best = vema, deepcopy(m)
+            lowest, best, best_epoch = vema, deepcopy(m), epoch
     tr_x, _ = dset.get_transformed_data(train_loader)
-    va_x, _ = dset.get_transformed_data(valid_loader)
-    te_x, te_y = dset.get_transformed_data(test_loader)
-    lab = np.isin(np.asarray(te_y), [cfg.target_class])
     tr = O.get_diffs(tr_x.numpy(), best, batch_size=cfg.batch_size)
     te = O.get_diffs(te_x.numpy(), best)
     out = {"oracle/train_history": np.asarray(train_hist, np.float64),
+           "oracle/valid_history": np.asarray(valid_hist, np.float64),
+           "oracle/step_loss": np.asarray(steps, np.float64),
+           "oracle/best_epoch": np.int64(best_epoch),
+           "oracle/epoch_auroc/base": np.asarray(ep_auc["base"], np.float64),
+           "oracle/epoch_auroc/sap": np.asarray(ep_auc["sap"], np.float64),
            "oracle/base/auroc": np.float64(O.auroc(O.base_score(te), lab)),
            "oracle/sap/auroc": np.float64(O.auroc(O.sap_score(te), lab))}
     fit = O.nap_fit(np.concatenate(tr, axis=1))
@@ -236,8 +254,18 @@ RUN_KEYS = ("base/auroc", "sap/auroc", "nap/auroc", "base/aupr", "sap/aupr", "na
 
 def run_job(seed, nthreads, part_dir):
     """One reference training run of one seed at one thread count -> a part
-    file (the 8-thread run keeps every output; the others RUN_KEYS)."""
+    file (the 8-thread run keeps every output; the others RUN_KEYS);
+    nthreads 0 = the CPU oracle's run (run_oracle, one thread)."""
     t0 = time.time()
+    if nthreads == 0:
+        torch.set_num_threads(1)
+        o = run_oracle(seed)
+        os.makedirs(part_dir, exist_ok=True)
+        np.savez(os.path.join(part_dir, f"seed{seed}_t0.npz"), **o)
+        print(f"seed {seed} oracle: {time.time() - t0:.0f} s, best epoch {int(o['oracle/best_epoch'])}, "
+              f"AUROC base {float(o['oracle/base/auroc']):.4f} sap {float(o['oracle/sap/auroc']):.4f} "
+              f"nap {float(o['oracle/nap/auroc']):.4f}", flush=True)
+        return
     torch.set_num_threads(nthreads)
     o = run_reference(seed, per_epoch_nap=False)
     if nthreads != 8:
@@ -255,7 +283,7 @@ def schedule(seeds, part_dir, budget=8):
     torch threads at once (oversubscribed BLAS threads spin and multiply the
     wall time), longest jobs first."""
     import subprocess
-    jobs = [(s, t) for t in (1, 2, 4, 8) for s in seeds
+    jobs = [(s, t) for t in (0, 1, 2, 4, 8) for s in seeds
             if not os.path.exists(os.path.join(part_dir, f"seed{s}_t{t}.npz"))]
     running = []
     os.makedirs(part_dir, exist_ok=True)
@@ -264,14 +292,14 @@ def schedule(seeds, part_dir, budget=8):
         used = sum(t for _, t in running)
         started = False
         for j in list(jobs):
-            if used + j[1] <= budget:
+            if used + max(1, j[1]) <= budget:
                 log = open(os.path.join(part_dir, f"log_s{j[0]}_t{j[1]}.txt"), "w")
                 p = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--job", str(j[0]),
                                       str(j[1]), part_dir], stdout=log, stderr=subprocess.STDOUT,
                                      env=dict(os.environ, PYTHONDONTWRITEBYTECODE="1",
-                                              OMP_NUM_THREADS=str(j[1])))
-                running.append((p, j[1]))
-                used += j[1]
+                                              OMP_NUM_THREADS=str(max(1, j[1]))))
+                running.append((p, max(1, j[1])))
+                used += max(1, j[1])
                 jobs.remove(j)
                 started = True
         if not started:

