@@ -421,7 +421,7 @@ def run(args):
                                    "ms_per_step": round(e1 / n1 * 1e3, 4), "steps": n1,
                                    "how": "same ranks, exchange off, after the timed region (max over ranks)"}
         model.dist = mdl_dist
-    durs, n_probe, probe_layers = [], 0, None
+    durs, n_probe, probe_layers, fwd_in_step = [], 0, None, []
     if not args.no_probe and rank == 0:
         # the dominant kernel is timed by the executor's probe on eager steps
         # of the same state and inputs right after the timed region (a HIP
@@ -440,7 +440,6 @@ def run(args):
         with mdist.rank_local():      # a step that still carried the exchange raises here
             for i in range(n_probe):
                 model.train_step_async(pool[i % len(pool)], opt)
-        model.dist = probe_dist
         torch.cuda.synchronize()
         buf = (ctypes.c_float * n_probe)()
         n = lib.mmad_ae_probe_read(nat._h, buf, n_probe)
@@ -449,6 +448,20 @@ def run(args):
         durs = list(buf[:n])
         mask = lib.mmad_ae_probe_layers(nat._h)
         probe_layers = [l for l in range(len(nat.layers)) if mask > 0 and (mask >> l) & 1] or [probe_layer]
+        # the encoder's first forward GEMM as it runs inside the step (train
+        # mode: its epilogue also finishes the layer's BatchNorm -- column
+        # barrier + y store -- when the fused schedule applies)
+        _native.check(lib.mmad_ae_probe(nat._h, 0, 0, n_probe), "mmad_ae_probe")
+        with mdist.rank_local():
+            for i in range(n_probe):
+                model.train_step_async(pool[i % len(pool)], opt)
+        model.dist = probe_dist
+        torch.cuda.synchronize()
+        fbuf = (ctypes.c_float * n_probe)()
+        nf = lib.mmad_ae_probe_read(nat._h, fbuf, n_probe)
+        if nf < 0:
+            _native.check(nf, "mmad_ae_probe_read")
+        fwd_in_step = list(fbuf[:nf])
         _native.check(lib.mmad_ae_probe(nat._h, 1, -1, 0), "mmad_ae_probe")
         nat.use_graph = graph_mode
         nat.check_status()
@@ -461,6 +474,15 @@ def run(args):
             res["roofline"] = dw_roofline(nat, probe_layer, durs, batch, n_probe, fused_adam=True,
                                           layers=probe_layers)
         res["roofline_encoder_gemm"] = gemm_roofline(model, batch)
+        if fwd_in_step:
+            import statistics
+            r = res["roofline_encoder_gemm"]
+            us = statistics.fmean(fwd_in_step) * 1e3
+            r["in_step_us"] = round(us, 2)
+            r["in_step_frac"] = round(r["flops_per_launch"] / (us * 1e-6) / 1e12 / r["peak"], 4)
+            r["in_step_timing"] = (f"executor probe: HIP event pair around the layer-0 forward GEMM inside "
+                                   f"{len(fwd_in_step)} eager train steps (its epilogue also finishes the "
+                                   f"layer's train-mode BatchNorm in the fused schedule)")
         if not args.no_cpu_baseline and world == 1:   # host baseline: rank 0 at N=1 only
             res["cpu_baseline"] = cpu_baseline(dim, batch, vib, budget_s=args.cpu_budget)
         print(json.dumps(res), flush=True)

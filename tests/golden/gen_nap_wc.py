@@ -6,6 +6,7 @@ Runs only in the build container (needs /root/reference); writes
 tests/golden/nap_wc.npz.  Usage:
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_nap_wc.py [--explore]
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_nap_wc.py --extend   # + 2/4-thread and oracle runs
 
 Why a second NAP fixture.  NAP (utils/metric.py:183-238,
 utils/normalize.py:20-103) rotates the train diffs onto their principal axes
@@ -145,10 +146,85 @@ def base_sap_reference(tr, va, te, lab):
     return (np.asarray(b[0], np.float32), float(b[1])), (np.asarray(sp[0], np.float32), float(sp[1]))
 
 
+def oracle_run(cfg):
+    """The same training + NAP scoring with the CPU oracle (oracle/ae_oracle.py,
+    numpy / OpenBLAS fp32, NAP fit with an fp64 SVD): a FOREIGN fp32
+    implementation -- the reference's thread counts share most of their
+    summation order.  Returns (best_epoch, base, sap, {(s, e): nap})."""
+    from copy import deepcopy
+    from oracle import ae_oracle as O
+    from oracle.model_io import model_from_state_dict
+    m = model_from_state_dict(init_state_dict(cfg.input_size, cfg.btl_size, cfg.n_layers, seed=cfg.model_seed))
+    dset, train_loader, valid_loader, test_loader = get_loaders(cfg, device="cpu")
+    st, lowest, best, best_epoch = {}, np.inf, None, 0
+    for epoch in range(1, cfg.n_epochs + 1):
+        for x, _ in train_loader:
+            O.train_step(x.numpy(), m, st)
+        vema = None
+        for x, _ in valid_loader:
+            xh, _ = O.ae_forward(x.numpy(), m, train=False)
+            vema = ema_update(vema, O.mse_sum(xh, x.numpy()))
+        if vema < lowest:
+            lowest, best, best_epoch = vema, deepcopy(m), epoch
+    tr_x, _ = dset.get_transformed_data(train_loader)
+    te_x, te_y = dset.get_transformed_data(test_loader)
+    lab = np.isin(np.asarray(te_y), [cfg.target_class])
+    tr = O.get_diffs(tr_x.numpy(), best, batch_size=cfg.batch_size)
+    te = O.get_diffs(te_x.numpy(), best)
+    naps = {}
+    for s_ in range(len(tr)):
+        for e_ in range(s_ + 1, len(tr) + 1):
+            fit = O.nap_fit(np.concatenate(tr[s_:e_], axis=1))
+            naps[(s_, e_)] = O.auroc(O.nap_score(np.concatenate(te[s_:e_], axis=1), fit), lab)
+    return best_epoch, O.auroc(O.base_score(te), lab), O.auroc(O.sap_score(te), lab), naps
+
+
+def extend(path):
+    """Add the reference's 2- and 4-thread runs and the CPU oracle's run to an
+    existing fixture (every key already there is kept as is): the ensemble
+    whose pairwise spread is the floor tests/test_gpu_nap_wc.py judges the
+    product's trained-model NAP by."""
+    with np.load(path) as z:
+        res = {k: z[k] for k in z.files}
+    for seed in [int(s) for s in res["meta/seeds"]]:
+        cfg = config_for(seed)
+        p = f"s{seed}/"
+        rngs = [tuple(int(v) for v in r) for r in np.asarray(res[p + "ranges"]).reshape(-1, 2)]
+        for nt in (2, 4):
+            mdl, _, be, vh, steps, loaders = train_reference(cfg, nt)
+            torch.set_num_threads(nt)
+            tr, va, te, lab = diffs_of(mdl, cfg, loaders)
+            q = p + f"ref{nt}/"
+            res[q + "best_epoch"] = np.int64(be)
+            res[q + "valid_history"] = vh
+            res[q + "step_loss"] = steps
+            (_, ba), (_, sa) = base_sap_reference(tr, va, te, lab)
+            res[q + "base/auroc"], res[q + "sap/auroc"] = np.float64(ba), np.float64(sa)
+            for s_, e_ in rngs:
+                res[q + f"nap_{s_}_{e_}/auroc"] = np.float64(nap_reference(tr, va, te, lab, cfg, s_, e_)[1])
+        be, ba, sa, naps = oracle_run(cfg)
+        q = p + "oracle/"
+        res[q + "best_epoch"] = np.int64(be)
+        res[q + "base/auroc"], res[q + "sap/auroc"] = np.float64(ba), np.float64(sa)
+        for s_, e_ in rngs:
+            res[q + f"nap_{s_}_{e_}/auroc"] = np.float64(naps[(s_, e_)])
+        print(f"seed {seed}: " + "; ".join(
+            f"[{s_},{e_}) " + " ".join(f"{float(res[p + k + f'nap_{s_}_{e_}/auroc']):.4f}"
+                                      for k in ("", "ref1/", "ref2/", "ref4/", "oracle/"))
+            for s_, e_ in rngs), flush=True)
+    res["meta/members"] = np.asarray(["", "ref1/", "ref2/", "ref4/", "oracle/"])
+    np.savez_compressed(path, **res)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--explore", action="store_true", help="print every layer range's conditioning")
+    ap.add_argument("--extend", action="store_true",
+                    help="add the 2- / 4-thread and oracle runs to the existing nap_wc.npz")
     a = ap.parse_args()
+    if a.extend:
+        extend(os.path.join(HERE, "nap_wc.npz"))
+        return
     res = {"meta/" + k: np.asarray(v) for k, v in NAPWC.items()}
     res["meta/torch"] = np.array(torch.__version__)
     res["meta/seeds"] = np.asarray(SEEDS, np.int64)

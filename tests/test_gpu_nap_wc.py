@@ -18,11 +18,10 @@ tests/test_gpu_e2e.py, NAP_ILL_CONDITIONED_BAR).
   of the reference's, its scores within 1e-3 relative; BASE / SAP within
   0.002 and 1e-4.
 * End to end: the product trains the same model from the same initial
-  weights on the same batches and is scored the same way; its NAP AUROC per
-  range is compared with the reference's (8 threads) next to the
-  reference's own 8-vs-1-thread distance (aggregate bars: the trained
-  model's NAP moves with the training trajectory, 0.012 between the
-  reference's own two runs)."""
+  weights on the same batches and is scored the same way (fp32 and bf16);
+  its NAP AUROC per range is judged against the ensemble of the reference's
+  runs at 8 / 1 / 2 / 4 threads and the CPU oracle's run (the trained
+  model's NAP moves with the training trajectory by ~0.01-0.02)."""
 import types
 
 import numpy as np
@@ -125,24 +124,26 @@ def test_nap_scoring_parity_on_reference_weights(wc):
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 def test_nap_end_to_end_training(wc, dtype):
     """After training, NAP AUROC is a property of the trajectory as much as
-    of the scorer: the reference's own 8- and 1-thread trainings of these
-    models land 0.012 apart on average over the 36 (seed, range) pairs (90th
-    percentile 0.03) although each scores its own weights exactly.  So the
-    product (trained from the same weights on the same batches, scored the
-    same way) is held to that floor in aggregate: mean |ours - ref8| <= 2 x
-    mean |ref1 - ref8| and the 90th percentile <= 2 x the floor's, over every
-    seed and well-conditioned range; every value is recorded
+    of the scorer: the ensemble -- the reference trained at 8 / 1 / 2 / 4
+    torch threads and the CPU oracle (a foreign numpy fp32 implementation) --
+    spreads by ~0.01-0.02 AUROC per (seed, range) although every member
+    scores its own weights exactly.  The product (trained from the same
+    weights on the same batches, scored the same way) is one more member:
+    T(j) = mean over (seed, range) and the other members of |NAP_j -
+    NAP_other|; bar T(product) <= 1.25 x max_j T(j), every value recorded
     (gpurun_out/nap_wc.json).  bf16: the throughput path's training (bf16
     activations, dz and weight shadow; NAP scored from the fp32 twin of the
-    master weights) under the same bars -- on these resolvable ranges the
-    bf16 trajectory must stay inside the reference's own fp32 floor too."""
+    master weights) under the same bar -- on these resolvable ranges the
+    bf16 trajectory must sit inside the fp32 ensemble too."""
     from icra2021_multimodal_ad_amd.data_loaders import get_loaders
     from icra2021_multimodal_ad_amd.common_utils import init_state_dict
     from icra2021_multimodal_ad_amd.model_builder import get_model
     from icra2021_multimodal_ad_amd.novelty_detection import NoveltyDetecter
     g = wc
-    rec = {}
-    ours_d, ref_d = [], []
+    members = [str(k) for k in g["meta/members"]] if "meta/members" in g.files else ["", "ref1/"]
+    names = [k.rstrip("/") or "ref8" for k in members]
+    rec = {"members": names}
+    prod, ens = [], []
     for seed in [int(s) for s in g["meta/seeds"]]:
         p = f"s{seed}/"
         cfg = _cfg(g, seed, dtype)
@@ -152,26 +153,27 @@ def test_nap_end_to_end_training(wc, dtype):
         loaders = get_loaders(cfg)
         det = NoveltyDetecter(cfg)
         det.train(model, loaders[1], loaders[2])
-        row = {"best_epoch": int(det.best_epoch), "ref_best_epoch": int(g[p + "best_epoch"]),
-               "ref1_best_epoch": int(g[p + "ref1/best_epoch"])}
+        row = {"best_epoch": int(det.best_epoch),
+               "member_best_epochs": {n: int(g[p + f"{k}best_epoch"]) for n, k in zip(names, members)}}
         for rg in _ranges(g, seed):
             s, e = rg
             d = _score(model, cfg, loaders, rg)
             ours = d.last_row["nap_auroc"]
-            r8 = float(g[p + f"nap_{s}_{e}/auroc"])
-            r1 = float(g[p + f"ref1/nap_{s}_{e}/auroc"])
-            ours_d.append(abs(ours - r8))
-            ref_d.append(abs(r1 - r8))
-            row[f"nap[{s},{e})"] = {"product": ours, "ref8": r8, "ref1": r1, "delta": ours - r8,
-                                    "ref_floor": abs(r8 - r1)}
-            print(f"\nseed {seed} trained NAP [{s},{e}): product {ours:.5f} ref8 {r8:.5f} ref1 {r1:.5f}")
+            mem = [float(g[p + f"{k}nap_{s}_{e}/auroc"]) for k in members]
+            prod.append(ours)
+            ens.append(mem)
+            row[f"nap[{s},{e})"] = {"product": ours, "members": dict(zip(names, mem))}
+            print(f"\nseed {seed} trained NAP [{s},{e}): product {ours:.5f} members "
+                  + " ".join(f"{v:.5f}" for v in mem))
         rec[seed] = row
-    agg = {"product_mean": float(np.mean(ours_d)), "product_p90": float(np.quantile(ours_d, 0.9)),
-           "ref_floor_mean": float(np.mean(ref_d)), "ref_floor_p90": float(np.quantile(ref_d, 0.9)),
-           "pairs": len(ours_d)}
+    ens = np.asarray(ens)
+    prod = np.asarray(prod)
+    t_mem = {n: float(np.mean(np.abs(ens[:, [i]] - np.delete(ens, i, axis=1)))) for i, n in enumerate(names)}
+    t_prod = float(np.mean(np.abs(prod[:, None] - ens)))
+    agg = {"T_product": t_prod, "T_members": t_mem, "bar": 1.25 * max(t_mem.values()),
+           "product_le_members_mean": t_prod <= float(np.mean(list(t_mem.values()))), "pairs": len(prod)}
     rec["aggregate"] = agg
     _REC[f"end_to_end_training_{dtype}"] = rec
     _record(_REC)
-    print(f"\naggregate {agg}")
-    assert agg["product_mean"] <= 2.0 * agg["ref_floor_mean"], agg
-    assert agg["product_p90"] <= 2.0 * agg["ref_floor_p90"], agg
+    print(f"\n{dtype} aggregate {agg}")
+    assert t_prod <= agg["bar"], agg
