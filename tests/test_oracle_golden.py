@@ -206,7 +206,7 @@ def test_nap_well_conditioned_ranges_match_reference(golden):
     worst = 0.0
     for seed in [int(s) for s in g["meta/seeds"]][:1]:
         p = f"s{seed}/"
-        skip = ("meta/torch", "meta/seeds", "meta/min_var_ratio")
+        skip = ("meta/torch", "meta/seeds", "meta/min_var_ratio", "meta/members")
         cfg = types.SimpleNamespace(**{k[5:]: g[k].item() for k in g.files
                                        if k.startswith("meta/") and k not in skip})
         cfg.gpu_id = -1

@@ -237,7 +237,7 @@ def run_wc(seed, mode):
     well-conditioned layer range; |AUROC - reference (8 threads)| per range
     next to the reference's own |ref1 - ref8|."""
     W = np.load("tests/golden/nap_wc.npz")
-    skip = ("meta/torch", "meta/seeds", "meta/min_var_ratio")
+    skip = ("meta/torch", "meta/seeds", "meta/min_var_ratio", "meta/members")
     c = types.SimpleNamespace(**{k[5:]: W[k].item() for k in W.files if k.startswith("meta/") and k not in skip})
     c.gpu_id, c.dtype = 0, "f32"
     c.data_seed, c.sampler_seed, c.model_seed = 500 + seed, 600 + seed, 700 + seed
