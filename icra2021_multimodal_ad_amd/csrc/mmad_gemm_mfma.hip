@@ -53,32 +53,23 @@ namespace {
 constexpr int MMAD_KB = 128;   // bytes of K per LDS row per stage
 
 template <int CFG> struct Cfg;
-template <> struct Cfg<0> { static constexpr int BM = 128, BN = 128, WM = 2, WN = 4, NS = 4, NT = 512, KB = MMAD_KB; };
-template <> struct Cfg<1> { static constexpr int BM = 256, BN = 128, WM = 4, WN = 2, NS = 3, NT = 512, KB = MMAD_KB; };
-template <> struct Cfg<2> { static constexpr int BM = 128, BN = 256, WM = 2, WN = 4, NS = 3, NT = 512, KB = MMAD_KB; };
-template <> struct Cfg<3> { static constexpr int BM = 64, BN = 64, WM = 2, WN = 2, NS = 4, NT = 256, KB = MMAD_KB; };
-template <> struct Cfg<4> { static constexpr int BM = 64, BN = 128, WM = 2, WN = 2, NS = 5, NT = 256, KB = MMAD_KB; };
-template <> struct Cfg<5> { static constexpr int BM = 128, BN = 128, WM = 2, WN = 2, NS = 4, NT = 256, KB = MMAD_KB; };
+template <> struct Cfg<0> { static constexpr int BM = 128, BN = 128, WM = 2, WN = 4, NS = 4, NT = 512; };
+template <> struct Cfg<1> { static constexpr int BM = 256, BN = 128, WM = 4, WN = 2, NS = 3, NT = 512; };
+template <> struct Cfg<2> { static constexpr int BM = 128, BN = 256, WM = 2, WN = 4, NS = 3, NT = 512; };
+template <> struct Cfg<3> { static constexpr int BM = 64, BN = 64, WM = 2, WN = 2, NS = 4, NT = 256; };
+template <> struct Cfg<4> { static constexpr int BM = 64, BN = 128, WM = 2, WN = 2, NS = 5, NT = 256; };
+template <> struct Cfg<5> { static constexpr int BM = 128, BN = 128, WM = 2, WN = 2, NS = 4, NT = 256; };
 // 256x256, 8 waves (2 x 4, wave tile 128x64), a 2-slot ring: twice the
 // operand reuse of 256x128 (128 FLOP per staged byte), for the large-row
 // bf16 GEMMs of the forward / score / MSE epilogues without the fused BN
 // (C5 scoring at 65,536 rows; a round-3 stand-alone loop study, since removed: 0.47-0.55 of peak at
 // 16384 x 2048 x 1664 vs 0.33 for 256x128); its epilogue staging fills LDS
 constexpr int CFG_BIG = 6;
-template <> struct Cfg<6> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NS = 2, NT = 512, KB = MMAD_KB; };
-// 32-deep ring (KB = 64 bytes of K per LDS row per stage): the same LDS in
-// twice as many, half-size slots, one barrier per 32-deep MFMA step, so NS-2
-// slots -- 2/3 to 3/4 of the ring instead of 1/3 to 1/2 -- stay in flight
-// across every barrier (bf16; forward-type and bwd-data epilogues)
-constexpr int CFG_R32 = 7;
-template <> struct Cfg<7> { static constexpr int BM = 256, BN = 128, WM = 4, WN = 2, NS = 6, NT = 512, KB = 64; };
-template <> struct Cfg<8> { static constexpr int BM = 128, BN = 256, WM = 2, WN = 4, NS = 6, NT = 512, KB = 64; };
-template <> struct Cfg<9> { static constexpr int BM = 128, BN = 128, WM = 2, WN = 4, NS = 8, NT = 512, KB = 64; };
-template <> struct Cfg<10> { static constexpr int BM = 64, BN = 64, WM = 2, WN = 2, NS = 8, NT = 256, KB = 64; };
-constexpr int NCFG = 11;
-constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256, 256, 128, 128, 64};
-constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256, 128, 256, 128, 64};
-constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512, 512, 512, 512, 256};
+template <> struct Cfg<6> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NS = 2, NT = 512; };
+constexpr int NCFG = 7;
+constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256};
+constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256};
+constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512};
 // the 256x256 tile: bf16 operands, forward-type epilogues, no fused BN
 template <typename T, int EPI>
 constexpr bool big_ok() {
@@ -87,18 +78,11 @@ constexpr bool big_ok() {
 inline bool big_ok_rt(int dtype, int epi) {
   return dtype == MMAD_BF16 && (epi == GEMM_EPI_FWD || epi == GEMM_EPI_MSE || epi == GEMM_EPI_SCORE);
 }
-// the 32-deep ring tiles: bf16, every epilogue but dW (its Adam prefetch
-// rides the 64-deep ring's tail)
-template <typename T, int EPI>
-constexpr bool r32_ok() {
-  return sizeof(T) == 2 && EPI != GEMM_EPI_BWD_WEIGHT;
-}
-inline bool r32_ok_rt(int dtype, int epi) { return dtype == MMAD_BF16 && epi != GEMM_EPI_BWD_WEIGHT; }
 
-template <typename T, bool KMAJ, int ROWS, int NT, int KB_ = MMAD_KB>
+template <typename T, bool KMAJ, int ROWS, int NT>
 struct Img {
   static constexpr int ES = sizeof(T);
-  static constexpr int KB = KB_;
+  static constexpr int KB = MMAD_KB;
   static constexpr int BK = KB / ES;                  // K per stage
   static constexpr int RB = KMAJ ? KB : ROWS * ES;    // bytes per LDS row
   static constexpr int BYTES = ROWS * KB;             // image bytes (both layouts)
@@ -108,8 +92,7 @@ struct Img {
 };
 
 // 16-byte-chunk XOR swizzle of LDS row `r` (an involution):
-//  * K-major, 128 B rows: (r>>1)&7; 64 B rows (the 32-deep ring): (r>>2)&3
-//    (rows r, r+4, r+8, r+12 of a 16-lane group share banks: 4 distinct chunks);
+//  * K-major, 128 B rows: (r>>1)&7;
 //  * MN-major bf16 (rows are k): one transposed read of a 32-lane half covers
 //    k rows {0..3, 8..11} (+4 for the second read) of a 32-deep step, 32 B of
 //    each; >= 256 B rows start every k row on bank 0, so the XOR takes
@@ -120,7 +103,7 @@ struct Img {
 template <typename T, bool KMAJ, int RB>
 __device__ __forceinline__ int swz(int r) {
   static_assert(KMAJ || RB >= (sizeof(T) == 2 ? 128 : 256), "MN-major row too short for its swizzle");
-  if constexpr (KMAJ) return RB == 64 ? (r >> 2) & 3 : (r >> 1) & 7;
+  if constexpr (KMAJ) return (r >> 1) & 7;
   else if constexpr (sizeof(T) == 2)
     return RB >= 256 ? (((r & 3) | (((r >> 3) & 1) << 2)) << 1)
                      : ((((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1);
@@ -144,10 +127,10 @@ __device__ __forceinline__ void dma16(const void* src, char* dst) {
 }
 
 // issue one stage of one operand: global -> LDS, 16 B per lane, no registers
-template <typename T, bool KMAJ, int ROWS, int NT, int KB = MMAD_KB>
+template <typename T, bool KMAJ, int ROWS, int NT>
 __device__ __forceinline__ void issue_stage(char* img, const T* __restrict__ G, int ld, int r0,
                                             int k0, int tid) {
-  using I = Img<T, KMAJ, ROWS, NT, KB>;
+  using I = Img<T, KMAJ, ROWS, NT>;
   constexpr int EPC = 16 / sizeof(T);
 #pragma unroll
   for (int i = 0; i < I::CHUNKS; ++i) {
@@ -161,10 +144,10 @@ __device__ __forceinline__ void issue_stage(char* img, const T* __restrict__ G, 
 }
 
 // chunk i (< Img::CHUNKS) of one stage of one operand (issue_stage = all i)
-template <typename T, bool KMAJ, int ROWS, int NT, int KB = MMAD_KB>
+template <typename T, bool KMAJ, int ROWS, int NT>
 __device__ __forceinline__ void issue_chunk(char* img, const T* __restrict__ G, int ld, int r0, int k0,
                                             int tid, int i) {
-  using I = Img<T, KMAJ, ROWS, NT, KB>;
+  using I = Img<T, KMAJ, ROWS, NT>;
   constexpr int EPC = 16 / sizeof(T);
   const int p = NT * i + tid;
   const int row = p / I::CPROW;
@@ -179,9 +162,9 @@ __device__ __forceinline__ void issue_chunk(char* img, const T* __restrict__ G, 
 // one ds_read_b128; MN-major: two ds_read_b64_tr_b16 of k rows 8g..8g+3 and
 // 8g+4..8g+7).  (NAT = false, the older permuted order {4g..4g+3} U
 // {16+4g..16+4g+3}, is kept for the K-major reader only.)
-template <bool KMAJ, bool NAT, int ROWS, int KB = MMAD_KB>
+template <bool KMAJ, bool NAT, int ROWS>
 __device__ __forceinline__ bf16x8 frag_bf16(const char* img, int rbase, int kk, int lane) {
-  using I = Img<bf16, KMAJ, ROWS, 256, KB>;   // RB only
+  using I = Img<bf16, KMAJ, ROWS, 256>;   // RB only
   const int g = lane >> 4;
   if constexpr (KMAJ) {
     const int m = rbase + (lane & 15);
@@ -249,18 +232,18 @@ template <typename T> struct SubFrag;
 template <> struct SubFrag<bf16> { using F = bf16x8; };
 template <> struct SubFrag<float> { using F = floatx4; };
 
-template <typename T, bool AK, bool BK_, bool NAT, int BM, int BN, int TM, int TN, int KB = MMAD_KB>
+template <typename T, bool AK, bool BK_, bool NAT, int BM, int BN, int TM, int TN>
 __device__ __forceinline__ void read_sub(const char* sa, const char* sb, int ra, int rb, int sub,
                                          int lane, typename SubFrag<T>::F (&fa)[TM],
                                          typename SubFrag<T>::F (&fb)[TN]) {
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    if constexpr (sizeof(T) == 2) fa[i] = frag_bf16<AK, NAT, BM, KB>(sa, ra + i * 16, sub, lane);
+    if constexpr (sizeof(T) == 2) fa[i] = frag_bf16<AK, NAT, BM>(sa, ra + i * 16, sub, lane);
     else fa[i] = frag_f32<AK, BM>(sa, ra + i * 16, sub, lane);
   }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    if constexpr (sizeof(T) == 2) fb[j] = frag_bf16<BK_, NAT, BN, KB>(sb, rb + j * 16, sub, lane);
+    if constexpr (sizeof(T) == 2) fb[j] = frag_bf16<BK_, NAT, BN>(sb, rb + j * 16, sub, lane);
     else fb[j] = frag_f32<BK_, BN>(sb, rb + j * 16, sub, lane);
   }
 }
@@ -314,18 +297,6 @@ __device__ __forceinline__ void wait_tail_x(int rem) {
   else if (rem == 2) wait_vmcnt<2 * NL + X>();
   else if (rem == 1) wait_vmcnt<NL + X>();
   else wait_vmcnt<X>();
-}
-
-// the same for up to R later stages (the 32-deep ring keeps NS-2 in flight)
-template <int NL, int R>
-__device__ __forceinline__ void wait_tail_n(int rem) {
-  if constexpr (R <= 0) {
-    wait_vmcnt<0>();
-  } else {
-    static_assert(R * NL <= 63, "vmcnt range");
-    if (rem >= R) wait_vmcnt<R * NL>();
-    else wait_tail_n<NL, R - 1>(rem);
-  }
 }
 
 __device__ __forceinline__ void block_barrier() {
@@ -421,14 +392,12 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
                                           int ldb, int K, const GemmEpi& ep, const int bid,
                                           const int nblk) {
   using C = Cfg<CFG>;
-  constexpr int BM = C::BM, BN = C::BN, WM = C::WM, WN = C::WN, NS = C::NS, NT = C::NT, KB = C::KB;
+  constexpr int BM = C::BM, BN = C::BN, WM = C::WM, WN = C::WN, NS = C::NS, NT = C::NT;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;   // 16x16 MFMA tiles per wave
   constexpr int NW = NT / 64;
   static_assert(WM * WN == NW && TM % 2 == 0, "wave grid");
-  constexpr bool R32 = KB != MMAD_KB;                   // the 32-deep ring
-  static_assert(!R32 || (KB == 64 && r32_ok<T, EPI>()), "32-deep ring: bf16, no dW epilogue");
-  using IA = Img<T, AK, BM, NT, KB>;
-  using IB = Img<T, BK_, BN, NT, KB>;
+  using IA = Img<T, AK, BM, NT>;
+  using IB = Img<T, BK_, BN, NT>;
   // bf16: every operand layout delivers the natural k order (lane group g owns
   // k = 8g..8g+7), so a K-major operand is one ds_read_b128 per fragment
   constexpr bool NAT = true;
@@ -573,15 +542,15 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   auto issue = [&](int s) {
     char* base = smem + (s % NS) * SLOT;
     const int k0 = kbase + s * IA::BK;
-    issue_stage<T, AK, BM, NT, KB>(base, A, lda, m0, k0, tid);
-    issue_stage<T, BK_, BN, NT, KB>(base + IA::BYTES, B, ldb, n0, k0, tid);
+    issue_stage<T, AK, BM, NT>(base, A, lda, m0, k0, tid);
+    issue_stage<T, BK_, BN, NT>(base + IA::BYTES, B, ldb, n0, k0, tid);
   };
   // chunk q (< NL) of stage s: A chunks first, then B
   auto issue_q = [&](int s, int q) {
     char* base = smem + (s % NS) * SLOT;
     const int k0 = kbase + s * IA::BK;
-    if (q < IA::CHUNKS) issue_chunk<T, AK, BM, NT, KB>(base, A, lda, m0, k0, tid, q);
-    else issue_chunk<T, BK_, BN, NT, KB>(base + IA::BYTES, B, ldb, n0, k0, tid, q - IA::CHUNKS);
+    if (q < IA::CHUNKS) issue_chunk<T, AK, BM, NT>(base, A, lda, m0, k0, tid, q);
+    else issue_chunk<T, BK_, BN, NT>(base + IA::BYTES, B, ldb, n0, k0, tid, q - IA::CHUNKS);
   };
 
   // ---- main loop: NS-slot LDS ring, all slots in flight; fragment registers
@@ -602,7 +571,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   constexpr int A_AG = A_ITERS < 4 ? A_ITERS : 4;
   // (not for the 8-wave 256x128 / 128x256 tiles: their 48 prefetch registers
   // spill beside the larger accumulator set)
-  constexpr bool APF_OK = EPI == GEMM_EPI_BWD_WEIGHT && !BIG && !R32 && CFG != 1 && CFG != 2 &&
+  constexpr bool APF_OK = EPI == GEMM_EPI_BWD_WEIGHT && !BIG && CFG != 1 && CFG != 2 &&
                           3 * NL + 3 * A_AG <= 63;
   floatx4 pf_p[A_AG], pf_m[A_AG], pf_v[A_AG];
   bool pf = false;
@@ -645,7 +614,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   // pattern) prefetched the same way, raw (converted only where used)
   constexpr int B_NG = NT / BN, B_PIECES = BM / 16;
   constexpr int B_PPT = (B_PIECES + B_NG - 1) / B_NG;
-  constexpr bool BPF_OK = EPI == GEMM_EPI_BWD_DATA && !BIG && !R32 && B_PIECES % B_NG == 0 && B_PPT <= 2 &&
+  constexpr bool BPF_OK = EPI == GEMM_EPI_BWD_DATA && !BIG && B_PIECES % B_NG == 0 && B_PPT <= 2 &&
                           3 * NL + 16 * B_PPT <= 63;
   TO pf_a[BPF_OK ? B_PPT : 1][16];
   bool pfa = false;
@@ -714,65 +683,6 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
           rd(t + 1, 0, 0);
         }
       }
-    }
-  } else if constexpr (R32) {
-    // 32-deep ring: one stage = one MFMA step.  Per stage u (fragments of u
-    // in registers): own reads of slot u done + stage u+1 landed (NS-2 later
-    // stages stay in flight); barrier; MFMAs of u with stage u+NS refilling
-    // slot u over their rows, the fragments of u+1 read between the halves.
-    // Fragment buffers alternate by the parity of u (no register copies).
-    if (nt > 0) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-        if (s < nt) issue(s);
-      if (nt >= NS) wait_vmcnt<(NS - 1) * NL>();
-      else wait_vmcnt<0>();
-      block_barrier();
-      FR f0a[TM], f0b[TN], f1a[TM], f1b[TN];
-      read_sub<T, AK, BK_, NAT, BM, BN, TM, TN, KB>(smem, smem + IA::BYTES, ra, rb, 0, lane, f0a, f0b);
-      auto sub = [&](int u, auto issue_c, auto last_c, auto& ca, auto& cb, auto& na, auto& nb) {
-        constexpr bool ISSUE = decltype(issue_c)::value, LAST = decltype(last_c)::value;
-        if constexpr (!LAST) {
-          if constexpr (ISSUE) wait_vmcnt<(NS - 2) * NL>();
-          else wait_tail_n<NL, NS - 2>(nt - u - 2);
-        }
-        wait_lgkm0();
-        if constexpr (!LAST) {
-          block_barrier();                   // stage u+1 visible; slot u free
-          MMAD_SB();
-        }
-        auto dma_row = [&](int i) {
-          if constexpr (ISSUE) {
-#pragma unroll
-            for (int q = 0; q < NL; ++q)
-              if (q * TM / NL == i) issue_q(u + NS, q);
-          }
-        };
-        mma_half<T, TM, TN, 0>(acc, ca, cb, dma_row);
-        MMAD_SB();
-        if constexpr (!LAST) {
-          const char* sn = smem + ((u + 1) % NS) * SLOT;
-          read_sub<T, AK, BK_, NAT, BM, BN, TM, TN, KB>(sn, sn + IA::BYTES, ra, rb, 0, lane, na, nb);
-        }
-        MMAD_SB();
-        mma_half<T, TM, TN, 1>(acc, ca, cb, dma_row);
-        MMAD_SB();
-      };
-      using T_ = std::true_type;
-      using F_ = std::false_type;
-      int u = 0;
-      auto run = [&](int u1, auto issue_c) {
-        if ((u & 1) && u < u1) sub(u++, issue_c, F_{}, f1a, f1b, f0a, f0b);
-        for (; u + 1 < u1; u += 2) {
-          sub(u, issue_c, F_{}, f0a, f0b, f1a, f1b);
-          sub(u + 1, issue_c, F_{}, f1a, f1b, f0a, f0b);
-        }
-        if (u < u1) sub(u++, issue_c, F_{}, f0a, f0b, f1a, f1b);
-      };
-      run(nt - NS, T_{});
-      run(nt - 1, F_{});
-      if (u & 1) sub(u, F_{}, T_{}, f1a, f1b, f0a, f0b);
-      else sub(u, F_{}, T_{}, f0a, f0b, f1a, f1b);
     }
   } else if (nt > 0) {
 #pragma unroll
@@ -1645,7 +1555,6 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
 static bool cfg_fits(int cfg, int Mp, int Np, int epi, int dtype) {
   if (Mp % CFG_BM[cfg] || Np % CFG_BN[cfg]) return false;
   if (cfg == CFG_BIG && !big_ok_rt(dtype, epi)) return false;
-  if (cfg >= CFG_R32 && !r32_ok_rt(dtype, epi)) return false;
   // the score epilogue reduces rows over 128-column groups inside one tile
   if (epi == GEMM_EPI_SCORE && CFG_BN[cfg] < 128) return false;
   return true;
@@ -1702,17 +1611,6 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
     case 3: mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
     case 4: mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
     case 5: mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep); break;
-    case 7: case 8: case 9: case 10:
-      if constexpr (r32_ok<T, EPI>()) {
-        if (cfg == 7) mmad_gemm_kernel<T, TO, AK, BK_, 7, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep);
-        if (cfg == 8) mmad_gemm_kernel<T, TO, AK, BK_, 8, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep);
-        if (cfg == 9) mmad_gemm_kernel<T, TO, AK, BK_, 9, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep);
-        if (cfg == 10) mmad_gemm_kernel<T, TO, AK, BK_, 10, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep);
-      } else {
-        mmad_set_error("gemm: tile configuration %d does not support this dtype / epilogue", cfg);
-        return MMAD_EUNSUPPORTED;
-      }
-      break;
     default:
       if constexpr (big_ok<T, EPI>()) {
         mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI><<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep);
@@ -1736,14 +1634,6 @@ static const void* kernel_ptr(int cfg) {
     case 3: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI>;
     case 4: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI>;
     case 5: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI>;
-    case 7: case 8: case 9: case 10:
-      if constexpr (r32_ok<T, EPI>()) {
-        if (cfg == 7) return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 7, EPI>;
-        if (cfg == 8) return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 8, EPI>;
-        if (cfg == 9) return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 9, EPI>;
-        return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 10, EPI>;
-      }
-      return nullptr;
     default:
       if constexpr (big_ok<T, EPI>()) return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI>;
       return nullptr;
@@ -1769,7 +1659,7 @@ std::map<long, int> g_occ;   // (device, dtype, epi, cfg) -> resident grid capac
 static int grid_capacity(int dtype, int epi, int cfg) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
-  const long key = (((long)dev * 4 + dtype) * 8 + epi) * 16 + cfg;
+  const long key = (((long)dev * 4 + dtype) * 8 + epi) * 8 + cfg;
   {
     std::lock_guard<std::mutex> lk(g_occ_mu);
     auto it = g_occ.find(key);

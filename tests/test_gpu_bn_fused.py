@@ -123,7 +123,7 @@ def test_fused_bn_deterministic_and_tile_independent(monkeypatch):
     lib = _native.load()
     outs = []
     try:
-        for tile in (-1, -1, 3, 4, 0, 9, 10):
+        for tile in (-1, -1, 3, 4, 0):
             lib.mmad_tune_set(0, tile)
             m, _ = _mk(monkeypatch, 2, 2048, 100, 5, sd, dtype="bf16")
             m._native.sync_shadow(force=True)

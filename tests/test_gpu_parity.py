@@ -322,15 +322,14 @@ def test_tile_configs_bit_identical(dtype):
     bit-identical gradients and BN statistics: the K accumulation order and all
     epilogue partial-sum orders are tile-independent, so the autotuner's pick
     can never change a result.  (A forced configuration that does not divide a
-    GEMM's output, or does not take its dtype / epilogue -- the 32-deep ring
-    tiles 7-10 are bf16 and not dW -- falls back to the tuned one for that GEMM.)"""
+    GEMM's output falls back to the tuned one for that GEMM.)"""
     from icra2021_multimodal_ad_amd import _native
     lib = _native.load()
     sd = init_state_dict(500, 40, 3, seed=17)
     x = torch.from_numpy(synth_windows(512, 500, seed=18)).cuda()
     ref = None
     try:
-        for cfg in (-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10):
+        for cfg in (-1, 0, 1, 2, 3, 4, 5, 6):
             lib.mmad_tune_set(0, cfg)
             m, _ = _model(500, 40, 3, sd, dtype=dtype)
             loss = float(m._native.train_step(x))
