@@ -300,13 +300,19 @@ class AutoEncoder(AbstractModel):
             if optimizer is not None:
                 self._mirror_optimizer_state(optimizer)
             return loss
+        # torch exchange: the backward records per-layer dW events so that each
+        # bucket's all-reduce + Adam starts while the lower layers still run
+        lr, betas, aeps = self._adam_hyper(optimizer)
+        if self.dist.overlap and not getattr(nat, "_dw_events", False):
+            nat.dw_events(True)
+            nat._dw_events = True
         loss = nat.train_step(x, k=self.k, eps=eps, seed=seed, offset=self._rng_offset,
                               beta_kl=self.beta_kl)
         self._rng_offset += 1
         self._count_bn_step()
-        self.dist.all_reduce_grads(nat.grads)
-        self.dist.all_reduce_loss(loss)
-        self._optimizer_step(optimizer)
+        self.dist.exchange_and_adam(nat, loss, lr, betas, aeps)
+        if optimizer is not None:
+            self._mirror_optimizer_state(optimizer)
         return loss
 
     @staticmethod
@@ -321,21 +327,6 @@ class AutoEncoder(AbstractModel):
                 raise NotImplementedError("native Adam: weight_decay/amsgrad/maximize unsupported")
             lr, betas, eps = float(grp["lr"]), tuple(grp["betas"]), float(grp["eps"])
         return lr, betas, eps
-
-    def _optimizer_step(self, optimizer):
-        nat = self._native
-        lr, betas, eps = 1e-3, (0.9, 0.999), 1e-8
-        if optimizer is not None:
-            if not isinstance(optimizer, torch.optim.Adam):
-                raise NotImplementedError("native step supports torch.optim.Adam "
-                                          "(novelty_detection.py:90)")
-            grp = optimizer.param_groups[0]
-            if grp.get("weight_decay", 0) or grp.get("amsgrad", False) or grp.get("maximize", False):
-                raise NotImplementedError("native Adam: weight_decay/amsgrad/maximize unsupported")
-            lr, betas, eps = float(grp["lr"]), tuple(grp["betas"]), float(grp["eps"])
-        nat.adam(lr=lr, betas=betas, eps=eps)
-        if optimizer is not None:
-            self._mirror_optimizer_state(optimizer)
 
     def _mirror_optimizer_state(self, optimizer):
         """Expose the native m/v as the torch optimizer's state (views)."""

@@ -89,6 +89,9 @@ struct mmad_ae {
   mmad_comm* comm = nullptr;
   hipStream_t cstream = nullptr;
   std::vector<hipEvent_t> ev_dw;
+  // torch-exchange data parallelism (mmad_ae_dw_events): the forward+backward
+  // without Adam records ev_dw[l] after dW_l and ev_data[l] after bwd-data of l
+  bool dw_events = false;
   hipEvent_t ev_small = nullptr, ev_cdone = nullptr;
   // fused step: dW GEMMs of layers < dw_main run on the caller's stream
   // (knob 19; tools/sched_sweep.py: 0.499 ms (2) vs 0.512 (1) vs 0.523 (3));
@@ -840,6 +843,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
       RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
                      nullptr, PROBE_DW + l));
+      if (h->dw_events) MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l], side));
     }
     if (l > 0) {
       const AeLayer& p = h->L[l - 1];
@@ -892,6 +896,8 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
                                   a.Np, ep, st));
       }
     }
+    // torch exchange: W_l is read for the last time by the bwd-data of l
+    if (!adam && h->dw_events && l > 0) MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
     if (dp && dp_loss && l == (nL > h->dp_small_at ? h->dp_small_at : 0)) {
       // the last bwd-data (l = 1, just enqueued) has produced every bias
       // partial and the loss partials are the forward's: reduce them on the
@@ -1182,8 +1188,10 @@ int mmad_ae_set_comm(mmad_ae* h, mmad_comm* c) {
     int least = 0, greatest = 0;
     MMAD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     MMAD_HIP_CHECK(hipStreamCreateWithPriority(&h->cstream, hipStreamNonBlocking, greatest));
-    h->ev_dw.resize(h->L.size());
-    for (auto& e : h->ev_dw) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, h->ev_flags_));
+    if (h->ev_dw.empty()) {
+      h->ev_dw.resize(h->L.size());
+      for (auto& e : h->ev_dw) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, h->ev_flags_));
+    }
     MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_small, h->ev_flags_));
     MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_cdone, h->ev_flags_));
   }
@@ -1192,6 +1200,38 @@ int mmad_ae_set_comm(mmad_ae* h, mmad_comm* c) {
 }
 
 int mmad_ae_dp_master_stale(const mmad_ae* h) { return h && h->master_stale ? 1 : 0; }
+
+int mmad_ae_dw_events(mmad_ae* h, int on) {
+  MMAD_CHECK_ARG(h && h->side, "ae_dw_events: bind the handle first");
+  if (on && h->ev_dw.empty()) {
+    h->ev_dw.resize(h->L.size());
+    for (auto& e : h->ev_dw) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, h->ev_flags_));
+  }
+  h->dw_events = on != 0;
+  return MMAD_OK;
+}
+
+int mmad_ae_wait_dw(mmad_ae* h, int layer, void* stream) {
+  MMAD_CHECK_ARG(h && h->dw_events, "ae_wait_dw: dW events are off (mmad_ae_dw_events)");
+  MMAD_CHECK_ARG(layer >= 0 && layer < (int)h->L.size(), "ae_wait_dw: bad layer %d", layer);
+  MMAD_HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream, h->ev_dw[layer], 0));
+  if (layer > 0) MMAD_HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream, h->ev_data[layer], 0));
+  return MMAD_OK;
+}
+
+int mmad_ae_dw_plan(const mmad_ae* h, int max_n, int64_t* off, int64_t* n, int* layer_lo) {
+  MMAD_CHECK_ARG(h && h->params, "ae_dw_plan: unbound handle");
+  std::vector<DpBucket> plan;
+  dp_plan(h, plan);
+  MMAD_CHECK_ARG(max_n >= (int)plan.size() && off && n && layer_lo,
+                 "ae_dw_plan: room for %d buckets needed", (int)plan.size());
+  for (size_t i = 0; i < plan.size(); ++i) {
+    off[i] = plan[i].off;
+    n[i] = plan[i].n;
+    layer_lo[i] = plan[i].l_lo;
+  }
+  return (int)plan.size();
+}
 
 int mmad_ae_dp_sync_master(mmad_ae* h, void* stream) {
   MMAD_CHECK_ARG(h && h->params && h->m && h->v, "ae_dp_sync_master: unbound handle");
@@ -1236,6 +1276,24 @@ int mmad_ae_adam(mmad_ae* h, float lr, float beta1, float beta2, float eps, int 
   return mmad_adam(h->n_params, h->params, h->grads, h->m, h->v, beta1, beta2, eps, ah.step_size,
                    ah.bc2_sqrt, h->dtype == MMAD_BF16 ? h->shadow : nullptr,
                    h->dtype == MMAD_BF16 ? h->n_weight : 0, stream);
+}
+
+int mmad_ae_adam_range(mmad_ae* h, float lr, float beta1, float beta2, float eps, int step,
+                       int64_t off, int64_t n, void* stream) {
+  MMAD_CHECK_ARG(h && h->params && h->grads && h->m && h->v, "ae_adam_range: unbound handle");
+  MMAD_CHECK_ARG(step >= 1, "ae_adam_range: step must be >= 1");
+  MMAD_CHECK_ARG(off >= 0 && n >= 0 && off + n <= h->n_params && off % 4 == 0,
+                 "ae_adam_range: bad range [%lld, +%lld)", (long long)off, (long long)n);
+  const AdamHyper ah = adam_hyper(lr, beta1, beta2, eps, step);
+  // the bf16 shadow covers the weights [0, n_weight)
+  void* sh = nullptr;
+  int64_t nsh = 0;
+  if (h->dtype == MMAD_BF16 && off < h->n_weight) {
+    sh = (char*)h->shadow + off * 2;
+    nsh = h->n_weight - off < n ? h->n_weight - off : n;
+  }
+  return mmad_adam(n, h->params + off, h->grads + off, h->m + off, h->v + off, beta1, beta2, eps,
+                   ah.step_size, ah.bc2_sqrt, sh, nsh, stream);
 }
 
 int mmad_ae_forward(mmad_ae* h, const float* x, int ld_x, int B, int train_bn, float* x_hat,

@@ -17,9 +17,11 @@ Two exchange paths:
   Adam.  The fp32 master and m / v are then current only on their owner:
   ``epoch_end`` all-gathers them (mmad_ae_dp_sync_master) before anything
   reads the state_dict.  One host call per step, no host sync.
-* torch (gloo / fallback): train_fwd_bwd, then one torch.distributed
-  all-reduce of the flat gradient buffer, then the flat Adam (weights and
-  Adam state replicated).
+* torch (gloo / fallback): train_fwd_bwd with per-layer dW events; each
+  weight bucket (the native plan) is all-reduced through torch.distributed on
+  its own stream as soon as its dW GEMMs are done and Adam-updated there
+  (mmad_ae_adam_range), overlapping the rest of the backward; the small bucket
+  and the loss follow the backward.  Weights and Adam state replicated.
 
 Around the step (NoveltyDetecter under data parallelism): each
 rank trains on its rows of every global batch (data_loaders.BatchLoader with
@@ -259,9 +261,60 @@ class DataParallel:
     def native(self):
         return self.comm is not None
 
+    # torch exchange: overlapped per bucket (False: the serial form -- one flat
+    # all-reduce after the backward, then the flat Adam; same bits at 2 ranks)
+    overlap = True
+
     def all_reduce_grads(self, flat_grads):
         if self.world > 1:
             dist.all_reduce(flat_grads, op=dist.ReduceOp.SUM, group=self.group)
+
+    def exchange_and_adam(self, nat, loss, lr, betas, eps):
+        """The torch exchange of one data-parallel step, after nat.train_step
+        was enqueued on the current stream: sum all-reduce of every gradient
+        and of the loss, then Adam (one step count for every range).
+        Overlapped: bucket b's all-reduce is issued on stream b, which first
+        waits for the bucket's dW GEMMs and for the bwd-data GEMM of its lowest
+        layer (the last reader of those weights: mmad_ae_wait_dw); Adam of the
+        bucket follows on the same stream once its collective is done; the
+        small bucket [bias | gamma | beta] and the loss are reduced after the
+        backward; the current stream joins every bucket stream.  Adam is
+        elementwise and a 2-rank sum is order-free, so at 2 ranks this is the
+        serial form's result bit for bit (tests/test_gpu_dp.py)."""
+        nat.adam_step_count += 1
+        step = nat.adam_step_count
+        if not self.overlap:
+            self.all_reduce_grads(nat.grads)
+            self.all_reduce_loss(loss)
+            nat.adam(lr=lr, betas=betas, eps=eps, step=step)
+            return
+        cur = torch.cuda.current_stream()
+        plan = getattr(nat, "_dw_plan", None)
+        if plan is None:
+            plan = nat._dw_plan = nat.dw_plan()
+        streams = getattr(nat, "_dw_streams", None)
+        if streams is None or len(streams) < len(plan):
+            streams = nat._dw_streams = [torch.cuda.Stream(device=nat.device) for _ in plan]
+        pending = []
+        for (off, n, lo), s in zip(plan, streams):
+            nat.wait_dw(lo, s)
+            with torch.cuda.stream(s):
+                work = dist.all_reduce(nat.grads[off:off + n], op=dist.ReduceOp.SUM, group=self.group,
+                                       async_op=True)
+            pending.append((work, s, off, n))
+        small = nat.grads[nat.n_weight:]
+        w_small = dist.all_reduce(small, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        w_loss = dist.all_reduce(loss, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        for work, s, off, n in pending:
+            with torch.cuda.stream(s):
+                work.wait()
+                nat.adam_range(off, n, lr=lr, betas=betas, eps=eps, step=step)
+        w_small.wait()
+        w_loss.wait()
+        nat.adam_range(nat.n_weight, nat.n_params - nat.n_weight, lr=lr, betas=betas, eps=eps, step=step)
+        for _, s, _, _ in pending:
+            cur.wait_stream(s)
+        nat._mark_synced()
 
     def all_reduce_loss(self, loss):
         if self.world > 1:

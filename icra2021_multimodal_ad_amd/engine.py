@@ -294,6 +294,29 @@ class NativeAE:
              int(step), stream_ptr())
         self._mark_synced()
 
+    def adam_range(self, off, n, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, step=1):
+        """Adam on the parameter range [off, off + n) (mmad_ae_adam_range) on
+        the current stream; the caller counts the step."""
+        call("mmad_ae_adam_range", self._h, float(lr), float(betas[0]), float(betas[1]), float(eps),
+             int(step), int(off), int(n), stream_ptr())
+
+    def dw_events(self, on=True):
+        call("mmad_ae_dw_events", self._h, int(bool(on)))
+
+    def wait_dw(self, layer, stream):
+        """`stream` waits for the last train_step's dW GEMM of `layer` and its
+        bwd-data GEMM (needs dw_events(True) before that step)."""
+        call("mmad_ae_wait_dw", self._h, int(layer), stream_ptr(stream))
+
+    def dw_plan(self):
+        """Weight buckets in backward order: [(offset, length, lowest layer)]."""
+        cap = len(self.enc_widths) + len(self.dec_widths)
+        off, n, lo = (ctypes.c_int64 * cap)(), (ctypes.c_int64 * cap)(), (ctypes.c_int * cap)()
+        cnt = _native.load().mmad_ae_dw_plan(self._h, cap, off, n, lo)
+        if cnt < 0:
+            _native.check(cnt, "mmad_ae_dw_plan")
+        return [(int(off[i]), int(n[i]), int(lo[i])) for i in range(cnt)]
+
     def forward(self, x, train_bn=False, want_xhat=True, want_loss=False):
         self._require(x)
         x = self._as_input(x, self.enc_widths[0])

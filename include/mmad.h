@@ -426,6 +426,24 @@ int mmad_ae_dp_master_stale(const mmad_ae* h);
 /* optimizer.step() (models/auto_encoder.py:75) on the bound buffers. */
 int mmad_ae_adam(mmad_ae* h, float lr, float beta1, float beta2, float eps, int step,
                  void* stream);
+/* The same on the parameter range [off, off + n) of the flat buffers (off a
+ * multiple of 4; the bf16 shadow is written where the range covers weights):
+ * Adam is elementwise, so the ranges of a partition give mmad_ae_adam's bits.
+ * Used by the torch-exchange data-parallel step, one range per bucket. */
+int mmad_ae_adam_range(mmad_ae* h, float lr, float beta1, float beta2, float eps, int step,
+                       int64_t off, int64_t n, void* stream);
+/* Torch-exchange data parallelism (no counterpart; the path taken when the
+ * native communicator is not attached): with dW events on, every
+ * mmad_ae_train_fwd_bwd records one event after each layer's dW GEMM and one
+ * after its bwd-data GEMM (the last reader of its weights);
+ * mmad_ae_wait_dw makes `stream` wait for both, so a caller can all-reduce and
+ * Adam-update a bucket while the rest of the backward runs.  mmad_ae_dw_plan
+ * writes the weight buckets in backward order (the native exchange's plan,
+ * knob 30): offset and length in the flat gradient buffer and the bucket's
+ * lowest layer (the one to wait for); returns their count (< 0: error). */
+int mmad_ae_dw_events(mmad_ae* h, int on);
+int mmad_ae_wait_dw(mmad_ae* h, int layer, void* stream);
+int mmad_ae_dw_plan(const mmad_ae* h, int max_n, int64_t* off, int64_t* n, int* layer_lo);
 
 /* AutoEncoder.forward (models/auto_encoder.py:46-50): x_hat fp32 [B][ld_out].
  * train_bn != 0: batch-stat BN + running-stat update (module.train()).

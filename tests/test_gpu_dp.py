@@ -53,6 +53,69 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
+def _xworker(rank, world, port, out, overlap, dtype, mib):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    import torch.distributed as dist
+    from icra2021_multimodal_ad_amd import _native
+    from icra2021_multimodal_ad_amd import dist as mdist
+    from icra2021_multimodal_ad_amd.common_utils import init_state_dict
+    from icra2021_multimodal_ad_amd.data import synth_windows
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    mdist.init_from_env(backend="gloo")
+    torch.cuda.set_device(0)
+    cfg = _cfg()
+    cfg.dtype = dtype
+    with _native.tune(dp_bucket_mib=mib):
+        m = get_model(cfg)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in
+                       init_state_dict(192, 16, 5, seed=51).items()})
+    mdist.attach_data_parallel(m)
+    m.dist.overlap = overlap
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    losses = []
+    for s in range(3):
+        x = torch.from_numpy(synth_windows(96, 192, seed=60 + 10 * s + rank)).cuda()
+        losses.append(float(m.train_step_async(x, opt)))
+    torch.cuda.synchronize()
+    nat = m._native
+    out[rank] = (nat.params.cpu().numpy(), nat.exp_avg.cpu().numpy(), nat.exp_avg_sq.cpu().numpy(),
+                 nat.shadow.float().cpu().numpy() if nat.shadow is not None else None, losses,
+                 len(nat.dw_plan()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dtype,mib", [("f32", 0), ("bf16", 0), ("bf16", 8)])
+def test_torch_exchange_overlapped_equals_serial(dtype, mib):
+    """The torch exchange (the path without the native communicator):
+    per-bucket all-reduce + Adam on bucket streams gated by the executor's dW
+    events (DataParallel.overlap, the default) gives the serial form's bits
+    -- one flat all-reduce after the backward, then the flat Adam -- over 3
+    steps at 2 ranks (a 2-operand sum is order-free, Adam elementwise):
+    parameters, Adam moments and the bf16 shadow (losses to 1e-6: tile-
+    dependent partial order).  mib = 0: one
+    bucket per layer (10 buckets); 8: the default plan (one bucket here)."""
+    world = 2
+    res = {}
+    for overlap in (False, True):
+        mgr = mp.get_context("spawn").Manager()
+        out = mgr.dict()
+        mp.start_processes(_xworker, args=(world, _free_port(), out, overlap, dtype, mib), nprocs=world,
+                           join=True, start_method="spawn")
+        res[overlap] = dict(out)
+    for rank in range(world):
+        a, b = res[False][rank], res[True][rank]
+        for i, name in enumerate(("params", "exp_avg", "exp_avg_sq", "shadow")):
+            if a[i] is not None:
+                assert np.array_equal(a[i], b[i]), (rank, name)
+        # the loss sums one partial per MSE output tile: the per-process
+        # autotuner's tile pick may reorder it (1 ulp), the gradients never
+        np.testing.assert_allclose(a[4], b[4], rtol=1e-6, atol=0)
+    assert np.array_equal(res[True][0][0], res[True][1][0])
+    assert res[True][0][5] == (10 if mib == 0 else 1)
+
+
 def test_dp_two_ranks_equals_summed_gradient_step():
     world = 2
     mgr = mp.get_context("spawn").Manager()
