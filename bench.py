@@ -313,6 +313,8 @@ def run(args):
     torch.manual_seed(0)
     model = get_model(cfg)
     mdist.attach_data_parallel(model)
+    if model.dist is not None and os.environ.get("MMAD_BENCH_DP_SERIAL", "0") == "1":
+        model.dist.overlap = False   # A/B of the torch exchange: flat all-reduce after the backward
     model._native.sync_shadow(force=True)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     dev = torch.device("cuda", local)
@@ -357,9 +359,12 @@ def run(args):
     fpw, _ = ae_flops_per_window(nat.enc_widths, nat.dec_widths)
     windows = args.steps * batch * world
     value = windows / el
-    exchange = ("native RCCL buckets (reduce-scatter, sharded Adam, all-gather) overlapped with backward"
+    exchange = ("native RCCL buckets (reduce-scatter" +
+                (" of bf16 gradients" if getattr(nat, "_grad_bf16", None) is not None else "") +
+                ", sharded Adam, all-gather) overlapped with backward"
                 if model.dist is not None and model.dist.native else
-                ("torch.distributed flat all-reduce" if world > 1 else "none"))
+                (("torch.distributed per-bucket all-reduce + Adam overlapped with backward"
+                  if model.dist.overlap else "torch.distributed flat all-reduce") if world > 1 else "none"))
     res = {
         "metric": "sensor-windows/sec (train fwd+bwd)",
         "value": round(value, 1),

@@ -102,6 +102,8 @@ SIGNATURES = {
     "mmad_ae_set_comm": (_I, [_P, _P]),
     "mmad_ae_adam_range": (_I, [_P, _F, _F, _F, _F, _I, _I64, _I64, _P]),
     "mmad_ae_dw_events": (_I, [_P, _I]),
+    "mmad_ae_set_grad_bf16": (_I, [_P, _P]),
+    "mmad_reduce_scatter_bucket_bf16": (_I, [_P, _P, _I64, _P]),
     "mmad_ae_wait_dw": (_I, [_P, _I, _P]),
     "mmad_ae_dw_plan": (_I, [_P, _I, ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(_I)]),
     "mmad_nap_fit_ws_bytes": (ctypes.c_size_t, [_I64, _I]),

@@ -92,6 +92,8 @@ struct mmad_ae {
   // torch-exchange data parallelism (mmad_ae_dw_events): the forward+backward
   // without Adam records ev_dw[l] after dW_l and ev_data[l] after bwd-data of l
   bool dw_events = false;
+  // optional bf16 gradient exchange (mmad_ae_set_grad_bf16): n_weight bf16
+  void* grad_bf16 = nullptr;
   hipEvent_t ev_small = nullptr, ev_cdone = nullptr;
   // fused step: dW GEMMs of layers < dw_main run on the caller's stream
   // (knob 19; tools/sched_sweep.py: 0.499 ms (2) vs 0.512 (1) vs 0.523 (3));
@@ -930,7 +932,15 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
           // ZeRO-1 form: reduce-scatter, Adam on this rank's shard, all-gather
           // of the updated weights the next step reads (bf16 shadow / fp32 p)
           const int64_t cnt = n / nr, off = boff + (int64_t)mmad_comm_rank(h->comm) * cnt;
-          RET_IF(mmad_reduce_scatter_bucket(h->comm, h->grads + boff, n, h->cstream));
+          if (h->grad_bf16) {
+            // bf16 on the wire: round the bucket, reduce-scatter, widen this rank's slice
+            char* gb = (char*)h->grad_bf16;
+            RET_IF(mmad_to_bf16(n, h->grads + boff, gb + boff * 2, h->cstream));
+            RET_IF(mmad_reduce_scatter_bucket_bf16(h->comm, gb + boff * 2, n, h->cstream));
+            RET_IF(mmad_from_bf16(cnt, gb + off * 2, h->grads + off, h->cstream));
+          } else {
+            RET_IF(mmad_reduce_scatter_bucket(h->comm, h->grads + boff, n, h->cstream));
+          }
           void* sh = h->dtype == MMAD_BF16 ? (void*)((char*)h->shadow + off * 2) : nullptr;
           RET_IF(mmad_adam(cnt, h->params + off, h->grads + off, h->m + off, h->v + off, adam->b1,
                            adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt, sh,
@@ -1200,6 +1210,13 @@ int mmad_ae_set_comm(mmad_ae* h, mmad_comm* c) {
 }
 
 int mmad_ae_dp_master_stale(const mmad_ae* h) { return h && h->master_stale ? 1 : 0; }
+
+int mmad_ae_set_grad_bf16(mmad_ae* h, void* buf) {
+  MMAD_CHECK_ARG(h && h->params, "ae_set_grad_bf16: unbound handle");
+  MMAD_CHECK_ARG(!buf || ((uintptr_t)buf % 16 == 0), "ae_set_grad_bf16: buffer must be 16-byte aligned");
+  h->grad_bf16 = buf;
+  return MMAD_OK;
+}
 
 int mmad_ae_dw_events(mmad_ae* h, int on) {
   MMAD_CHECK_ARG(h && h->side, "ae_dw_events: bind the handle first");

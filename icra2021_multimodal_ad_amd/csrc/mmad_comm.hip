@@ -74,6 +74,13 @@ __global__ void loopback_k(float* __restrict__ buf, int64_t n, float s) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     buf[i] *= s;
 }
+// the same on bf16 (RCCL's bf16 sum rounds each result to bf16: so does this)
+__global__ void loopback_bf16_k(bf16* __restrict__ buf, int64_t n, float s) {
+  const long long t0 = clock64();
+  while (clock64() - t0 < 20000) __builtin_amdgcn_s_sleep(8);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    buf[i] = (bf16)((float)buf[i] * s);
+}
 }  // namespace
 
 #define MMAD_RCCL_CHECK(expr)                                                        \
@@ -185,6 +192,26 @@ int mmad_reduce_scatter_bucket(mmad_comm* c, float* buf, int64_t n, void* stream
   if (c->loopback > 0.f) return mmad_allreduce_bucket(c, buf + (size_t)c->rank * cnt, (int64_t)cnt, stream);
   MMAD_RCCL_CHECK(rccl().reduce_scatter(buf, buf + (size_t)c->rank * cnt, cnt, ncclFloat32, ncclSum,
                                         c->comm, (hipStream_t)stream));
+  return MMAD_OK;
+}
+
+// the same on a bf16 buffer (the optional bf16 gradient exchange: half the bytes)
+int mmad_reduce_scatter_bucket_bf16(mmad_comm* c, void* buf, int64_t n, void* stream) {
+  MMAD_CHECK_ARG(c && (buf || n == 0) && n >= 0, "reduce_scatter_bucket_bf16: bad arguments");
+  MMAD_CHECK_ARG(n % c->nranks == 0, "reduce_scatter_bucket_bf16: n=%lld not divisible by %d ranks",
+                 (long long)n, c->nranks);
+  if (n == 0) return MMAD_OK;
+  const size_t cnt = (size_t)(n / c->nranks);
+  bf16* b = (bf16*)buf;
+  if (c->loopback > 0.f) {
+    const int64_t blocks = ((int64_t)cnt + 255) / 256 < 256 ? ((int64_t)cnt + 255) / 256 : 256;
+    loopback_bf16_k<<<(int)blocks, 256, 0, (hipStream_t)stream>>>(b + (size_t)c->rank * cnt, (int64_t)cnt,
+                                                                   c->loopback);
+    MMAD_LAUNCH_CHECK();
+    return MMAD_OK;
+  }
+  MMAD_RCCL_CHECK(rccl().reduce_scatter(b, b + (size_t)c->rank * cnt, cnt, ncclBfloat16, ncclSum, c->comm,
+                                        (hipStream_t)stream));
   return MMAD_OK;
 }
 

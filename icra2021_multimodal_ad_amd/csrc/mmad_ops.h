@@ -11,6 +11,7 @@ int mmad_sum2d(int rows, int cols, const float* x, int64_t ld, float scale, floa
 int mmad_sse_partials(int dtype, int M, int N, int Np, const void* y, const float* x, int ldx,
                       float* part, int nparts, void* stream);
 int mmad_to_bf16(int64_t n, const float* x, void* y, void* stream);
+int mmad_from_bf16(int64_t n, const void* x, float* y, void* stream);
 int64_t mmad_vib_kl_parts(int B, int k, int ld_z);
 // as the C-ABI forms, with the per-call values read from `dyn` (nullable)
 int mmad_pack_input_dyn(int dtype, int M, int K, int Mp, int Kp, const float* x, int ld_x,

@@ -671,6 +671,10 @@ __global__ void to_bf16_k(int64_t n, const float* __restrict__ x, bf16* __restri
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) y[i] = (bf16)x[i];
 }
+__global__ void from_bf16_k(int64_t n, const bf16* __restrict__ x, float* __restrict__ y) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = (float)x[i];
+}
 
 // ---------------------------------------------------------------------------
 // One launch for all end-of-backward reductions (bias grads, loss): job j,
@@ -1118,6 +1122,13 @@ int mmad_adam_dyn(int64_t n, float* p, const float* g, float* m, float* v, float
 int mmad_to_bf16(int64_t n, const float* x, void* y, void* stream) {
   if (n == 0) return MMAD_OK;
   to_bf16_k<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(n, x, (bf16*)y);
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+
+int mmad_from_bf16(int64_t n, const void* x, float* y, void* stream) {
+  if (n == 0) return MMAD_OK;
+  from_bf16_k<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(n, (const bf16*)x, y);
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
 }

@@ -146,7 +146,7 @@ class NativeComm:
     def self_test(self, n=4096):
         """Every collective the step uses, through the library's communicator,
         on fresh stream-ordered buffers, checked on the host: sum all-reduce
-        (rank r contributes r + 1), in-place reduce-scatter (fp32) and
+        (rank r contributes r + 1), in-place reduce-scatter (fp32, bf16) and
         all-gather (fp32, bf16).  A communicator that builds but cannot
         exchange fails here, before any train step depends on it.  Every rank
         issues EVERY collective whatever an earlier check found (a rank that
@@ -175,6 +175,12 @@ class NativeComm:
             shard = buf[self.rank * 4096:(self.rank + 1) * 4096]
             if not bool(torch.all(shard == want)):
                 errors.append(f"reduce-scatter: got {float(shard[0])}, want {want}")
+        buf = torch.full((m,), float(self.rank + 1), device="cuda", dtype=torch.bfloat16)
+        if issue(self._lib.mmad_reduce_scatter_bucket_bf16(self.handle, ptr(buf), m, stream_ptr()),
+                 "mmad_reduce_scatter_bucket_bf16"):
+            shard = buf[self.rank * 4096:(self.rank + 1) * 4096].float()
+            if not bool(torch.all(shard == want)):
+                errors.append(f"reduce-scatter (bf16): got {float(shard[0])}, want {want}")
         owners = torch.arange(self.world, device="cuda").repeat_interleave(4096).float() + 1.0
         for dt, code in ((torch.float32, _native.F32), (torch.bfloat16, _native.BF16)):
             g = torch.zeros(m, device="cuda", dtype=dt)
@@ -359,15 +365,22 @@ class DataParallel:
             dist.broadcast(model._native.params, src=src, group=self.group)
 
 
-def attach_data_parallel(model, group=None, native=None):
+def attach_data_parallel(model, group=None, native=None, grad_bf16=None):
     """Replicate rank-0 weights and make AutoEncoder.step all-reduce grads
     (natively over RCCL, overlapped with the backward, when the process group
-    is 'nccl'; through torch.distributed otherwise)."""
+    is 'nccl'; through torch.distributed otherwise).  grad_bf16 (native path;
+    default: env MMAD_DP_GRAD_BF16=1, else off): reduce-scatter the weight
+    gradients in bf16 (mmad_ae_set_grad_bf16, half the exchange bytes; not the
+    reference's fp32 sum)."""
     dp = DataParallel(group, native=native)
     dp.broadcast_params(model)
     if dp.world > 1:
         model._native.sync_shadow(force=True)
     if dp.native:
         model._native.set_comm(dp.comm)
+        if grad_bf16 is None:
+            grad_bf16 = os.environ.get("MMAD_DP_GRAD_BF16", "0") == "1"
+        if grad_bf16:
+            model._native.set_grad_bf16(True)
     model.dist = dp if dp.world > 1 else None
     return model

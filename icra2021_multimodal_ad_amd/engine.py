@@ -132,6 +132,13 @@ class NativeAE:
         self._comm = comm        # keep the communicator alive as long as the handle uses it
         call("mmad_ae_set_comm", self._h, comm.handle if comm is not None else None)
 
+    def set_grad_bf16(self, on=True):
+        """Optional bf16 gradient exchange of the sharded DP buckets
+        (mmad_ae_set_grad_bf16): this object owns the bf16 scratch buffer."""
+        self._grad_bf16 = (torch.empty(self.n_weight, device=self.device, dtype=torch.bfloat16)
+                           if on else None)
+        call("mmad_ae_set_grad_bf16", self._h, ptr(self._grad_bf16))
+
     @property
     def master_stale(self):
         """True while the sharded DP step has left the fp32 master weights (bf16

@@ -403,6 +403,8 @@ int mmad_comm_size(const mmad_comm* c);
  * [r*n/N, (r+1)*n/N) by the loopback's scale (after the same short delay),
  * the all-gather does nothing. */
 int mmad_reduce_scatter_bucket(mmad_comm* c, float* buf, int64_t n, void* stream);
+/* the same on bf16 buf[n] (RCCL's bf16 sum; loopback: bf16(x * scale)) */
+int mmad_reduce_scatter_bucket_bf16(mmad_comm* c, void* buf, int64_t n, void* stream);
 int mmad_all_gather_bucket(mmad_comm* c, void* buf, int64_t n, int dtype, void* stream);
 /* Attach (c != NULL) or detach a communicator.  With one attached,
  * mmad_ae_train_step runs the data-parallel step: each layer's dW lands in the
@@ -420,6 +422,13 @@ int mmad_all_gather_bucket(mmad_comm* c, void* buf, int64_t n, int dtype, void* 
  * mmad_ae_dp_sync_master (collective: every rank, same point) all-gathers
  * them; mmad_ae_dp_master_stale says whether one is due. */
 int mmad_ae_set_comm(mmad_ae* h, mmad_comm* c);
+/* Optional bf16 gradient exchange for the sharded buckets (NULL: off, the
+ * default): `buf` is an n_weight-element bf16 scratch buffer; each sharded
+ * bucket's fp32 gradient is rounded to bf16 into it, reduce-scattered in bf16
+ * (half the bytes on the wire), and this rank's summed slice is widened back to
+ * fp32 before its Adam.  Not the reference's arithmetic (its gradients are
+ * summed in fp32): an opt-in for exchange-bound runs. */
+int mmad_ae_set_grad_bf16(mmad_ae* h, void* buf);
 int mmad_ae_dp_sync_master(mmad_ae* h, void* stream);
 int mmad_ae_dp_master_stale(const mmad_ae* h);
 

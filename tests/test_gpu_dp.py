@@ -333,9 +333,11 @@ def _dp_plan(layers, mib):
     return out
 
 
-@pytest.mark.parametrize("dtype,rank,mib", [("bf16", 0, 8), ("bf16", 1, 8), ("f32", 1, 8),
-                                            ("bf16", 1, 0), ("f32", 0, 2)])
-def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank, mib):
+@pytest.mark.parametrize("dtype,rank,mib,gbf", [("bf16", 0, 8, False), ("bf16", 1, 8, False),
+                                                ("f32", 1, 8, False), ("bf16", 1, 0, False),
+                                                ("f32", 0, 2, False), ("bf16", 1, 0, True),
+                                                ("bf16", 0, 8, True), ("f32", 1, 8, True)])
+def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank, mib, gbf):
     """The sharded DP step (knob dp_shard: reduce-scatter, Adam on this rank's
     1/N of each weight bucket, all-gather of the updated weights) on one GPU,
     through a loopback communicator posing as rank `rank` of 2 (its
@@ -347,7 +349,11 @@ def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank, mib):
     the small bucket is all-reduced and fully updated; the handle reports
     stale master weights and refuses to detach until synced.  The shards
     follow the bucket plan (knob dp_bucket_mib: consecutive layers share a
-    bucket, split once over the ranks)."""
+    bucket, split once over the ranks).  gbf: the optional bf16 gradient
+    exchange (mmad_ae_set_grad_bf16) -- this rank's shard then equals "bf16(g)
+    x 2 widened to fp32, then Adam" bit for bit (the loopback's bf16 sum of
+    two identical shards is exact, as RCCL's 2-rank bf16 sum of bf16 inputs
+    rounds once)."""
     import ctypes
     import types as _t
     from icra2021_multimodal_ad_amd import _native
@@ -372,10 +378,14 @@ def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank, mib):
         mb = mk()
         a, b = ma._native, mb._native
         a.set_comm(comm)
+        if gbf:
+            a.set_grad_bf16(True)
         x = torch.from_numpy(synth_windows(384, 700, seed=95)).cuda()
         p0, m0, v0 = a.params.clone(), a.exp_avg.clone(), a.exp_avg_sq.clone()
         la = float(a.train_step_fused(x))
         lb = b.train_step(x)
+        if gbf:
+            b.grads[:b.n_weight] = b.grads[:b.n_weight].bfloat16().float()
         b.grads.mul_(2.0)
         b.adam()
         torch.cuda.synchronize()
