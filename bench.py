@@ -313,8 +313,9 @@ def run(args):
     torch.manual_seed(0)
     model = get_model(cfg)
     mdist.attach_data_parallel(model)
-    if model.dist is not None and os.environ.get("MMAD_BENCH_DP_SERIAL", "0") == "1":
-        model.dist.overlap = False   # A/B of the torch exchange: flat all-reduce after the backward
+    if model.dist is not None and os.environ.get("MMAD_BENCH_DP_OVERLAP") in ("0", "1"):
+        # A/B of the torch exchange (default: overlapped)
+        model.dist.overlap = os.environ["MMAD_BENCH_DP_OVERLAP"] == "1"
     model._native.sync_shadow(force=True)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     dev = torch.device("cuda", local)
@@ -364,7 +365,7 @@ def run(args):
                 ", sharded Adam, all-gather) overlapped with backward"
                 if model.dist is not None and model.dist.native else
                 (("torch.distributed per-bucket all-reduce + Adam overlapped with backward"
-                  if model.dist.overlap else "torch.distributed flat all-reduce") if world > 1 else "none"))
+                  if model.dist.overlapped else "torch.distributed flat all-reduce") if world > 1 else "none"))
     res = {
         "metric": "sensor-windows/sec (train fwd+bwd)",
         "value": round(value, 1),

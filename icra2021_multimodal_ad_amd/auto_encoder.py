@@ -303,7 +303,7 @@ class AutoEncoder(AbstractModel):
         # torch exchange: the backward records per-layer dW events so that each
         # bucket's all-reduce + Adam starts while the lower layers still run
         lr, betas, aeps = self._adam_hyper(optimizer)
-        if self.dist.overlap and not getattr(nat, "_dw_events", False):
+        if self.dist.overlapped and not getattr(nat, "_dw_events", False):
             nat.dw_events(True)
             nat._dw_events = True
         loss = nat.train_step(x, k=self.k, eps=eps, seed=seed, offset=self._rng_offset,

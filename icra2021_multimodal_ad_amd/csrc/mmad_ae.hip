@@ -90,8 +90,11 @@ struct mmad_ae {
   hipStream_t cstream = nullptr;
   std::vector<hipEvent_t> ev_dw;
   // torch-exchange data parallelism (mmad_ae_dw_events): the forward+backward
-  // without Adam records ev_dw[l] after dW_l and ev_data[l] after bwd-data of l
+  // without Adam records ev_xdw[l] after dW_l and ev_xdata[l] after bwd-data of
+  // l.  System-scope fences (unlike the executor's own events): the exchange
+  // may read the gradients with a copy engine, which does not see the L2
   bool dw_events = false;
+  std::vector<hipEvent_t> ev_xdw, ev_xdata;
   // optional bf16 gradient exchange (mmad_ae_set_grad_bf16): n_weight bf16
   void* grad_bf16 = nullptr;
   hipEvent_t ev_small = nullptr, ev_cdone = nullptr;
@@ -187,6 +190,8 @@ struct mmad_ae {
     if (ev_join) (void)hipEventDestroy(ev_join);
     if (ev_loss) (void)hipEventDestroy(ev_loss);
     for (auto e : ev_dw) (void)hipEventDestroy(e);
+    for (auto e : ev_xdw) (void)hipEventDestroy(e);
+    for (auto e : ev_xdata) (void)hipEventDestroy(e);
     if (ev_small) (void)hipEventDestroy(ev_small);
     if (ev_cdone) (void)hipEventDestroy(ev_cdone);
     if (cstream) (void)hipStreamDestroy(cstream);
@@ -845,7 +850,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
       RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
                      nullptr, PROBE_DW + l));
-      if (h->dw_events) MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l], side));
+      if (h->dw_events) MMAD_HIP_CHECK(hipEventRecord(h->ev_xdw[l], side));
     }
     if (l > 0) {
       const AeLayer& p = h->L[l - 1];
@@ -899,7 +904,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       }
     }
     // torch exchange: W_l is read for the last time by the bwd-data of l
-    if (!adam && h->dw_events && l > 0) MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
+    if (!adam && h->dw_events && l > 0) MMAD_HIP_CHECK(hipEventRecord(h->ev_xdata[l], st));
     if (dp && dp_loss && l == (nL > h->dp_small_at ? h->dp_small_at : 0)) {
       // the last bwd-data (l = 1, just enqueued) has produced every bias
       // partial and the loss partials are the forward's: reduce them on the
@@ -1198,11 +1203,12 @@ int mmad_ae_set_comm(mmad_ae* h, mmad_comm* c) {
     int least = 0, greatest = 0;
     MMAD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     MMAD_HIP_CHECK(hipStreamCreateWithPriority(&h->cstream, hipStreamNonBlocking, greatest));
-    if (h->ev_dw.empty()) {
-      h->ev_dw.resize(h->L.size());
-      for (auto& e : h->ev_dw) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, h->ev_flags_));
-    }
-    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_small, h->ev_flags_));
+    // the events RCCL's reads of a bucket wait on keep the system-scope
+    // fence (a transport may move the bytes with a copy engine, which does
+    // not see the L2); one per bucket and step
+    h->ev_dw.resize(h->L.size());
+    for (auto& e : h->ev_dw) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_small, hipEventDisableTiming));
     MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_cdone, h->ev_flags_));
   }
   h->comm = c;
@@ -1220,9 +1226,11 @@ int mmad_ae_set_grad_bf16(mmad_ae* h, void* buf) {
 
 int mmad_ae_dw_events(mmad_ae* h, int on) {
   MMAD_CHECK_ARG(h && h->side, "ae_dw_events: bind the handle first");
-  if (on && h->ev_dw.empty()) {
-    h->ev_dw.resize(h->L.size());
-    for (auto& e : h->ev_dw) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, h->ev_flags_));
+  if (on && h->ev_xdw.empty()) {
+    h->ev_xdw.resize(h->L.size());
+    h->ev_xdata.resize(h->L.size());
+    for (auto& e : h->ev_xdw) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : h->ev_xdata) MMAD_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   h->dw_events = on != 0;
   return MMAD_OK;
@@ -1231,8 +1239,8 @@ int mmad_ae_dw_events(mmad_ae* h, int on) {
 int mmad_ae_wait_dw(mmad_ae* h, int layer, void* stream) {
   MMAD_CHECK_ARG(h && h->dw_events, "ae_wait_dw: dW events are off (mmad_ae_dw_events)");
   MMAD_CHECK_ARG(layer >= 0 && layer < (int)h->L.size(), "ae_wait_dw: bad layer %d", layer);
-  MMAD_HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream, h->ev_dw[layer], 0));
-  if (layer > 0) MMAD_HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream, h->ev_data[layer], 0));
+  MMAD_HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream, h->ev_xdw[layer], 0));
+  if (layer > 0) MMAD_HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream, h->ev_xdata[layer], 0));
   return MMAD_OK;
 }
 

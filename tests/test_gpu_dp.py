@@ -53,7 +53,7 @@ def _worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def _xworker(rank, world, port, out, overlap, dtype, mib):
+def _xworker(rank, world, port, out, overlap, dtype, mib, dim, batch):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0")
     import torch.distributed as dist
@@ -66,16 +66,20 @@ def _xworker(rank, world, port, out, overlap, dtype, mib):
     torch.cuda.set_device(0)
     cfg = _cfg()
     cfg.dtype = dtype
+    cfg.input_size = dim
+    cfg.btl_size = 16 if dim == 192 else 100
+    torch.manual_seed(0)
     with _native.tune(dp_bucket_mib=mib):
         m = get_model(cfg)
-    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in
-                       init_state_dict(192, 16, 5, seed=51).items()})
+    if dim == 192:
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in
+                           init_state_dict(192, 16, 5, seed=51).items()})
     mdist.attach_data_parallel(m)
     m.dist.overlap = overlap
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
     losses = []
     for s in range(3):
-        x = torch.from_numpy(synth_windows(96, 192, seed=60 + 10 * s + rank)).cuda()
+        x = torch.from_numpy(synth_windows(batch, dim, seed=60 + 10 * s + rank)).cuda()
         losses.append(float(m.train_step_async(x, opt)))
     torch.cuda.synchronize()
     nat = m._native
@@ -86,8 +90,9 @@ def _xworker(rank, world, port, out, overlap, dtype, mib):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dtype,mib", [("f32", 0), ("bf16", 0), ("bf16", 8)])
-def test_torch_exchange_overlapped_equals_serial(dtype, mib):
+@pytest.mark.parametrize("dtype,mib,dim,batch", [("f32", 0, 192, 96), ("bf16", 0, 192, 96),
+                                                 ("bf16", 8, 192, 96), ("bf16", 8, 2048, 1024)])
+def test_torch_exchange_overlapped_equals_serial(dtype, mib, dim, batch):
     """The torch exchange (the path without the native communicator):
     per-bucket all-reduce + Adam on bucket streams gated by the executor's dW
     events (DataParallel.overlap, the default) gives the serial form's bits
@@ -95,13 +100,16 @@ def test_torch_exchange_overlapped_equals_serial(dtype, mib):
     steps at 2 ranks (a 2-operand sum is order-free, Adam elementwise):
     parameters, Adam moments and the bf16 shadow (losses to 1e-6: tile-
     dependent partial order).  mib = 0: one
-    bucket per layer (10 buckets); 8: the default plan (one bucket here)."""
+    bucket per layer (10 buckets); 8: the default plan (one bucket at D=192,
+    five at D=2048 -- the size at which executor events without a system-scope
+    fence let the exchange's copy read stale gradients, round 4)."""
     world = 2
     res = {}
     for overlap in (False, True):
         mgr = mp.get_context("spawn").Manager()
         out = mgr.dict()
-        mp.start_processes(_xworker, args=(world, _free_port(), out, overlap, dtype, mib), nprocs=world,
+        mp.start_processes(_xworker, args=(world, _free_port(), out, overlap, dtype, mib, dim, batch),
+                           nprocs=world,
                            join=True, start_method="spawn")
         res[overlap] = dict(out)
     for rank in range(world):
@@ -113,7 +121,7 @@ def test_torch_exchange_overlapped_equals_serial(dtype, mib):
         # autotuner's tile pick may reorder it (1 ulp), the gradients never
         np.testing.assert_allclose(a[4], b[4], rtol=1e-6, atol=0)
     assert np.array_equal(res[True][0][0], res[True][1][0])
-    assert res[True][0][5] == (10 if mib == 0 else 1)
+    assert res[True][0][5] == (10 if mib == 0 else (1 if dim == 192 else 5))
 
 
 def test_dp_two_ranks_equals_summed_gradient_step():

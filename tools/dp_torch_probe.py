@@ -1,7 +1,9 @@
 """Torch-exchange DP step (2 ranks sharing cuda:0 over gloo) at a chosen
 size, with a traceback dump of every thread if a rank stalls: the harness
 for debugging / timing the overlapped exchange (dist.DataParallel.overlap).
-Usage: python tools/dp_torch_probe.py <overlap 0|1> <model ae|vib_ae> <batch> <steps>"""
+Usage: python tools/dp_torch_probe.py <overlap 0|1|2> <model ae|vib_ae> <batch> <steps>
+(2: the overlapped form with every bucket stream waiting for the whole
+backward instead of its dW events -- isolates the event gating)"""
 import faulthandler
 import os
 import socket
@@ -39,6 +41,10 @@ def worker(rank, world, port, overlap, model_name, batch, steps):
     m = get_model(cfg)
     mdist.attach_data_parallel(m)
     m.dist.overlap = bool(overlap)
+    if overlap == 2:
+        m._native.dw_events(True)
+        m._native._dw_events = True
+        m._native.wait_dw = lambda layer, stream: stream.wait_stream(torch.cuda.current_stream())
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
     pool = [synth_windows_device(batch, 2048, torch.device("cuda", 0), seed=1000 * rank + i) for i in range(4)]
     for i in range(2):
