@@ -314,7 +314,7 @@ def run(args):
     model = get_model(cfg)
     mdist.attach_data_parallel(model)
     if model.dist is not None and os.environ.get("MMAD_BENCH_DP_OVERLAP") in ("0", "1"):
-        # A/B of the torch exchange (default: overlapped)
+        # A/B of the torch exchange (default: serial, dist.DataParallel.overlap)
         model.dist.overlap = os.environ["MMAD_BENCH_DP_OVERLAP"] == "1"
     model._native.sync_shadow(force=True)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)

@@ -17,11 +17,12 @@ Two exchange paths:
   Adam.  The fp32 master and m / v are then current only on their owner:
   ``epoch_end`` all-gathers them (mmad_ae_dp_sync_master) before anything
   reads the state_dict.  One host call per step, no host sync.
-* torch (gloo / fallback): train_fwd_bwd with per-layer dW events; each
-  weight bucket (the native plan) is all-reduced through torch.distributed on
-  its own stream as soon as its dW GEMMs are done and Adam-updated there
-  (mmad_ae_adam_range), overlapping the rest of the backward; the small bucket
-  and the loss follow the backward.  Weights and Adam state replicated.
+* torch (gloo / fallback): train_fwd_bwd, one torch.distributed all-reduce
+  of the flat gradient, the flat Adam; or (DataParallel.overlap, opt-in) each
+  weight bucket of the native plan all-reduced on its own stream as soon as
+  the executor's dW events say its GEMMs are done and Adam-updated there
+  (mmad_ae_adam_range), overlapping the rest of the backward.  Weights and
+  Adam state replicated.
 
 Around the step (NoveltyDetecter under data parallelism): each
 rank trains on its rows of every global batch (data_loaders.BatchLoader with
@@ -267,12 +268,15 @@ class DataParallel:
     def native(self):
         return self.comm is not None
 
-    # torch exchange: overlapped per bucket (True, default), or the serial
-    # form -- one flat all-reduce after the backward, then the flat Adam (False;
-    # same bits at 2 ranks).  Two ranks sharing one GPU over gloo, D=2048 bf16,
-    # 1024 windows per rank: 13.4 vs 16.6 ms/step
-    # (profiles/r07g_torch_exchange_gloo.txt)
-    overlap = True
+    # torch exchange: overlapped per bucket (True), or the serial form -- one
+    # flat all-reduce after the backward, then the flat Adam (False, default;
+    # same bits at 2 ranks).  Default off: over gloo (two ranks sharing one GPU,
+    # the only multi-rank run available here) the overlapped form is 19 %
+    # faster at D=2048 / 1024 windows per rank (13.4 vs 16.6 ms/step) but
+    # 4.2 s/step at the C4 shape (VIB, 4096 windows) against 18 ms serial
+    # (profiles/r07g_torch_exchange_gloo.txt): the fallback keeps the form
+    # that measured well everywhere; env MMAD_DP_OVERLAP=1 opts in
+    overlap = os.environ.get("MMAD_DP_OVERLAP", "0") == "1"
 
     def all_reduce_grads(self, flat_grads):
         if self.world > 1:

@@ -95,7 +95,7 @@ def _xworker(rank, world, port, out, overlap, dtype, mib, dim, batch):
 def test_torch_exchange_overlapped_equals_serial(dtype, mib, dim, batch):
     """The torch exchange (the path without the native communicator):
     per-bucket all-reduce + Adam on bucket streams gated by the executor's dW
-    events (DataParallel.overlap, the default) gives the serial form's bits
+    events (DataParallel.overlap, opt-in) gives the serial form's bits
     -- one flat all-reduce after the backward, then the flat Adam -- over 3
     steps at 2 ranks (a 2-operand sum is order-free, Adam elementwise):
     parameters, Adam moments and the bf16 shadow (losses to 1e-6: tile-
