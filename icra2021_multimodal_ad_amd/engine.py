@@ -98,6 +98,9 @@ class NativeAE:
              ptr(self.running))
         if self._pair:
             call("mmad_ae_set_shadow_pair", self._h, ptr(sb[self.n_weight:]))
+        if getattr(self, "_grad_bf16", None) is not None:
+            # the bf16 exchange scratch follows the buffers to their new device
+            self.set_grad_bf16(True)
 
     @property
     def shadow(self):
@@ -118,6 +121,7 @@ class NativeAE:
         self.device = device
         self._alloc(device, src=old)
         self._ws = None
+        self._dw_streams = None   # the torch exchange's bucket streams belong to the old device
         return self
 
     def set_comm(self, comm):
