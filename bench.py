@@ -292,15 +292,15 @@ def run(args):
     if shared:
         local = 0
     cname = args.config if args.config != "auto" else ("c2" if world == 1 else "c4")
+    for kv in args.tune:
+        k, v = kv.split("=", 1)
+        _native.tune_set(k, int(v))
     if cname == "c5":
         import bench_score
         if world > 1:
             raise SystemExit("c5 (scoring) is a one-GPU configuration")
         bench_score.run_c5(args)
         return
-    for kv in args.tune:
-        k, v = kv.split("=", 1)
-        _native.tune_set(k, int(v))
     cfgd = dict(CONFIGS[cname])
     for k in ("model", "dim", "batch"):
         if getattr(args, k) is not None:

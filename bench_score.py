@@ -173,6 +173,8 @@ def run_c5(args):
     }
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(dim, budget_s=min(args.cpu_budget, 12.0))
+    if getattr(args, "tune", None):
+        res["tune"] = args.tune
     print(json.dumps(res), flush=True)
 
 
