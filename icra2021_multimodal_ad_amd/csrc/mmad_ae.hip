@@ -153,6 +153,7 @@ struct mmad_ae {
   mutable int probe_n = 0;
   mutable unsigned probe_mask = 0;    // layers the last probed launch covered (bit l)
   std::vector<hipEvent_t> probe_ev;   // [2 * capacity]: start, end pairs
+  hipEvent_t probe_sync = nullptr;    // a main-stream probe's start waits for the side stream
   // hipGraph-captured fused train steps (mmad_ae_train_step_graph): one per
   // call signature, replayed after a host->device copy of the per-call values
   // (a ring of pinned host slots, each reused only once its copy has run)
@@ -183,6 +184,7 @@ struct mmad_ae {
       if (e) (void)hipEventDestroy(e);
     if (dyn_host) (void)hipHostFree(dyn_host);
     for (auto e : probe_ev) (void)hipEventDestroy(e);
+    if (probe_sync) (void)hipEventDestroy(probe_sync);
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.exec);
     if (gstream) (void)hipStreamDestroy(gstream);
     for (auto e : ev_fork) (void)hipEventDestroy(e);
@@ -581,6 +583,16 @@ static int ae_gemm(const mmad_ae* h, const AeWS& w, int dt, int epi, const void*
   ep.sk_ctl = w.sk_ctl[r];
   const bool rec = probe >= 0 && probe == h->probe_id && !h->capturing &&
                    2 * h->probe_n < (int)h->probe_ev.size();
+  if (rec && h->side && s != h->side && h->probe_sync) {
+    // a probed main-stream launch starts its clock once the side stream's
+    // earlier GEMMs are done: its blocks (a whole CU's LDS each on the tail
+    // tiles) wait for those CUs anyway, and the event pair then brackets the
+    // launch's own execution, first dispatch to completion, as rocprofv3's
+    // kernel records do (without it the pair also held ~4 us of that wait on
+    // the c2 tail: 31.2 vs 26.8 us, profiles/r08o_prof_c2)
+    MMAD_HIP_CHECK(hipEventRecord(h->probe_sync, h->side));
+    MMAD_HIP_CHECK(hipStreamWaitEvent(s, h->probe_sync, 0));
+  }
   if (rec) MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n], s));
   const int rc = mmad_gemm_dispatch(dt, epi, A, lda, B, ldb, Mp, Np, K, ep, s, cfg);
   if (rc != MMAD_OK) return rc;
@@ -1519,6 +1531,7 @@ int mmad_ae_probe(mmad_ae* h, int kind, int layer, int capacity) {
   if (layer < 0 || capacity == 0) return MMAD_OK;
   h->probe_ev.resize(2 * (size_t)capacity, nullptr);
   for (auto& e : h->probe_ev) MMAD_HIP_CHECK(hipEventCreate(&e));
+  if (!h->probe_sync) MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->probe_sync, hipEventDisableTiming));
   h->probe_id = (kind == 0 ? PROBE_FWD : PROBE_DW) + layer;
   return MMAD_OK;
 }

@@ -491,7 +491,10 @@ int mmad_ae_status(mmad_ae* h, void* ws, int64_t ws_bytes, void* stream);
  * executor brackets ONE GEMM launch per call with a pair of timing events on
  * the stream that launch runs on -- kind 0: the forward (or MSE / score) GEMM
  * of `layer`, kind 1: its dW GEMM (Adam fused in mmad_ae_train_step) -- for
- * the next `capacity` calls.  layer < 0 or capacity 0 turns it off.
+ * the next `capacity` calls.  layer < 0 or capacity 0 turns it off.  A
+ * probed launch on the main stream starts its clock only after the side
+ * stream's earlier work (in probed calls only), so the pair brackets the
+ * launch's own execution as a profiler's kernel record does.
  * mmad_ae_probe_read synchronises on the recorded events and writes up to
  * max_n durations (ms) in call order; returns how many (or < 0). */
 int mmad_ae_probe(mmad_ae* h, int kind, int layer, int capacity);
