@@ -138,6 +138,9 @@ struct mmad_ae {
   // GEMMs of the layers in between wait for the next recorded one (knob 22;
   // c2 0.435-0.440 vs 0.442-0.444 with 1, profiles/r02bv_*)
   int ev_every = 2;
+  // the main stream's hand-off events (bwd-data -> side-stream dW, MSE ->
+  // side-stream loss) completed by the GEMM launch itself (knob 31)
+  int ev_on_kernel = 1;
   // hipGraph cache for mmad_ae_score_stream: one captured graph per
   // (input, output, workspace, N, batch) pass, replayed with one launch
   struct ScoreGraph {
@@ -364,6 +367,7 @@ int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, i
     h->pair_rows = mmad_knob(20);
     h->dw_main_ping = mmad_knob(21);
     h->ev_every = mmad_knob(22);
+    h->ev_on_kernel = mmad_knob(31);
     h->loss_side = mmad_knob(23);
     h->dp_small_at = mmad_knob(24);
     h->keep_grads = mmad_knob(25);
@@ -632,8 +636,9 @@ static GemmEpi fwd_epi(const mmad_ae* h, const AeWS& w, const AeLayer& a, const 
 }
 
 // mode 0 = train (MSE-fused last layer), 1 = eval, 2 = train BN, plain last layer
+// mse_done (nullable): an event the train-mode MSE GEMM launch completes itself
 static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, const float* eps,
-                       uint64_t seed, uint64_t offset, hipStream_t st) {
+                       uint64_t seed, uint64_t offset, hipStream_t st, hipEvent_t mse_done = nullptr) {
   const int dt = h->dtype;
   const int nL = (int)h->L.size();
   const int B = w.B, k = w.k;
@@ -657,6 +662,7 @@ static int run_forward(mmad_ae* h, AeWS& w, const float* x, int ld_x, int mode, 
       ep.gscale = 2.0f / (float)k;
       ep.lossp = w.lossp;
       ep.dyn = w.dyn;
+      ep.done_ev = mse_done;
       int cfg = 0;
       RET_IF(ae_gemm(h, w, dt, GEMM_EPI_MSE, in, a.Kp, wt, a.Kp, Mp, a.Np, a.Kp, ep, st, &cfg,
                      PROBE_FWD + l));
@@ -835,6 +841,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     const bool side_dw = adam && !dp && !ping && l >= w.dw_main;
     const bool rec = bk || (side_dw && (h->ev_every <= 1 || l == w.dw_main ||
                                         (l - w.dw_main) % h->ev_every == 0));
+    bool ev_attached = false;   // ev_data[l] completed by the bwd-data launch (ev_on_kernel)
     if (dp) {
       // data parallel: the dW GEMMs of a bucket's layers are issued together
       // once the layer that closes it has its dz (one fork per bucket: the
@@ -900,9 +907,13 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
           ep.bn_act = p.act;
           ep.slope = h->slope;
         }
+        if (rec && h->ev_on_kernel && !h->capturing) {
+          ep.done_ev = h->ev_data[l];
+          ev_attached = true;
+        }
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
                                   a.Np, ep, st));
-        if (rec) MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
+        if (rec && !ev_attached) MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
         if (!ps.bwd_fused)
           RET_IF(mmad_bn_act_bwd_apply(dt, p.act, h->slope, rows_of(w, p), p.N, Mpp, p.Np, ps.dy,
                                        ps.out, ps.mean, ps.rstd, h->params + p.g_off, ps.bnpart,
@@ -911,6 +922,10 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       } else {
         ep.out = ps.dy;
         ep.part = ps.stats;
+        if (rec && h->ev_on_kernel && !h->capturing) {
+          ep.done_ev = h->ev_data[l];
+          ev_attached = true;
+        }
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
                                   a.Np, ep, st));
       }
@@ -938,7 +953,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       // as its last dW GEMM is complete, then its Adam update (which rewrites
       // the bucket's weights, so it also waits for the main stream's bwd-data
       // of layer l, the last GEMM of the chain that reads them)
-      if (l == 0 || !(h->L[l - 1].bn) || (h->vib && l == h->n_enc))
+      if ((l == 0 || !(h->L[l - 1].bn) || (h->vib && l == h->n_enc)) && !ev_attached)
         MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
       MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_data[l], 0));
       const int nr = mmad_comm_size(h->comm) > 0 ? mmad_comm_size(h->comm) : 1;
@@ -979,7 +994,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       // dW_l with this layer's Adam update fused into its epilogue.  It rewrites
       // W_l, so it starts only once the main stream has finished reading W_l
       // (bwd-data of l); the rest of the chain keeps overlapping it.
-      if (rec && (l == 0 || !(h->L[l - 1].bn) || (h->vib && l == h->n_enc)))
+      if (rec && !ev_attached && (l == 0 || !(h->L[l - 1].bn) || (h->vib && l == h->n_enc)))
         MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
       fill_adam(dwe, l, true);
       // the last dW GEMMs of the chain go to the main stream, which is idle
@@ -1090,7 +1105,9 @@ int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const
   // ping-pong schedule (bf16 with a shadow pair, large calls, single process)
   w.ping = h->shadow_alt && !h->comm && !h->capturing && w.Mpe >= h->pair_rows;
   if (w.ping) w.dw_main = h->dw_main_ping;
-  RET_IF(run_forward(h, w, x, ld_x, 0, eps, seed, offset, st));
+  // the side stream's loss reduction waits on the MSE launch's own completion
+  const bool loss_ev_on_kernel = !h->comm && h->loss_side && h->ev_on_kernel && !h->capturing;
+  RET_IF(run_forward(h, w, x, ld_x, 0, eps, seed, offset, st, loss_ev_on_kernel ? h->ev_loss : nullptr));
   if (!h->comm && !h->loss_side) {
     RET_IF(run_backward(h, w, true, beta_kl, &ah, st));
     RET_IF(finish_reductions(h, w, false, true, beta_kl, loss_out, st));
@@ -1101,7 +1118,7 @@ int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const
     // the loss needs only the forward's MSE (and KL) partials: reduce it on
     // the side stream now, off the main stream's tail (the backward joins the
     // side stream back into the caller's before the step ends)
-    MMAD_HIP_CHECK(hipEventRecord(h->ev_loss, st));
+    if (!loss_ev_on_kernel) MMAD_HIP_CHECK(hipEventRecord(h->ev_loss, st));
     MMAD_HIP_CHECK(hipStreamWaitEvent(h->side, h->ev_loss, 0));
     RET_IF(finish_reductions(h, w, false, true, beta_kl, loss_out, h->side));
     RET_IF(run_backward(h, w, true, beta_kl, &ah, st));

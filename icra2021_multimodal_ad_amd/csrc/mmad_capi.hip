@@ -64,6 +64,7 @@ int g_knob[MMAD_KNOB_COUNT] = {
     1,     // 28 DP: sharded weight buckets (reduce-scatter, Adam on 1/N, all-gather)
     0,     // 29 retired (graph node priorities: no effect, profiles/r03w_graph_priority.txt)
     8,     // 30 DP: minimum exchange bucket (MiB of fp32 gradient; consecutive layers merge)
+    1,     // 31 bwd-data hand-off events completed by the GEMM launch (hipExtLaunchKernel)
 };
 }  // namespace
 int mmad_knob(int k) { return g_knob[k]; }

@@ -114,6 +114,10 @@ struct GemmEpi {
   int dbg;               // diagnostics (tools/gemm_phase): 1 skip main loop, 2 skip epilogue,
                          // 4 force the split-K combine's timeout path (tests),
                          // 8 skip the FWD Welford partial stores
+  // host only (nullable): an event completed by the launch itself
+  // (hipExtLaunchKernel's stop event) instead of a separate hipEventRecord
+  // behind it, whose marker packet holds the stream's next dispatch
+  hipEvent_t done_ev;
 };
 
 int mmad_knob(int k);          // the tune table (mmad_tune_set)

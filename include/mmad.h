@@ -83,8 +83,11 @@ int mmad_pad_granule(void);
  *   29 retired (EINVAL)
  *   30 data parallel: minimum exchange bucket in MiB of fp32 gradient;
  *      consecutive layers (backward order) share a bucket until it holds this
- *      much (8; 0 = one bucket per layer) */
-#define MMAD_KNOB_COUNT 31
+ *      much (8; 0 = one bucket per layer)
+ *   31 the bwd-data GEMM's hand-off event to the side stream completed by the
+ *      launch itself (hipExtLaunchKernel stop event, 1) or recorded behind it
+ *      (0: a marker packet that holds the main stream's next dispatch) */
+#define MMAD_KNOB_COUNT 32
 int mmad_tune_set(int knob, int value);
 int mmad_tune_get(int knob, int* value);
 /* The split-K factor the dispatcher picks for a padded GEMM shape (Mp x Np
