@@ -1,7 +1,9 @@
 """Benchmark: sensor-windows/sec of the AE train step (fwd + sum-MSE + bwd +
 Adam) on synthetic 4-modal windows, 1..8 MI355X (BASELINE.json metric).
 
-Workloads (``--config``; ``auto`` = c2 on one GPU, c4 on several):
+Workloads (``--config``; ``auto`` = c3 on one GPU -- the largest single-GPU
+configuration, C4's per-GPU shard -- with c2 measured after it in the same line
+as the ``c2`` sub-object; c4 on several):
   c2  BASELINE configs[1]: FC-AE, D=2048, 1024 windows, bf16, 1 GPU
   c3  BASELINE configs[2]: VIB-AE (k=1, beta_kl=1), D=2048, 4096 windows, bf16
   c4  BASELINE configs[3]: the c3 model, 4096 windows PER GPU (global 4096*N),
@@ -148,16 +150,57 @@ def pick_dominant_layer(nat, batch):
     return max(range(len(nat.layers)), key=lambda l: (nat.layers[l]["N"] * nat.layers[l]["K"], -l))
 
 
-def _pmc_file(kind, workload):
+CSRC = os.path.join(REPO, "icra2021_multimodal_ad_amd", "csrc")
+
+
+def src_sha16(kind):
+    """Hash of the kernel sources a PMC summary of `kind` measured: the GEMM
+    template (+ the executor's dW tile rule for `dw`).  A summary whose hash
+    differs from this tree's was taken on other code: bench reports it as
+    `traffic_prior_profile`, not as `traffic`."""
     import glob
+    import hashlib
+    files = sorted(glob.glob(os.path.join(CSRC, "mmad_gemm*")) + [os.path.join(CSRC, "mmad_common.h")])
+    if kind == "dw":
+        files.append(os.path.join(CSRC, "mmad_ae.hip"))
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def _pmc_file(kind, workload):
+    """Newest profiles/*_pmc_<kind>.json for this workload: (summary, path,
+    matches-this-build)."""
+    import glob
+    cur = src_sha16(kind)
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", f"*_pmc_{kind}.json")))[::-1]:
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
         if d.get("workload") == workload:
-            return d, os.path.relpath(f, REPO)
-    return None, None
+            return d, os.path.relpath(f, REPO), d.get("src_sha16") == cur
+    return None, None, False
+
+
+def pmc_fields(kind, workload):
+    """roofline `traffic` (+ provenance) from the matching PMC summary; a
+    summary taken on other kernel sources is reported as prior, never as
+    this build's traffic."""
+    pmc, src, current = _pmc_file(kind, workload)
+    out = {"traffic": None}
+    if pmc is None:
+        return out, None
+    if current:
+        out["traffic"] = pmc.get("traffic_bytes_per_launch")
+    else:
+        out["traffic_prior_profile"] = pmc.get("traffic_bytes_per_launch")
+    out["traffic_source"] = src
+    out["traffic_source_matches_build"] = current
+    return out, (pmc if current else None)
 
 
 def gemm_roofline(model, batch, iters=50):
@@ -195,14 +238,20 @@ def gemm_roofline(model, batch, iters=50):
     peak = BF16_PEAK_TFLOPS if dt == _native.BF16 else F32_PEAK_TFLOPS
     ach = flops / avg_s / 1e12
     wl = {"dim": L["K"], "batch": batch, "dtype": nat.dtype_name}
-    pmc, src = _pmc_file("traffic", wl)
-    return {"kernel": f"mmad_gemm_kernel fwd (encoder layer 1: {batch}x{L['K']} . {L['N']}x{L['K']}^T,"
-                      f" bias+LeakyReLU+BN-stat epilogue)",
-            "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(ach / peak, 4),
-            "traffic": pmc["traffic_bytes_per_launch"] if pmc else None,
-            "traffic_source": src, "avg_us": round(avg_s * 1e6, 2), "flops_per_launch": flops,
-            "timing": f"{iters} back-to-back launches between one HIP event pair"}
+    tf, pmc = pmc_fields("traffic", wl)
+    res = {"kernel": f"mmad_gemm fwd (encoder layer 1: {batch}x{L['K']} . {L['N']}x{L['K']}^T,"
+                     f" bias+LeakyReLU+BN-stat epilogue)",
+           "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+           "frac": round(ach / peak, 4), **tf,
+           "avg_us": round(avg_s * 1e6, 2), "flops_per_launch": flops,
+           "timing": f"{iters} back-to-back launches between one HIP event pair"}
+    if pmc is not None and pmc.get("SQ_VALU_MFMA_BUSY_CYCLES"):
+        # rocprofv3 counters of the same kernel and shape (tools/pmc_gemm.py)
+        res["mfma_counters"] = {k: pmc.get(k) for k in (
+            "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "mfma_busy_over_issued",
+            "mfma_busy_frac_grbm", "mfma_busy_frac_at_2p4ghz", "effective_clock_ghz_grbm",
+            "kernel_trace_median_us", "l2_hit_rate")}
+    return res
 
 
 def dw_roofline(nat, layer, durations_ms, batch, steps_timed, fused_adam=True, layers=None):
@@ -230,18 +279,15 @@ def dw_roofline(nat, layer, durations_ms, batch, steps_timed, fused_adam=True, l
     ach = nbytes / avg_s / 1e9
     wl = {"dim": nat.enc_widths[0], "batch": batch, "dtype": nat.dtype_name,
           "model": "vib_ae" if nat.vib else "ae", "layer": layer}
-    pmc, src = _pmc_file("dw", wl)
     if len(layers) > 1:
         wl["layers"] = layers
-        pmc, src = _pmc_file("dw", wl)
+    tf, _ = pmc_fields("dw", wl)
     shapes = ", ".join(f"layer {l}: dW[{nat.layers[l]['N']}x{nat.layers[l]['K']}]" for l in layers)
-    kern = "mmad_gemm_kernel"
+    kern = "mmad_gemm"
     return {"kernel": f"{kern} {what} ({shapes} = dz^T a over {rows} windows"
                       f"{'; both layers in one launch' if len(layers) > 1 else ''}; {body})",
             "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4),
-            "traffic": pmc["traffic_bytes_per_launch"] if pmc else None,
-            "traffic_source": src,
+            "frac": round(ach / HBM_PEAK_GBS, 4), **tf,
             "avg_us": round(avg_s * 1e6, 2), "launches_timed": len(durations_ms),
             "algorithmic_bytes_per_launch": nbytes,
             "flops_per_launch": flops,
@@ -262,6 +308,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-probe", action="store_true", help="skip the in-situ kernel probe")
+    ap.add_argument("--no-c2", action="store_true",
+                    help="auto at N=1: skip the c2 sub-object (BASELINE configs[1]) in the same line")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
                     help="set a tune-table knob for the whole run (A/B of schedules; "
                          "icra2021_multimodal_ad_amd._native.KNOB names)")
@@ -275,13 +323,9 @@ def _spawn_entry(rank, world, port, argv):
 
 
 def run(args):
-    import types
     import torch
-    import torch.distributed as dist
     from icra2021_multimodal_ad_amd import dist as mdist
     from icra2021_multimodal_ad_amd import _native
-    from icra2021_multimodal_ad_amd.model_builder import get_model
-    from icra2021_multimodal_ad_amd.data import synth_windows_device
 
     # MMAD_BENCH_SHARED_GPU=1 (harness test only): every rank on cuda:0 over
     # gloo, so the N>1 launch / rendezvous / max-over-ranks / report path can be
@@ -291,7 +335,10 @@ def run(args):
     rank, world, local = mdist.init_from_env(backend="gloo" if shared else None)
     if shared:
         local = 0
-    cname = args.config if args.config != "auto" else ("c2" if world == 1 else "c4")
+    # auto: the largest single-GPU configuration on one GPU (c3 = BASELINE
+    # configs[2], which is also C4's per-GPU shard, where the 1/2/4/8 curve
+    # starts); c4 on several
+    cname = args.config if args.config != "auto" else ("c3" if world == 1 else "c4")
     for kv in args.tune:
         k, v = kv.split("=", 1)
         _native.tune_set(k, int(v))
@@ -305,6 +352,40 @@ def run(args):
     for k in ("model", "dim", "batch"):
         if getattr(args, k) is not None:
             cfgd[k] = getattr(args, k)
+    res, model = train_workload(args, cname, cfgd, rank, world, local, with_cpu=True)
+    if (rank == 0 and world == 1 and args.config == "auto" and not args.no_c2
+            and all(getattr(args, k) is None for k in ("model", "dim", "batch"))):
+        # the smaller BASELINE configs[1] in the same line, so the c2 series of
+        # earlier rounds stays comparable (same steps / warmup, its own probes)
+        del model
+        torch.cuda.synchronize()
+        sub, _ = train_workload(args, "c2", dict(CONFIGS["c2"]), rank, world, local, with_cpu=False)
+        keep = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "model_tflops",
+                "host_enqueue_ms_per_step", "final_loss", "step_spread", "train_step", "roofline",
+                "roofline_encoder_gemm")
+        res["c2"] = {k: sub[k] for k in keep if k in sub}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        if model.dist is not None and model.dist.native:
+            model._native.set_comm(None)
+            model.dist.close()
+        dist.destroy_process_group()
+
+
+def train_workload(args, cname, cfgd, rank, world, local, with_cpu):
+    """W untimed + K timed train steps of one workload; returns (result dict,
+    model).  The probes and the CPU baseline run after the timed region."""
+    import types
+    import torch
+    import torch.distributed as dist
+    from icra2021_multimodal_ad_amd import dist as mdist
+    from icra2021_multimodal_ad_amd import _native
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    from icra2021_multimodal_ad_amd.data import synth_windows_device
+
     model_name, dim, batch = cfgd["model"], cfgd["dim"], cfgd["batch"]
     vib = model_name == "vib_ae"
     torch.cuda.set_device(local)
@@ -489,15 +570,9 @@ def run(args):
             r["in_step_timing"] = (f"executor probe: HIP event pair around the layer-0 forward GEMM inside "
                                    f"{len(fwd_in_step)} eager train steps (its epilogue also finishes the "
                                    f"layer's train-mode BatchNorm in the fused schedule)")
-        if not args.no_cpu_baseline and world == 1:   # host baseline: rank 0 at N=1 only
+        if with_cpu and not args.no_cpu_baseline and world == 1:   # host baseline: rank 0 at N=1 only
             res["cpu_baseline"] = cpu_baseline(dim, batch, vib, budget_s=args.cpu_budget)
-        print(json.dumps(res), flush=True)
-    if world > 1:
-        dist.barrier()
-        if model.dist is not None and model.dist.native:
-            nat.set_comm(None)
-            model.dist.close()
-        dist.destroy_process_group()
+    return res, model
 
 
 def main():

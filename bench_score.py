@@ -120,28 +120,18 @@ def score_gemm_roofline(nat, B, iters=30):
     fl = 2.0 * B * L["K"] * L["N"]
     peak = BF16_PEAK_TFLOPS if nat.dt == _native.BF16 else F32_PEAK_TFLOPS
     # HBM bytes per launch from the newest PMC summary of the same kernel and
-    # shape (tools/score_one.py + tools/pmc_score.py: FETCH_SIZE x2 + WRITE_SIZE)
-    import glob
-    traffic, src = None, None
-    repo = os.path.dirname(os.path.abspath(__file__))
+    # shape taken on THIS build's GEMM sources (tools/gpu_pmc.sh +
+    # tools/pmc_gemm.py); one taken on other sources is reported as prior
+    from bench import pmc_fields
     want = {"dim": nat.enc_widths[0], "batch": B, "dtype": "bf16" if nat.dt == _native.BF16 else "f32",
             "kind": "score"}
-    for f in sorted(glob.glob(os.path.join(repo, "profiles", "*_pmc_score.json")))[::-1]:
-        try:
-            d = json.load(open(f))
-        except (OSError, ValueError):
-            continue
-        if d.get("workload") == want:
-            traffic, src = d["traffic_bytes_per_launch"], os.path.relpath(f, repo)
-            break
-    res = {"kernel": f"mmad_gemm_kernel score (decoder last layer {B}x{L['K']} . "
+    tf, _ = pmc_fields("score", want)
+    res = {"kernel": f"mmad_gemm score (decoder last layer {B}x{L['K']} . "
                      f"{L['N']}x{L['K']}^T + sum (y-x)^2 epilogue)",
            "bound": "mfma", "achieved": round(fl / avg / 1e12, 2), "peak": peak,
-           "unit": "TFLOP/s", "frac": round(fl / avg / 1e12 / peak, 4), "traffic": traffic,
+           "unit": "TFLOP/s", "frac": round(fl / avg / 1e12 / peak, 4), **tf,
            "avg_us": round(avg * 1e6, 2), "flops_per_launch": fl,
            "timing": f"{iters} launches, a HIP event pair around each"}
-    if src:
-        res["traffic_source"] = src
     return res
 
 

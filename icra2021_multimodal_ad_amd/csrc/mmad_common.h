@@ -71,16 +71,30 @@ __device__ __forceinline__ float apply_act(float z, int act, float slope) {
     default: return z;
   }
 }
+// the piecewise-linear activations (LeakyReLU / ReLU / none) as one
+// branch-free form z > 0 ? z : lo(z): inside the fully unrolled GEMM
+// epilogues a per-element `switch` on the (uniform) activation became one
+// scalar branch tree per element -- ~17k instructions of epilogue code, most
+// of a 256x256 tile's epilogue time in instruction fetch.  Same values as
+// apply_act for these three (z * 1 == z exactly; ReLU's 0 is +0).
+__device__ __forceinline__ bool act_is_linear_piecewise(int act) {
+  return act == MMAD_ACT_LEAKYRELU || act == MMAD_ACT_RELU || act == MMAD_ACT_NONE;
+}
+__device__ __forceinline__ float act_lo_slope(int act, float slope) {
+  return act == MMAD_ACT_LEAKYRELU ? slope : (act == MMAD_ACT_NONE ? 1.f : 0.f);
+}
+__device__ __forceinline__ float apply_act_pw(float z, bool relu, float lo_slope) {
+  const float lo = relu ? 0.f : z * lo_slope;
+  return z > 0.f ? z : lo;
+}
 // derivative expressed through the activation OUTPUT a (all supported acts
-// are monotone so the output determines the branch / value)
+// are monotone so the output determines the branch / value); branch-free
+// (selects, no per-element branch tree in unrolled epilogues)
 __device__ __forceinline__ float act_grad_from_out(float a, int act, float slope) {
-  switch (act) {
-    case MMAD_ACT_LEAKYRELU: return a > 0.f ? 1.f : slope;
-    case MMAD_ACT_RELU: return a > 0.f ? 1.f : 0.f;
-    case MMAD_ACT_SIGMOID: return a * (1.f - a);
-    case MMAD_ACT_TANH: return 1.f - a * a;
-    default: return 1.f;
-  }
+  const float pw = a > 0.f ? 1.f : (act == MMAD_ACT_LEAKYRELU ? slope : (act == MMAD_ACT_RELU ? 0.f : 1.f));
+  const float sg = a * (1.f - a);
+  const float th = 1.f - a * a;
+  return act == MMAD_ACT_SIGMOID ? sg : (act == MMAD_ACT_TANH ? th : pw);
 }
 
 // torch.optim.Adam element update (single-tensor formula, amsgrad=False):

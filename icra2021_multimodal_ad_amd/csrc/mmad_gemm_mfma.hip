@@ -68,11 +68,20 @@ template <> struct Cfg<5> { static constexpr int BM = 128, BN = 128, WM = 2, WN 
 // 16384 x 2048 x 1664 vs 0.33 for 256x128); its epilogue staging fills LDS
 constexpr int CFG_BIG = 6;
 template <> struct Cfg<6> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NS = 2, NT = 512; };
-constexpr int NCFG = 7;
-constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256};
-constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256};
-constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512};
-// the 256x256 tile: bf16 operands, forward-type epilogues, no fused BN
+// 7: 256x256, 8 waves (2 x 4, wave tile 128x64), STAGGERED: waves 4-7 run one
+// workgroup barrier behind waves 0-3, so on every SIMD one wave computes
+// (16 MFMAs) while its partner reads its next fragments and issues its share
+// of the LDS-DMA; 32-deep K-tiles in a 4-slot ring (32 KB each), 3 K-tiles in
+// flight (tile7_loop below; CFG 6's loop is the 2-slot, one-barrier-per-stage
+// form it replaces where it measures faster)
+constexpr int CFG_P8 = 7;
+template <> struct Cfg<7> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NS = 2, NT = 512; };
+constexpr int NCFG = 8;
+constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256, 256};
+constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256, 256};
+constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512, 512};
+inline bool is_big(int cfg) { return cfg == CFG_BIG || cfg == CFG_P8; }
+// the 256x256 tiles: bf16 operands, forward-type epilogues, no fused BN
 template <typename T, int EPI>
 constexpr bool big_ok() {
   return sizeof(T) == 2 && (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_MSE || EPI == GEMM_EPI_SCORE);
@@ -217,6 +226,32 @@ __device__ __forceinline__ floatx4 frag_f32(const char* img, int rbase, int kc, 
     }
     return r;
   }
+}
+
+// ---- CFG 7 image: [256 rows][64 B] per operand and K-tile (32 bf16 of K) --
+// 16-byte chunk j of row r stored at j ^ sw64(r).  A ds_read_b128 of 16 rows
+// (lane & 15) x chunk g (lane >> 4) is served in four 16-lane groups, e.g.
+// {0-3, 12-15, 20-27} = rows 0-3 and 12-15 at g, rows 4-11 at g^1; with
+// sw64 = (4 - ((r >> 2) & 3)) & 3 each group's 16 (row, chunk) pairs land on
+// 16 distinct 16-B bank slots of the 256-B bank row (conflict-free).  The
+// DMA writes the image lane-linearly; the swizzle is applied to the per-lane
+// global source address (an involution, undone on the read).
+__device__ __forceinline__ int sw64(int r) { return (4 - ((r >> 2) & 3)) & 3; }
+
+// chunk c (0..1) of one 256-row x 32-k operand image (16 KB = 1024 pieces of
+// 16 B; 512 threads x 2)
+__device__ __forceinline__ void stage64(char* img, const bf16* __restrict__ G, int ld, int r0, int k0,
+                                        int tid, int c) {
+  const int p = c * 512 + tid;
+  const int row = p >> 2;
+  const int j = (p & 3) ^ sw64(row);
+  dma16(G + (size_t)(r0 + row) * ld + k0 + j * 8, img + (c * 512 + (tid & ~63)) * 16);
+}
+
+// 16x16x32 operand fragment: rows rbase + (lane & 15), k = 8g..8g+7 (g = lane >> 4)
+__device__ __forceinline__ bf16x8 frag64(const char* img, int rbase, int lane) {
+  const int m = rbase + (lane & 15);
+  return *(const bf16x8*)(img + m * 64 + (((lane >> 4) ^ sw64(m)) << 4));
 }
 
 // every phase of the main loop pinned in issue order
@@ -406,7 +441,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   constexpr int SLOT = IA::BYTES + IB::BYTES;
   constexpr int NL = IA::CHUNKS + IB::CHUNKS;          // vm ops per thread per stage
   constexpr bool FWDLIKE = EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_MSE || EPI == GEMM_EPI_SCORE;
-  constexpr bool BIG = CFG == CFG_BIG;
+  constexpr bool BIG = CFG == CFG_BIG || CFG == CFG_P8;
   static_assert(!BIG || big_ok<T, EPI>(), "256x256 tile: bf16 forward-type epilogues only");
   // prefetched bias partials per lane (none for the 256x256 tile: its
   // 128 accumulator registers leave no room to hold them across the loop)
@@ -629,7 +664,116 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       for (int r = 0; r < 16; ++r)
         pf_a[u][r] = an[(size_t)(m0 + (grp + u * B_NG) * 16 + r) * ep.ldo + n0 + cc];
   };
-  if constexpr (BIG) {
+  if constexpr (CFG == CFG_P8) {
+    // ---- staggered 256x256 loop ------------------------------------------
+    // K-tile t (32 deep) lives in ring slot t % 4: A image | B image, 16 KB
+    // each.  Per K-tile every wave runs two load segments (L) and two compute
+    // segments (C), each closed by a workgroup barrier:
+    //   L(2t):   B fragments (4 n-tiles) + A top (4 m-tiles); DMA chunk 0 of
+    //            both operands of K-tile t+3 (2 issues)
+    //   C(2t):   16 MFMAs, rows 0..63 of the wave tile
+    //   L(2t+1): A bottom; vmcnt retires K-tile t+1; DMA chunk 1 of t+3
+    //   C(2t+1): 16 MFMAs, rows 64..127
+    // Waves 4-7 (the SIMD partners of waves 0-3) pass one extra barrier first,
+    // so every barrier closes one group's load segment and the other group's
+    // compute segment: each SIMD's matrix pipe is fed by one wave while its
+    // partner loads.  Every load segment ends with lgkmcnt(0), so the reads
+    // of segment L(j) are complete at the barrier that closes it.
+    // Correctness by barrier count (group 0 closes L(j) at barrier 2j, group 1
+    // at 2j+1):
+    //  * WAR: K-tile t+3 overwrites slot (t-1) % 4, last read in L(2t-1) and
+    //    closed by barrier 4t-1 (group 1); its first DMA issue is in L(2t),
+    //    which opens after barrier 4t-1 (group 0) / 4t (group 1).
+    //  * RAW: K-tile u is first read in L(2u), after barrier 4u-1 (group 0) /
+    //    4u (group 1); every wave retires its own DMAs of u with the counted
+    //    vmcnt in L(2u-1), which closes at barrier <= 4u-1, and the DMA data
+    //    is ordered for other waves by that barrier.
+    // The K accumulation order per output element is the same as every other
+    // tile's (32-deep MFMA steps in k order): results are bit-identical.
+    static_assert(sizeof(T) == 2 && AK && BK_ && BM == 256 && BN == 256 && TM == 8 && TN == 4,
+                  "CFG 7: bf16, K-major operands");
+    constexpr int SL = 32768, HB = 16384;
+    const int grp = w >> 2;
+    const int ntk = (ep.dbg & 1) ? 0 : Ks / 32;
+    auto slot = [&](int t) -> char* { return smem + (t & 3) * SL; };
+    // diagnostics (dbg bits, loop studies only): 16 = no DMA inside the loop
+    // (the MFMAs read stale slots), 32 = no MFMAs (accumulators stay live)
+    const bool d_nodma = ep.dbg & 16, d_nomfma = ep.dbg & 32;
+    auto dma = [&](int t, int c) {
+      if (t >= 3 && d_nodma) return;
+      stage64(slot(t), A, lda, m0, kbase + t * 32, tid, c);
+      stage64(slot(t) + HB, B, ldb, n0, kbase + t * 32, tid, c);
+    };
+    if (ntk > 0) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+        if (u < ntk) { dma(u, 0); dma(u, 1); }
+      // K-tile 0 landed (1 and 2 may stay in flight)
+      if (ntk >= 3) wait_vmcnt<8>();
+      else if (ntk == 2) wait_vmcnt<4>();
+      else wait_vmcnt<0>();
+      block_barrier();
+      if (grp) block_barrier();            // the stagger
+      for (int t = 0; t < ntk; ++t) {
+        const char* sa = slot(t);
+        const char* sb = sa + HB;
+        // ---- L(2t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = frag64(sb, rb + j * 16, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = frag64(sa, ra + i * 16, lane);
+        if (t + 3 < ntk) dma(t + 3, 0);
+        wait_lgkm0();
+        MMAD_SB();
+        block_barrier();
+        // ---- C(2t)
+        __builtin_amdgcn_s_setprio(1);
+        if (!d_nomfma) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        } else {
+          asm volatile("" ::"v"(fa[0]), "v"(fa[1]), "v"(fa[2]), "v"(fa[3]), "v"(fb[0]), "v"(fb[1]),
+                       "v"(fb[2]), "v"(fb[3]));
+        }
+        __builtin_amdgcn_s_setprio(0);
+        MMAD_SB();
+        block_barrier();
+        // ---- L(2t+1)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = frag64(sa, ra + (4 + i) * 16, lane);
+        if (t + 1 < ntk) {
+          // retire K-tile t+1: newer in flight are K-tile t+2 (4 issues) and
+          // chunk 0 of t+3 (2), where they exist
+          if (t + 3 < ntk) wait_vmcnt<6>();
+          else if (t + 2 < ntk) wait_vmcnt<4>();
+          else wait_vmcnt<0>();
+        }
+        if (t + 3 < ntk) dma(t + 3, 1);
+        wait_lgkm0();
+        MMAD_SB();
+        block_barrier();
+        // ---- C(2t+1)
+        __builtin_amdgcn_s_setprio(1);
+        if (!d_nomfma) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[4 + i][j], 0, 0, 0);
+        } else {
+          asm volatile("" ::"v"(fa[0]), "v"(fa[1]), "v"(fa[2]), "v"(fa[3]));
+        }
+        __builtin_amdgcn_s_setprio(0);
+        MMAD_SB();
+        block_barrier();
+      }
+      if (!grp) block_barrier();           // both groups: 4 * ntk + 2 barriers
+    }
+  } else if constexpr (BIG) {
     // 256x256 tile (bf16, both operands K-major): a 2-slot ring, one barrier
     // per stage after both 32-deep sub-steps; the fragment registers of a
     // sub-step are re-read row by row under the MFMAs that free them (their
@@ -929,6 +1073,13 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         }
     }
   }
+  // the register phase, instantiated twice: PW = the piecewise-linear
+  // activations (branch-free, the hot path), else the general one (sigmoid /
+  // tanh; FWD / SCORE only -- the other epilogues apply no activation)
+  const bool pw_relu = ep.act == MMAD_ACT_RELU;
+  const float pw_lo = act_lo_slope(ep.act, ep.slope);
+  auto reg_phase = [&](auto pw_c) {
+    constexpr bool PW = decltype(pw_c)::value;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = cw + j * 16 + c;
@@ -960,7 +1111,9 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         const bool valid = cvalid && row < ep.M;
         float v = acc[i][j][r];
         if (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_SCORE) {
-          v = fmaf(apply_act(v + bias, ep.act, ep.slope), sc, sh);   // pinned: tile-independent
+          // pinned: tile-independent
+          if constexpr (PW) v = fmaf(apply_act_pw(v + bias, pw_relu, pw_lo), sc, sh);
+          else v = fmaf(apply_act(v + bias, ep.act, ep.slope), sc, sh);
           v = valid ? v : 0.f;
           s1[i >> 1] += v;
         } else if (EPI == GEMM_EPI_MSE) {
@@ -1025,6 +1178,10 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
     }
   }
 
+  };
+  if (!FWDLIKE || EPI == GEMM_EPI_MSE || act_is_linear_piecewise(ep.act)) reg_phase(std::true_type{});
+  else reg_phase(std::false_type{});
+
   // ===================== epilogue, LDS-staged coalesced store ===============
   // fused BN (forward): the Welford partials are out -- arrive at the column
   // barrier now, store the a tile while the other blocks catch up
@@ -1056,16 +1213,19 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       __syncthreads();
     }
   }
+  // (dbg 128, epilogue studies: no LDS staging writes)
+  if (!(ep.dbg & 128)) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int rl = wm * 16 * TM + i * 16 + 4 * g + r;
-        const int cl = wn * 16 * TN + j * 16 + c;
-        *(TO*)(smem + rl * OSTRIDE + cl * (int)sizeof(TO)) = from_f32<TO>(acc[i][j][r]);
-      }
+        for (int r = 0; r < 4; ++r) {
+          const int rl = wm * 16 * TM + i * 16 + 4 * g + r;
+          const int cl = wn * 16 * TN + j * 16 + c;
+          *(TO*)(smem + rl * OSTRIDE + cl * (int)sizeof(TO)) = from_f32<TO>(acc[i][j][r]);
+        }
+  }
   __syncthreads();
   constexpr int CPR = BN * (int)sizeof(TO) / 16;  // 16-byte chunks per output row
   constexpr int OEPC = 16 / (int)sizeof(TO);
@@ -1163,7 +1323,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
       const int row = m0 + rl;
       const int col = n0 + ch * OEPC;
-      if (out) {
+      if (out && !(ep.dbg & 64)) {   // (dbg 64, epilogue studies: no output stores)
         *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
       }
       if constexpr (EPI == GEMM_EPI_SCORE) {
@@ -1556,7 +1716,7 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
 // -------------------------------------------------------------------------
 static bool cfg_fits(int cfg, int Mp, int Np, int epi, int dtype) {
   if (Mp % CFG_BM[cfg] || Np % CFG_BN[cfg]) return false;
-  if (cfg == CFG_BIG && !big_ok_rt(dtype, epi)) return false;
+  if (is_big(cfg) && !big_ok_rt(dtype, epi)) return false;
   // the score epilogue reduces rows over 128-column groups inside one tile
   if (epi == GEMM_EPI_SCORE && CFG_BN[cfg] < 128) return false;
   return true;
@@ -1623,7 +1783,8 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
     case 5: go(mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI>); break;
     default:
       if constexpr (big_ok<T, EPI>()) {
-        go(mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI>);
+        if (cfg == CFG_P8) go(mmad_gemm_kernel<T, TO, AK, BK_, CFG_P8, EPI>);
+        else go(mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI>);
       } else {
         mmad_set_error("gemm: tile configuration %d does not support this dtype / epilogue", cfg);
         return MMAD_EUNSUPPORTED;
@@ -1645,7 +1806,9 @@ static const void* kernel_ptr(int cfg) {
     case 4: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI>;
     case 5: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI>;
     default:
-      if constexpr (big_ok<T, EPI>()) return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI>;
+      if constexpr (big_ok<T, EPI>())
+        return cfg == CFG_P8 ? (const void*)mmad_gemm_kernel<T, TO, AK, BK_, CFG_P8, EPI>
+                             : (const void*)mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI>;
       return nullptr;
   }
 }
@@ -1702,7 +1865,7 @@ bool mmad_gemm_bn_fusable(int dtype, int epi, int Mp, int Np) {
   if (epi != GEMM_EPI_FWD && epi != GEMM_EPI_BWD_DATA) return false;
   if (Mp % 128 || Np % 128 || Np / 64 > MMAD_BN_EXIT) return false;
   for (int c = 0; c < NCFG; ++c)
-    if (cfg_fits(c, Mp, Np, epi, dtype) && c != CFG_BIG && coresident(dtype, epi, c, Mp, Np)) return true;
+    if (cfg_fits(c, Mp, Np, epi, dtype) && !is_big(c) && coresident(dtype, epi, c, Mp, Np)) return true;
   return false;
 }
 
@@ -1761,7 +1924,7 @@ static int tune_cfg(int dtype, int epi, const void* A, int lda, const void* B, i
   int rc = MMAD_OK;
   for (int c = 0; c < NCFG && rc == MMAD_OK; ++c) {
     if (!cfg_fits(c, Mp, Np, epi, dtype)) continue;
-    if (c == CFG_BIG && (ep.bn_sync || ep.splitk > 1)) continue;   // no fused BN / split on 256x256
+    if (is_big(c) && (ep.bn_sync || ep.splitk > 1)) continue;   // no fused BN / split on 256x256
     if (ep.bn_sync && !coresident(dtype, epi, c, Mp, Np)) continue;
     rc = launch_cfg(dtype, epi, A, lda, B, ldb, Mp, Np, K, et, c, s);   // warm
     if (rc != MMAD_OK) break;
@@ -1883,8 +2046,8 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   ep.splitk = (ep.sk_slab && ep.sk_ctl && !bnf) ? mmad_gemm_splitk(Mp, Np, K, dtype, epi) : 1;
   auto allowed = [&](int c) {
     return c >= 0 && c < NCFG && cfg_fits(c, Mp, Np, epi, dtype) &&
-           (c != CFG_BIG || ep.splitk <= 1) &&
-           (!bnf || (c != CFG_BIG && coresident(dtype, epi, c, Mp, Np)));
+           (!is_big(c) || ep.splitk <= 1) &&
+           (!bnf || (!is_big(c) && coresident(dtype, epi, c, Mp, Np)));
   };
   const int env = mmad_tile_override();
   const int env_epi = ep.ad_p ? mmad_tile_adam_for(Mp, Np, K) : mmad_tile_epi_override(epi);

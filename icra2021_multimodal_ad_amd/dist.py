@@ -221,10 +221,14 @@ class DataParallel:
     torch.distributed.  ``_fail`` (tests): inject a failure on this rank at
     'uid' / 'create' / 'selftest'."""
 
-    def __init__(self, group=None, native=None, _fail=None):
+    def __init__(self, group=None, native=None, _fail=None, overlap=None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.comm = None
+        # torch exchange form (see `overlap` below): read here, not at import,
+        # so a launcher that sets MMAD_DP_OVERLAP after importing the package
+        # gets it (as MMAD_DP_GRAD_BF16 is read in attach_data_parallel)
+        self.overlap = (os.environ.get("MMAD_DP_OVERLAP", "0") == "1") if overlap is None else bool(overlap)
         if native is None:
             native = (self.world > 1 and torch.cuda.is_available()
                       and dist.get_backend(group) == "nccl"
@@ -275,8 +279,9 @@ class DataParallel:
     # faster at D=2048 / 1024 windows per rank (13.4 vs 16.6 ms/step) but
     # 4.2 s/step at the C4 shape (VIB, 4096 windows) against 18 ms serial
     # (profiles/r07g_torch_exchange_gloo.txt): the fallback keeps the form
-    # that measured well everywhere; env MMAD_DP_OVERLAP=1 opts in
-    overlap = os.environ.get("MMAD_DP_OVERLAP", "0") == "1"
+    # that measured well everywhere; env MMAD_DP_OVERLAP=1 (read when the
+    # DataParallel is built) or attach_data_parallel(overlap=True) opts in
+    overlap = False
 
     def all_reduce_grads(self, flat_grads):
         if self.world > 1:
@@ -298,12 +303,15 @@ class DataParallel:
         backward; the current stream joins every bucket stream.  Adam is
         elementwise and a 2-rank sum is order-free, so at 2 ranks this is the
         serial form's result bit for bit (tests/test_gpu_dp.py)."""
-        nat.adam_step_count += 1
-        step = nat.adam_step_count
+        # the step count advances only once every collective and Adam call of
+        # this step has been issued: a collective that raises (e.g. a gloo
+        # timeout) leaves it, and the mirrored optimizer 'step', unchanged
+        step = nat.adam_step_count + 1
         if not self.overlapped:
             self.all_reduce_grads(nat.grads)
             self.all_reduce_loss(loss)
             nat.adam(lr=lr, betas=betas, eps=eps, step=step)
+            nat.adam_step_count = step
             return
         cur = torch.cuda.current_stream()
         plan = getattr(nat, "_dw_plan", None)
@@ -331,6 +339,7 @@ class DataParallel:
         nat.adam_range(nat.n_weight, nat.n_params - nat.n_weight, lr=lr, betas=betas, eps=eps, step=step)
         for _, s, _, _ in pending:
             cur.wait_stream(s)
+        nat.adam_step_count = step
         nat._mark_synced()
 
     def all_reduce_loss(self, loss):
@@ -376,14 +385,15 @@ class DataParallel:
             dist.broadcast(model._native.params, src=src, group=self.group)
 
 
-def attach_data_parallel(model, group=None, native=None, grad_bf16=None):
+def attach_data_parallel(model, group=None, native=None, grad_bf16=None, overlap=None):
     """Replicate rank-0 weights and make AutoEncoder.step all-reduce grads
     (natively over RCCL, overlapped with the backward, when the process group
     is 'nccl'; through torch.distributed otherwise).  grad_bf16 (native path;
     default: env MMAD_DP_GRAD_BF16=1, else off): reduce-scatter the weight
     gradients in bf16 (mmad_ae_set_grad_bf16, half the exchange bytes; not the
-    reference's fp32 sum)."""
-    dp = DataParallel(group, native=native)
+    reference's fp32 sum).  overlap (torch exchange; default: env
+    MMAD_DP_OVERLAP=1, else off): the per-bucket overlapped all-reduce + Adam."""
+    dp = DataParallel(group, native=native, overlap=overlap)
     dp.broadcast_params(model)
     if dp.world > 1:
         model._native.sync_shadow(force=True)

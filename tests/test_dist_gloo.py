@@ -1,8 +1,12 @@
 """Data-parallel protocol on CPU: world_size=2 over gloo (127.0.0.1).
 
-The GPU exchange is the same code path with the 'nccl' (RCCL) backend: one sum
-all-reduce of the flat fp32 gradient buffer per step, parameters broadcast
-from rank 0 at attach time.  Checked here: (1) the all-reduced gradient of
+On the GPU with the 'nccl' group the default exchange is the native RCCL one
+(dist.NativeComm attached to the executor): per bucket of consecutive layers a
+reduce-scatter of the fp32 weight gradients, Adam on this rank's 1/N slice,
+an all-gather of the bf16 shadow (ZeRO-1), plus one all-reduce of the small
+bucket (bias / gamma / beta + loss); parameters are broadcast from rank 0 at
+attach time.  The torch fallback checked here (gloo) sums the flat gradient
+with one all-reduce -- both are the sum of the per-shard gradients.  Checked here: (1) the all-reduced gradient of
 two shards equals the gradient of the concatenated batch (sum-reduced loss),
 computed with the CPU oracle per shard; (2) after attach, both ranks hold
 rank-0's parameters."""
@@ -188,3 +192,32 @@ def test_rank_local_guard():
     # the guard follows the executor's communicator, not only model.dist
     # (tests/test_gpu_dp.py::test_rank_local_guard_follows_the_attached_communicator)
     assert "assert_collective_context" in src and "nat, \"_comm\"" in src
+
+
+def test_exchange_failure_leaves_adam_step_count(monkeypatch):
+    """A collective that raises inside DataParallel.exchange_and_adam (e.g. a
+    gloo timeout) must not advance the Adam step count: a caller that catches
+    the error and continues would otherwise run bias correction one step off.
+    The count advances once the collectives and Adam calls are issued."""
+    import types
+
+    import pytest
+    from icra2021_multimodal_ad_amd import dist as mdist
+    monkeypatch.setenv("MMAD_DP_OVERLAP", "1")
+    dp = mdist.DataParallel()                 # no process group: world 1
+    assert dp.overlap is True                 # env read when built, not at import
+    assert mdist.DataParallel(overlap=False).overlap is False
+    dp.overlap = False
+    calls = []
+    nat = types.SimpleNamespace(adam_step_count=7, grads=torch.zeros(4),
+                                adam=lambda **kw: calls.append(kw["step"]))
+
+    def boom(_):
+        raise RuntimeError("collective timed out")
+    monkeypatch.setattr(dp, "all_reduce_grads", boom)
+    with pytest.raises(RuntimeError, match="timed out"):
+        dp.exchange_and_adam(nat, torch.zeros(()), 1e-3, (0.9, 0.999), 1e-8)
+    assert nat.adam_step_count == 7 and calls == []
+    monkeypatch.setattr(dp, "all_reduce_grads", lambda g: None)
+    dp.exchange_and_adam(nat, torch.zeros(()), 1e-3, (0.9, 0.999), 1e-8)
+    assert nat.adam_step_count == 8 and calls == [8]
