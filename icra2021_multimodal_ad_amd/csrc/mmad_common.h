@@ -121,6 +121,30 @@ __device__ __forceinline__ void adam4(floatx4& p, floatx4& m, floatx4& v, floatx
   }
 }
 
+// v[lane ^ 16] and v[lane ^ 32] for every lane of the wave through the gfx950
+// lane-swap VALU ops (v_permlane16_swap_b32: odd 16-lane rows of vdst <->
+// even rows of vsrc; v_permlane32_swap_b32: lanes 32-63 of vdst <-> lanes
+// 0-31 of vsrc), called with vdst = vsrc = v: one VALU op + a select, no LDS
+// round trip (__shfl_xor lowers to ds_bpermute_b32, ~100+ cycles of latency
+// per dependent step in the GEMM epilogues' column reductions).  The values
+// are exactly those of __shfl_xor(v, 16 / 32) (tools/permlane_check.hip).
+__device__ __forceinline__ float lane_xor16(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (__lane_id() & 16) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float lane_xor32(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (__lane_id() & 32) ? r[0] : r[1]);
+}
+// (x + x^16) + (x^32 + x^48) in every lane: the same association as
+// x += shfl_xor(x, 16); x += shfl_xor(x, 32)
+__device__ __forceinline__ float sum_lane_groups(float x) {
+  x += lane_xor16(x);
+  return x + lane_xor32(x);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
