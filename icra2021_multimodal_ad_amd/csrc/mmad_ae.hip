@@ -745,7 +745,7 @@ static BiasSrc bias_src(const mmad_ae* h, const AeWS& w, int l, bool from_mse) {
   return {s.stats, Mp / MMAD_PART_ROWS, 2 * a.Np};  // bwd-data epilogue column sums
 }
 
-struct AdamHyper { float b1, b2, eps, step_size, bc2_sqrt; };
+using AdamHyper = MmadAdamConsts;   // w1 = float(1 - beta1), w2 = float(1 - beta2), ...
 
 // backward through every layer.  from_mse: the last layer's dz and bias
 // partials come from the MSE-fused forward epilogue; otherwise the caller has
@@ -787,8 +787,8 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       // it only when asked (h->keep_grads)
       e.dw_nostore = h->keep_grads ? 0 : 1;
     }
-    e.ad_b1 = adam->b1;
-    e.ad_b2 = adam->b2;
+    e.ad_w1 = adam->w1;
+    e.ad_w2 = adam->w2;
     e.ad_eps = adam->eps;
     e.ad_step = adam->step_size;
     e.ad_bc2 = adam->bc2_sqrt;
@@ -943,8 +943,8 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       MMAD_HIP_CHECK(hipStreamWaitEvent(h->cstream, h->ev_small, 0));
       const int64_t ns = h->n_params - h->n_weight;
       RET_IF(mmad_allreduce_pair(h->comm, h->grads + h->n_weight, ns, dp_loss, 1, h->cstream));
-      RET_IF(mmad_adam(ns, h->params + h->n_weight, h->grads + h->n_weight, h->m + h->n_weight,
-                       h->v + h->n_weight, adam->b1, adam->b2, adam->eps, adam->step_size,
+      RET_IF(mmad_adam_w(ns, h->params + h->n_weight, h->grads + h->n_weight, h->m + h->n_weight,
+                       h->v + h->n_weight, adam->w1, adam->w2, adam->eps, adam->step_size,
                        adam->bc2_sqrt, nullptr, 0, h->cstream));
     }
     if (bk) {
@@ -974,8 +974,8 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
             RET_IF(mmad_reduce_scatter_bucket(h->comm, h->grads + boff, n, h->cstream));
           }
           void* sh = h->dtype == MMAD_BF16 ? (void*)((char*)h->shadow + off * 2) : nullptr;
-          RET_IF(mmad_adam(cnt, h->params + off, h->grads + off, h->m + off, h->v + off, adam->b1,
-                           adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt, sh,
+          RET_IF(mmad_adam_w(cnt, h->params + off, h->grads + off, h->m + off, h->v + off, adam->w1,
+                           adam->w2, adam->eps, adam->step_size, adam->bc2_sqrt, sh,
                            h->dtype == MMAD_BF16 ? cnt : 0, h->cstream));
           if (h->dtype == MMAD_BF16)
             RET_IF(mmad_all_gather_bucket(h->comm, (char*)h->shadow + boff * 2, n, MMAD_BF16, h->cstream));
@@ -985,8 +985,8 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
         } else {
           RET_IF(mmad_allreduce_bucket(h->comm, h->grads + boff, n, h->cstream));
           void* sh = adam_shadow(h, a, w.ping);
-          RET_IF(mmad_adam(n, h->params + boff, h->grads + boff, h->m + boff, h->v + boff,
-                           adam->b1, adam->b2, adam->eps, adam->step_size, adam->bc2_sqrt,
+          RET_IF(mmad_adam_w(n, h->params + boff, h->grads + boff, h->m + boff, h->v + boff,
+                           adam->w1, adam->w2, adam->eps, adam->step_size, adam->bc2_sqrt,
                            sh, h->dtype == MMAD_BF16 ? n : 0, h->cstream));
         }
       }
@@ -1085,9 +1085,7 @@ int mmad_ae_train_fwd_bwd(mmad_ae* h, const float* x, int ld_x, int B, int k, co
 }
 
 static AdamHyper adam_hyper(float lr, float b1, float b2, float eps, int step) {
-  const double bc1 = 1.0 - pow((double)b1, step);
-  const double bc2 = 1.0 - pow((double)b2, step);
-  return AdamHyper{b1, b2, eps, (float)(lr / bc1), (float)sqrt(bc2)};
+  return mmad_adam_consts(lr, b1, b2, eps, step);
 }
 
 int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const float* eps,
@@ -1327,7 +1325,7 @@ int mmad_ae_adam(mmad_ae* h, float lr, float beta1, float beta2, float eps, int 
   MMAD_CHECK_ARG(h && h->params && h->grads && h->m && h->v, "ae_adam: unbound handle");
   MMAD_CHECK_ARG(step >= 1, "ae_adam: step must be >= 1");
   const AdamHyper ah = adam_hyper(lr, beta1, beta2, eps, step);
-  return mmad_adam(h->n_params, h->params, h->grads, h->m, h->v, beta1, beta2, eps, ah.step_size,
+  return mmad_adam_w(h->n_params, h->params, h->grads, h->m, h->v, ah.w1, ah.w2, eps, ah.step_size,
                    ah.bc2_sqrt, h->dtype == MMAD_BF16 ? h->shadow : nullptr,
                    h->dtype == MMAD_BF16 ? h->n_weight : 0, stream);
 }
@@ -1346,7 +1344,7 @@ int mmad_ae_adam_range(mmad_ae* h, float lr, float beta1, float beta2, float eps
     sh = (char*)h->shadow + off * 2;
     nsh = h->n_weight - off < n ? h->n_weight - off : n;
   }
-  return mmad_adam(n, h->params + off, h->grads + off, h->m + off, h->v + off, beta1, beta2, eps,
+  return mmad_adam_w(n, h->params + off, h->grads + off, h->m + off, h->v + off, ah.w1, ah.w2, eps,
                    ah.step_size, ah.bc2_sqrt, sh, nsh, stream);
 }
 

@@ -287,7 +287,8 @@ int mmad_fc_bwd_weight_adam(int dtype, int Mp, int Np, int Kp, const void* dz, c
   GemmEpi ep{};
   ep.M = Np; ep.N = Kp; ep.out = dw; ep.ldo = Kp;
   ep.ad_p = p; ep.ad_m = m; ep.ad_v = v; ep.ad_shadow = shadow;
-  ep.ad_b1 = beta1; ep.ad_b2 = beta2; ep.ad_eps = eps; ep.ad_step = step_size; ep.ad_bc2 = bc2_sqrt;
+  const MmadAdamConsts c = mmad_adam_consts(1e-3f, beta1, beta2, eps, 1);   // w1 / w2 only
+  ep.ad_w1 = c.w1; ep.ad_w2 = c.w2; ep.ad_eps = eps; ep.ad_step = step_size; ep.ad_bc2 = bc2_sqrt;
   ep.dw_nostore = dw ? 0 : 1;
   return layer_gemm(dtype, GEMM_EPI_BWD_WEIGHT, dz, Np, x, Kp, Np, Kp, Mp, ep, stream);
 }

@@ -97,24 +97,38 @@ __device__ __forceinline__ float act_grad_from_out(float a, int act, float slope
   return act == MMAD_ACT_SIGMOID ? sg : (act == MMAD_ACT_TANH ? th : pw);
 }
 
-// torch.optim.Adam element update (single-tensor formula, amsgrad=False):
-// m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2; p -= step * m / (sqrt(v)/bc2 + eps).
-// Contractions pinned with fmaf so every kernel that fuses an Adam update
-// (flat Adam, dW-epilogue Adam) produces bit-identical results.
-__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float b1,
-                                          float b2, float eps, float step, float bc2) {
-  m = fmaf(b1, m, (1.f - b1) * g);
-  v = fmaf(b2, v, ((1.f - b2) * g) * g);
-  const float denom = __fsqrt_rn(v) / bc2 + eps;
-  p = fmaf(-step, __fdiv_rn(m, denom), p);
+// torch.optim.Adam element update, as torch's _single_tensor_adam computes it
+// on the CPU (the reference's optimizer, novelty_detection.py:90) -- every
+// rounding step in torch's order (checked against torch 2.10 CPU kernels):
+//   exp_avg.lerp_(g, 1 - b1)            m = fma(w1, g - m, m)   (w1 < 0.5)
+//   exp_avg_sq.mul_(b2).addcmul_(g, g, value=1 - b2)
+//                                       v = fma(w2 * g, g, v * b2)
+//   denom = (exp_avg_sq.sqrt() / bc2_sqrt).add_(eps)
+//   param.addcdiv_(exp_avg, denom, value=-step_size)
+//                                       p = p + (-step_size * m) / denom
+// w1 = float(1 - b1), w2 = float(1 - b2) are formed from the DOUBLE betas
+// (mmad_adam_consts: the decimal the float came from); b2 = float(1 - w2)
+// recovers torch's float(beta2) exactly.  Until round 5 the update was
+// m = fma(b1, m, (1 - b1) g), v = fma(b2, v, (1 - b2) g^2) with 1 - b
+// formed in float (1 - 0.999f = 0.00099998713, 1.3e-5 below torch's 0.001)
+// and bc2 from the float beta2: a systematic ~-5e-6 relative step size that
+// the teacher-forced test (tests/test_gpu_teacher.py) found.
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, float w1,
+                                          float w2, float eps, float step, float bc2) {
+  const float b2 = (float)(1.0 - (double)w2);
+  const float d = g - m;
+  m = w1 < 0.5f ? fmaf(w1, d, m) : fmaf(w1 - 1.f, d, g);
+  v = fmaf(w2 * g, g, v * b2);
+  const float denom = __fdiv_rn(__fsqrt_rn(v), bc2) + eps;
+  p = p + __fdiv_rn(-step * m, denom);
 }
 
-__device__ __forceinline__ void adam4(floatx4& p, floatx4& m, floatx4& v, floatx4 g, float b1,
-                                      float b2, float eps, float step, float bc2) {
+__device__ __forceinline__ void adam4(floatx4& p, floatx4& m, floatx4& v, floatx4 g, float w1,
+                                      float w2, float eps, float step, float bc2) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     float pe = p[e], me = m[e], ve = v[e];
-    adam_elem(pe, me, ve, g[e], b1, b2, eps, step, bc2);
+    adam_elem(pe, me, ve, g[e], w1, w2, eps, step, bc2);
     p[e] = pe;
     m[e] = me;
     v[e] = ve;

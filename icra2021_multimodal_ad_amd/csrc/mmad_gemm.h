@@ -60,7 +60,7 @@ struct GemmEpi {
   float* ad_m;
   float* ad_v;
   void* ad_shadow;
-  float ad_b1, ad_b2, ad_eps, ad_step, ad_bc2;
+  float ad_w1, ad_w2, ad_eps, ad_step, ad_bc2;   // Adam: w = float(1 - beta) (mmad_adam_consts)
   int dw_nostore;        // with ad_p: do not materialise dW (Adam consumed it)
   // ... and the layer's small segment [bias | gamma | beta], spread over all
   // blocks; the first bNp elements take g = sum of bias partials.

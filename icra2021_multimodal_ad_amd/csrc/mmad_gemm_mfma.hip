@@ -1268,7 +1268,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         const int rl = idx / CPR, ch = idx % CPR;
         const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
         if (!ep.dw_nostore) *(uint4v*)(out + off[u]) = v;
-        adam4(P[u], Mm[u], Vv[u], __builtin_bit_cast(floatx4, v), ep.ad_b1, ep.ad_b2, ep.ad_eps,
+        adam4(P[u], Mm[u], Vv[u], __builtin_bit_cast(floatx4, v), ep.ad_w1, ep.ad_w2, ep.ad_eps,
               ad_step, ad_bc2);
         bf16x4 sh;
 #pragma unroll
@@ -1488,7 +1488,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
           mm = ep.sm_m[n];
           vv = ep.sm_v[n];
         }
-        adam_elem(pp, mm, vv, g, ep.ad_b1, ep.ad_b2, ep.ad_eps, ad_step, ad_bc2);
+        adam_elem(pp, mm, vv, g, ep.ad_w1, ep.ad_w2, ep.ad_eps, ad_step, ad_bc2);
         ep.sm_p[n] = pp;
         ep.sm_m[n] = mm;
         ep.sm_v[n] = vv;
@@ -1499,7 +1499,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         // the first chunk was read before the main loop
         const int i4 = ep.sm_bNp + q * 4;
         floatx4 pp = smq_p, mm = smq_m, vv = smq_v;
-        adam4(pp, mm, vv, smq_g, ep.ad_b1, ep.ad_b2, ep.ad_eps, ad_step, ad_bc2);
+        adam4(pp, mm, vv, smq_g, ep.ad_w1, ep.ad_w2, ep.ad_eps, ad_step, ad_bc2);
         *(floatx4*)(ep.sm_p + i4) = pp;
         *(floatx4*)(ep.sm_m + i4) = mm;
         *(floatx4*)(ep.sm_v + i4) = vv;
@@ -1510,7 +1510,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         const floatx4 gg = *(const floatx4*)(ep.sm_g + i4);
         floatx4 pp = *(floatx4*)(ep.sm_p + i4), mm = *(floatx4*)(ep.sm_m + i4);
         floatx4 vv = *(floatx4*)(ep.sm_v + i4);
-        adam4(pp, mm, vv, gg, ep.ad_b1, ep.ad_b2, ep.ad_eps, ad_step, ad_bc2);
+        adam4(pp, mm, vv, gg, ep.ad_w1, ep.ad_w2, ep.ad_eps, ad_step, ad_bc2);
         *(floatx4*)(ep.sm_p + i4) = pp;
         *(floatx4*)(ep.sm_m + i4) = mm;
         *(floatx4*)(ep.sm_v + i4) = vv;

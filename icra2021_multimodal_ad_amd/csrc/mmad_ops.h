@@ -45,11 +45,20 @@ struct MmadAdamSeg {
   float* p; float* g; float* m; float* v; void* shadow; int64_t n;
   const float* bsrc; int bparts, bstride, bN, bNp;
 };
-// mmad_adam with the step terms read from `dyn` when non-null (graph capture)
-int mmad_adam_dyn(int64_t n, float* p, const float* g, float* m, float* v, float beta1, float beta2,
+// Adam constants as torch.optim.Adam forms them from its double hyper-
+// parameters (recovered from the floats: mmad_decimal_of); w = float(1 - beta)
+struct MmadAdamConsts { float w1, w2, eps, step_size, bc2_sqrt; };
+double mmad_decimal_of(float f);
+MmadAdamConsts mmad_adam_consts(float lr, float beta1, float beta2, float eps, int step);
+// flat Adam with the constants already formed (w1, w2: MmadAdamConsts)
+int mmad_adam_w(int64_t n, float* p, const float* g, float* m, float* v, float w1, float w2,
+                float eps, float step_size, float bc2_sqrt, void* shadow, int64_t n_shadow,
+                void* stream);
+// mmad_adam_w with the step terms read from `dyn` when non-null (graph capture)
+int mmad_adam_dyn(int64_t n, float* p, const float* g, float* m, float* v, float w1, float w2,
                   float eps, float step_size, float bc2_sqrt, void* shadow, int64_t n_shadow,
                   const MmadDyn* dyn, void* stream);
-int mmad_adam2(const MmadAdamSeg& s0, const MmadAdamSeg& s1, float beta1, float beta2, float eps,
+int mmad_adam2(const MmadAdamSeg& s0, const MmadAdamSeg& s1, float w1, float w2, float eps,
                float step_size, float bc2_sqrt, void* stream);
 
 int mmad_bn_finalize(int M, int N, int Mp, int Np, const float* stats, const float* gamma,

@@ -6,6 +6,10 @@
 #include "mmad_common.h"
 #include "mmad_ops.h"
 
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+
 #define SLAB_COLS 64
 #define SLAB_ROWS 128
 
@@ -633,7 +637,7 @@ __global__ void sse_k(int M, int N, int Np, const T* __restrict__ y, const float
 // Adam (torch.optim.Adam, single-tensor formula) over a flat buffer
 __global__ __launch_bounds__(256) void adam_k(int64_t n, float* __restrict__ p,
                                               const float* __restrict__ g, float* __restrict__ m,
-                                              float* __restrict__ v, float b1, float b2, float eps,
+                                              float* __restrict__ v, float w1, float w2, float eps,
                                               float step_size, float bc2_sqrt, bf16* shadow,
                                               int64_t n_shadow, const MmadDyn* dyn) {
   const int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
@@ -645,7 +649,7 @@ __global__ __launch_bounds__(256) void adam_k(int64_t n, float* __restrict__ p,
   if (i4 + 4 <= n) {
     floatx4 pp = *(floatx4*)(p + i4), gg = *(const floatx4*)(g + i4);
     floatx4 mm = *(floatx4*)(m + i4), vv = *(floatx4*)(v + i4);
-    adam4(pp, mm, vv, gg, b1, b2, eps, step_size, bc2_sqrt);
+    adam4(pp, mm, vv, gg, w1, w2, eps, step_size, bc2_sqrt);
     *(floatx4*)(p + i4) = pp;
     *(floatx4*)(m + i4) = mm;
     *(floatx4*)(v + i4) = vv;
@@ -658,7 +662,7 @@ __global__ __launch_bounds__(256) void adam_k(int64_t n, float* __restrict__ p,
   } else {
     for (int64_t i = i4; i < n; ++i) {
       float pp = p[i], mm = m[i], vv = v[i];
-      adam_elem(pp, mm, vv, g[i], b1, b2, eps, step_size, bc2_sqrt);
+      adam_elem(pp, mm, vv, g[i], w1, w2, eps, step_size, bc2_sqrt);
       p[i] = pp;
       m[i] = mm;
       v[i] = vv;
@@ -721,7 +725,7 @@ __global__ __launch_bounds__(256) void reduce_jobs_k(MmadReduceJobs jobs) {
 }
 
 // Adam over two flat segments (a layer's weights and its bias/gamma/beta)
-__global__ __launch_bounds__(256) void adam2_k(MmadAdamSeg s0, MmadAdamSeg s1, float b1, float b2,
+__global__ __launch_bounds__(256) void adam2_k(MmadAdamSeg s0, MmadAdamSeg s1, float w1, float w2,
                                                float eps, float step_size, float bc2_sqrt) {
   int64_t i4 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
   const MmadAdamSeg* sg = &s0;
@@ -746,7 +750,7 @@ __global__ __launch_bounds__(256) void adam2_k(MmadAdamSeg s0, MmadAdamSeg s1, f
     gg = *(const floatx4*)g;
   }
   floatx4 pp = *(floatx4*)p, mm = *(floatx4*)m, vv = *(floatx4*)v;
-  adam4(pp, mm, vv, gg, b1, b2, eps, step_size, bc2_sqrt);
+  adam4(pp, mm, vv, gg, w1, w2, eps, step_size, bc2_sqrt);
   *(floatx4*)p = pp;
   *(floatx4*)m = mm;
   *(floatx4*)v = vv;
@@ -943,12 +947,12 @@ int mmad_reduce_jobs(const MmadReduceJobs& jobs, int n_jobs, int max_np, void* s
   return MMAD_OK;
 }
 
-int mmad_adam2(const MmadAdamSeg& s0, const MmadAdamSeg& s1, float beta1, float beta2, float eps,
+int mmad_adam2(const MmadAdamSeg& s0, const MmadAdamSeg& s1, float w1, float w2, float eps,
                float step_size, float bc2_sqrt, void* stream) {
   MMAD_CHECK_ARG(s0.n % 4 == 0 && s1.n % 4 == 0, "adam2: segment lengths must be multiples of 4");
   const int64_t n4 = (s0.n + s1.n) / 4;
   if (n4 == 0) return MMAD_OK;
-  adam2_k<<<nblk(n4, 256), 256, 0, (hipStream_t)stream>>>(s0, s1, beta1, beta2, eps, step_size,
+  adam2_k<<<nblk(n4, 256), 256, 0, (hipStream_t)stream>>>(s0, s1, w1, w2, eps, step_size,
                                                           bc2_sqrt);
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
@@ -1093,20 +1097,48 @@ int mmad_sse_partials(int dtype, int M, int N, int Np, const void* y, const floa
   return MMAD_OK;
 }
 
+double mmad_decimal_of(float f) {
+  // the shortest decimal that rounds to f, as a double: the Python float a
+  // caller's optimizer holds (0.9, 0.999, 1e-3) when it reached us as float
+  char buf[32];
+  for (int prec = 1; prec <= 9; ++prec) {
+    snprintf(buf, sizeof buf, "%.*g", prec, (double)f);
+    if (strtof(buf, nullptr) == f) return strtod(buf, nullptr);
+  }
+  return (double)f;
+}
+
+MmadAdamConsts mmad_adam_consts(float lr, float beta1, float beta2, float eps, int step) {
+  // torch.optim.Adam (_single_tensor_adam): 1 - beta, lr / (1 - beta1^t) and
+  // sqrt(1 - beta2^t) in double from the optimizer's double hyper-parameters,
+  // each cast to float where torch casts it (the scalar operand of a float op)
+  const double b1 = mmad_decimal_of(beta1), b2 = mmad_decimal_of(beta2), l = mmad_decimal_of(lr);
+  const double bc1 = 1.0 - pow(b1, step), bc2 = 1.0 - pow(b2, step);
+  MmadAdamConsts c;
+  c.w1 = (float)(1.0 - b1);
+  c.w2 = (float)(1.0 - b2);
+  c.eps = eps;
+  c.step_size = (float)(l / bc1);
+  c.bc2_sqrt = (float)pow(bc2, 0.5);
+  return c;
+}
+
+int mmad_adam_w(int64_t n, float* p, const float* g, float* m, float* v, float w1, float w2,
+                float eps, float step_size, float bc2_sqrt, void* shadow, int64_t n_shadow,
+                void* stream) {
+  return mmad_adam_dyn(n, p, g, m, v, w1, w2, eps, step_size, bc2_sqrt, shadow, n_shadow, nullptr,
+                       stream);
+}
+
 int mmad_adam(int64_t n, float* p, const float* g, float* m, float* v, float beta1, float beta2,
               float eps, float step_size, float bc2_sqrt, void* shadow, int64_t n_shadow,
               void* stream) {
-  MMAD_CHECK_ARG(n >= 0 && n_shadow >= 0 && n_shadow <= n, "adam: bad sizes");
-  if (n == 0) return MMAD_OK;
-  MMAD_CHECK_ARG(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
-                 "adam: buffers must be 16-byte aligned");
-  adam_k<<<nblk((n + 3) / 4, 256), 256, 0, (hipStream_t)stream>>>(
-      n, p, g, m, v, beta1, beta2, eps, step_size, bc2_sqrt, (bf16*)shadow, n_shadow, nullptr);
-  MMAD_LAUNCH_CHECK();
-  return MMAD_OK;
+  // public entry: the caller's betas; the update constants as torch forms them
+  const MmadAdamConsts c = mmad_adam_consts(1e-3f, beta1, beta2, eps, 1);
+  return mmad_adam_w(n, p, g, m, v, c.w1, c.w2, eps, step_size, bc2_sqrt, shadow, n_shadow, stream);
 }
 
-int mmad_adam_dyn(int64_t n, float* p, const float* g, float* m, float* v, float beta1, float beta2,
+int mmad_adam_dyn(int64_t n, float* p, const float* g, float* m, float* v, float w1, float w2,
                   float eps, float step_size, float bc2_sqrt, void* shadow, int64_t n_shadow,
                   const MmadDyn* dyn, void* stream) {
   MMAD_CHECK_ARG(n >= 0 && n_shadow >= 0 && n_shadow <= n, "adam: bad sizes");
@@ -1114,7 +1146,7 @@ int mmad_adam_dyn(int64_t n, float* p, const float* g, float* m, float* v, float
   MMAD_CHECK_ARG(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0,
                  "adam: buffers must be 16-byte aligned");
   adam_k<<<nblk((n + 3) / 4, 256), 256, 0, (hipStream_t)stream>>>(
-      n, p, g, m, v, beta1, beta2, eps, step_size, bc2_sqrt, (bf16*)shadow, n_shadow, dyn);
+      n, p, g, m, v, w1, w2, eps, step_size, bc2_sqrt, (bf16*)shadow, n_shadow, dyn);
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
 }

@@ -255,9 +255,12 @@ int mmad_unpack_output(int dtype, int M, int N, int Np, const void* y, float* ou
                        void* stream);
 
 /* torch.optim.Adam step (novelty_detection.py:90; amsgrad=False,
- * weight_decay=0) over a flat fp32 buffer of n params:
- * m = b1 m + (1-b1) g; v = b2 v + (1-b2) g^2;
- * p -= step_size * m / (sqrt(v)/bc2_sqrt + eps); step_size = lr/(1-b1^t).
+ * weight_decay=0) over a flat fp32 buffer of n params, rounded as torch's
+ * CPU _single_tensor_adam rounds it:
+ * m = lerp(m, g, 1-b1); v = v*b2 + (1-b2)*g*g;
+ * p += (-step_size * m) / (sqrt(v)/bc2_sqrt + eps); step_size = lr/(1-b1^t),
+ * with 1-b1 and 1-b2 formed in double from the decimal each float beta came
+ * from (0.9f -> 0.9), as torch forms them from the optimizer's Python floats.
  * shadow (nullable, bf16) receives bf16(p) for the first n_shadow elements. */
 int mmad_adam(int64_t n, float* p, const float* g, float* m, float* v, float beta1, float beta2,
               float eps, float step_size, float bc2_sqrt, void* shadow, int64_t n_shadow,

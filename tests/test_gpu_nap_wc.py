@@ -181,3 +181,51 @@ def test_nap_end_to_end_training(wc, dtype):
     _record(_REC)
     print(f"\n{dtype} aggregate {agg}")
     assert t_prod <= agg["bar"], agg
+
+
+def test_nap_bf16_scoring_on_reference_weights(wc):
+    """bf16 NAP scoring (missing 5).  The REFERENCE's trained
+    weights in a bf16 model, scored on every well-conditioned range:
+    * default (config.nap_dtype unset): NAP reads the diffs of the fp32 eval
+      twin built from the same master weights (novelty_detection._nap_model),
+      so its AUROC is the fp32 product's -- within 0.002 of the reference;
+    * config.nap_dtype = 'model': NAP on the bf16 path's own diffs (bf16
+      activations, 8 significant bits).  Held to the bf16 bar of this suite
+      (AUROC within 0.01 of the reference, tests/test_gpu_parity.py), every
+      delta recorded; BASE / SAP on the bf16 path within 0.01 too."""
+    from icra2021_multimodal_ad_amd.data_loaders import get_loaders
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    g = wc
+    rec = {}
+    deltas = {"twin": [], "bf16": []}
+    for seed in [int(s) for s in g["meta/seeds"]]:
+        p = f"s{seed}/"
+        keys = [str(k) for k in g[p + "state_dict_keys"]]
+        sd = {k: torch.from_numpy(np.asarray(g[p + f"sd/{k}"])) for k in keys}
+        row = {}
+        for mode in ("twin", "bf16"):
+            cfg = _cfg(g, seed, "bf16")
+            if mode == "bf16":
+                cfg.nap_dtype = "model"
+            model = get_model(cfg)
+            model.load_state_dict(sd)
+            loaders = get_loaders(cfg)
+            full = _score(model, cfg, loaders, (0, cfg.n_layers + 1))
+            for m in ("base", "sap"):
+                d = full.last_row[f"{m}_auroc"] - float(g[p + f"{m}/auroc"])
+                row[f"{mode}/{m}"] = d
+                assert abs(d) <= 0.01, (seed, mode, m, d)
+            for rg in _ranges(g, seed):
+                s, e = rg
+                det = _score(model, cfg, loaders, rg)
+                d = det.last_row["nap_auroc"] - float(g[p + f"nap_{s}_{e}/auroc"])
+                row[f"{mode}/nap[{s},{e})"] = d
+                deltas[mode].append(d)
+        rec[seed] = row
+    summary = {m: {"max_abs": float(np.max(np.abs(v))), "mean_abs": float(np.mean(np.abs(v))), "n": len(v)}
+               for m, v in deltas.items()}
+    _REC["bf16_nap_scoring_on_reference_weights"] = {"per_seed": rec, "summary": summary}
+    _record(_REC)
+    print(f"\nbf16 NAP scoring of the reference's weights: {summary}")
+    assert summary["twin"]["max_abs"] <= 0.002, summary
+    assert summary["bf16"]["max_abs"] <= 0.01, summary

@@ -231,3 +231,55 @@ def test_nap_well_conditioned_ranges_match_reference(golden):
             worst = max(worst, d)
             assert d <= 0.002, (seed, s, e, a, float(g[p + f"nap_{s}_{e}/auroc"]))
     assert worst <= 0.002
+
+
+def test_teacher_forced_oracle_step_within_reference_band(golden):
+    """tests/golden/teacher.npz: from the reference's own mid-training state
+    (D=256, steps 36 / 72 / 108 of a seeded run: parameters, BN buffers, Adam
+    moments and step), the oracle's one step lands within 3x the reference's
+    own 8-vs-1-thread band of the 8-thread step (+ 2^-22 of the tensor's norm), for
+    the loss, every gradient and every parameter / buffer after the step.
+    The batch is regenerated from the build's seeded loaders (checksum)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from gen_nap_wc import config_for
+    from icra2021_multimodal_ad_amd.data_loaders import get_loaders
+    g = golden("teacher")
+    cfg = config_for(int(g["meta/seed"]))
+    names = [str(n) for n in g["meta/param_names"]]
+    pmap = {"layer.weight": "W", "layer.bias": "b", "bn.weight": "gamma", "bn.bias": "beta"}
+    _, tl, _, _ = get_loaders(cfg, device="cpu")
+    batches = {}
+    for e in range(1, int(max(g["meta/snap_steps"])) // int(g["meta/per_epoch"]) + 2):
+        for i, (x, _) in enumerate(tl):
+            batches[(e, i)] = x.numpy()
+    for s in g["meta/snap_steps"]:
+        p = f"s{int(s)}/"
+        x = batches[(int(g[p + "epoch"]), int(g[p + "batch"]))]
+        assert abs(float(x.astype(np.float64).sum()) - float(g[p + "x_checksum"])) < 1e-6 * abs(float(g[p + "x_checksum"])) + 1e-6
+        m = model_from_state_dict(_sd(g, p + "before/"))
+        state = {"t": int(g[p + "adam_step"])}
+        for n in names:
+            side = "enc" if n.startswith("encoder") else "dec"
+            key = (side, int(n.split(".")[2]), pmap[n.split(".", 3)[3]])
+            state[("m",) + key] = np.array(g[p + "exp_avg/" + n], np.float32)
+            state[("v",) + key] = np.array(g[p + "exp_avg_sq/" + n], np.float32)
+        loss, _, grads = O.ae_train_grads(x, m)
+        O.adam_step(m, grads, state)
+        l8 = float(g[p + "ref8/loss"])
+        assert abs(loss - l8) <= 3 * abs(float(g[p + "ref1/loss"]) - l8) + 1e-6 * l8, (s, loss, l8)
+        flat = grads_to_flat(grads)
+        for n in names:
+            r = np.asarray(g[p + "ref8/grad/" + n], np.float64)
+            dev = np.linalg.norm(np.asarray(flat[n], np.float64) - r)
+            assert dev <= 3 * float(g[p + "ref1/grad_norm/" + n]) + 2.0 ** -22 * np.linalg.norm(r), (s, n)
+        after = state_dict_from_model(m)
+        for k, v in after.items():
+            if k.endswith("num_batches_tracked"):
+                continue
+            r = np.asarray(g[p + "ref8/after/" + k], np.float64)
+            dev = np.linalg.norm(np.asarray(v, np.float64) - r)
+            # floor: a couple of fp32 ulps of the parameter itself (a rounding
+            # of p - lr * m / (sqrt(v) / bc2 + eps) may land one ulp apart)
+            assert dev <= 3 * float(g[p + "ref1/after_norm/" + k]) + 2.0 ** -22 * np.linalg.norm(r), (s, k, dev)
