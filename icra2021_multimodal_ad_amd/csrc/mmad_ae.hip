@@ -98,6 +98,11 @@ struct mmad_ae {
   // optional bf16 gradient exchange (mmad_ae_set_grad_bf16): n_weight bf16
   void* grad_bf16 = nullptr;
   hipEvent_t ev_small = nullptr, ev_cdone = nullptr;
+  // schedule study (knob 29): every side-stream dW + Adam GEMM held until the
+  // main stream has enqueued the whole bwd-data chain (ev_hold), to separate
+  // the chain's in-step contention from its barrier costs
+  int side_hold = 0;
+  hipEvent_t ev_hold = nullptr;
   // fused step: dW GEMMs of layers < dw_main run on the caller's stream
   // (knob 19; tools/sched_sweep.py: 0.499 ms (2) vs 0.512 (1) vs 0.523 (3));
   // keep_grads (knob 25): also write dW to the grads buffer
@@ -193,6 +198,7 @@ struct mmad_ae {
     for (auto e : ev_fork) (void)hipEventDestroy(e);
     for (auto e : ev_data) (void)hipEventDestroy(e);
     if (ev_join) (void)hipEventDestroy(ev_join);
+    if (ev_hold) (void)hipEventDestroy(ev_hold);
     if (ev_loss) (void)hipEventDestroy(ev_loss);
     for (auto e : ev_dw) (void)hipEventDestroy(e);
     for (auto e : ev_xdw) (void)hipEventDestroy(e);
@@ -373,6 +379,7 @@ int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, i
     h->keep_grads = mmad_knob(25);
     h->side_prio_hi = mmad_knob(26);
     h->dp_shard = mmad_knob(28);
+    h->side_hold = mmad_knob(29);
     h->dp_bucket_mib = mmad_knob(30) < 0 ? 0 : mmad_knob(30);
     h->ev_flags_ = ev_flags(mmad_knob(27));
   }
@@ -460,6 +467,7 @@ int mmad_ae_bind(mmad_ae* h, float* params, float* grads, float* adam_m, float* 
       MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_data[i], h->ev_flags_));
     }
     MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_join, h->ev_flags_));
+    MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_hold, h->ev_flags_));
     MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->ev_loss, h->ev_flags_));
   }
   return MMAD_OK;
@@ -1004,6 +1012,8 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
         dwe.tile_force = mmad_tile_adam_main_for(a.Np, a.Kp, Mp) + 1;
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, st,
                        nullptr, PROBE_DW + l));
+      } else if (h->side_hold) {
+        pending.push_back(PendingDW{dz, in, a.Np, a.Kp, a.Np, a.Kp, Mp, dwe, l});
       } else if (ping) {
         MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
@@ -1020,6 +1030,14 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
                        nullptr, PROBE_DW + l));
       }
     }
+  }
+  if (h->side_hold && !pending.empty()) {
+    MMAD_HIP_CHECK(hipEventRecord(h->ev_hold, st));
+    MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_hold, 0));
+    for (const PendingDW& q : pending)
+      RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, q.dz, q.lda, q.in, q.ldb, q.M, q.N, q.K, q.ep, side,
+                     nullptr, PROBE_DW + q.layer));
+    pending.clear();
   }
   MMAD_CHECK_ARG(pending.empty(), "ae backward: deferred dW GEMMs left unissued");
   // join the side stream back into the main stream

@@ -48,7 +48,8 @@ int g_knob[MMAD_KNOB_COUNT] = {
     0,     // 9  split-K override of the dW GEMMs
     0,     // 10 dW split rule: target 64x64-tile blocks (0 = no split)
     8,     // 11 dW split rule: minimum K stages per slice
-    0, 0, 0, 0,   // 12-15 retired (measured-slower experiments, removed in round 3)
+    0,     // 12 persistent grid for forward-type GEMMs (-1 rule, 0 off, 1 on)
+    0, 0, 0,      // 13-15 retired (measured-slower experiments, removed in round 3)
     -1,    // 16 train-mode BN schedule (-1 = dtype default: bf16 fused, fp32 apply; 0 apply, 1 fold, 2 fused)
     -1,    // 17 backward BN schedule (-1 = the forward's; 2 = fused into the bwd-data GEMMs)
     2048,  // 18 fused BN up to this many padded rows (fold above)
@@ -62,7 +63,7 @@ int g_knob[MMAD_KNOB_COUNT] = {
     0,     // 26 side stream at the highest priority (schedule sweeps)
     0,     // 27 executor events with the system-scope fence
     1,     // 28 DP: sharded weight buckets (reduce-scatter, Adam on 1/N, all-gather)
-    0,     // 29 retired (graph node priorities: no effect, profiles/r03w_graph_priority.txt)
+    0,     // 29 schedule study: hold every side-stream dW + Adam until the bwd-data chain is enqueued
     8,     // 30 DP: minimum exchange bucket (MiB of fp32 gradient; consecutive layers merge)
     1,     // 31 bwd-data hand-off events completed by the GEMM launch (hipExtLaunchKernel)
 };
@@ -72,6 +73,7 @@ int mmad_tile_override() { return g_knob[0]; }
 int mmad_group_override() { return g_knob[1]; }
 int mmad_autotune_enabled() { return g_knob[2]; }
 int mmad_dbg_override() { return g_knob[3]; }
+int mmad_persist_override() { return g_knob[12]; }
 int mmad_splitk_override() { return g_knob[4]; }
 int mmad_splitk_dw_override() { return g_knob[9]; }
 // dW split-K target blocks (0 = no split): 512 paid before the dW loop stopped
@@ -114,7 +116,7 @@ int mmad_tile_epi_override(int epi) {
 }
 
 static bool knob_valid(int knob) {
-  return knob >= 0 && knob < MMAD_KNOB_COUNT && !(knob >= 12 && knob <= 15) && knob != 29;
+  return knob >= 0 && knob < MMAD_KNOB_COUNT && !(knob >= 13 && knob <= 15);
 }
 int mmad_tune_set(int knob, int value) {
   if (!knob_valid(knob)) {

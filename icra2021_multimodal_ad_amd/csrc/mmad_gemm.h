@@ -79,6 +79,7 @@ struct GemmEpi {
   // set by the launcher: split factor, XCD-aware grouped tile order
   int splitk;
   int tiles_n, group_m;
+  int persist_tiles;   // persistent grid (knob 12): every block loops over these tiles
   int tile_force;        // caller's tile choice + 1 (0 = none; ignored if it does not fit)
   // graph-captured step (nullable): MSE target = dyn->x, Adam step terms
   // from dyn (see MmadDyn)
@@ -126,6 +127,7 @@ int mmad_group_override();
 int mmad_tile_override();
 int mmad_autotune_enabled();
 int mmad_dbg_override();
+int mmad_persist_override();   // knob 12
 int mmad_splitk_override();   // 0 = shape rule; 1, 2, 4, 8, 16 = forced split factor
 int mmad_splitk_dw_override();     // the same for the dW GEMMs only (knob 9)
 int mmad_splitk_dw_blocks();       // dW split rule: target 64x64-tile blocks (knob 10)

@@ -1708,6 +1708,27 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __r
   gemm_body<T, TO, AK, BK_, CFG, EPI>(A, lda, B, ldb, K, ep, blockIdx.x, gridDim.x);
 }
 
+// Persistent form (knob 12) of the forward-type bf16 GEMMs at large row
+// counts (C5 scoring: 65,536 rows, 8 rounds of tiles): one block per resident
+// slot walks the logical tiles v = blockIdx.x, + gridDim.x, ... (gridDim a
+// multiple of 8, so v & 7 -- the XCD label of the tile order -- stays the
+// block's own).  Per tile the body is gemm_body's, so every output bit is the
+// non-persistent kernel's; what changes is that the next tile's prologue
+// (LDS-DMA of its first stages) is issued right after this tile's epilogue
+// stores instead of after a block retirement and a new dispatch.  Never with
+// a fused BN (its column barrier needs every tile of a column resident) or a
+// split (the combine's last arriver waits for its sibling slices).
+template <typename T, typename TO, bool AK, bool BK_, int CFG, int EPI>
+__global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel_p(const T* __restrict__ A, int lda,
+                                                             const T* __restrict__ B, int ldb, int K,
+                                                             GemmEpi ep) {
+  const int nt = ep.persist_tiles;
+  for (int v = blockIdx.x; v < nt; v += gridDim.x) {
+    gemm_body<T, TO, AK, BK_, CFG, EPI>(A, lda, B, ldb, K, ep, v, nt);
+    __syncthreads();
+  }
+}
+
 // -------------------------------------------------------------------------
 // host-side planning and launch
 // -------------------------------------------------------------------------
@@ -1752,6 +1773,48 @@ static int plan_group_m(int ntiles, int tiles_m, int BM, int BN) {
   return gm < 1 ? 1 : (gm > tiles_m ? tiles_m : gm);
 }
 
+// the configurations that have a persistent instantiation (the large-row tiles)
+constexpr bool persist_cfg(int cfg) { return cfg == 1 || cfg == 2 || cfg == CFG_BIG; }
+
+template <typename T, typename TO, bool AK, bool BK_, int EPI>
+static const void* persist_kernel(int cfg) {
+  if constexpr (sizeof(T) == 2 && (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_MSE || EPI == GEMM_EPI_SCORE)) {
+    switch (cfg) {
+      case 1: return (const void*)mmad_gemm_kernel_p<T, TO, AK, BK_, 1, EPI>;
+      case 2: return (const void*)mmad_gemm_kernel_p<T, TO, AK, BK_, 2, EPI>;
+      case CFG_BIG: return (const void*)mmad_gemm_kernel_p<T, TO, AK, BK_, CFG_BIG, EPI>;
+      default: return nullptr;
+    }
+  }
+  return nullptr;
+}
+
+namespace {
+std::mutex g_pcap_mu;
+std::map<long, int> g_pcap;   // (device, epi, cfg) -> resident blocks of the persistent kernel
+}  // namespace
+
+static int persist_capacity(const void* fn, int epi, int cfg) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  const long key = ((long)dev * 8 + epi) * 8 + cfg;
+  {
+    std::lock_guard<std::mutex> lk(g_pcap_mu);
+    auto it = g_pcap.find(key);
+    if (it != g_pcap.end()) return it->second;
+  }
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, CFG_NT[cfg], 0) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    per_cu = 0;
+  }
+  const int cap = per_cu > 0 && cus > 0 ? (per_cu * cus) & ~7 : 0;   // a multiple of 8 (XCD labels)
+  std::lock_guard<std::mutex> lk(g_pcap_mu);
+  g_pcap[key] = cap;
+  return cap;
+}
+
 template <typename T, typename TO, bool AK, bool BK_, int EPI>
 static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np, int K,
                         const GemmEpi& ep_in, int cfg, hipStream_t s) {
@@ -1761,6 +1824,32 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
   ep.tiles_n = tiles_n;
   const int S = ep.splitk > 1 ? ep.splitk : 1;
   ep.group_m = plan_group_m(ntiles, tiles_m, BM, BN);
+  // persistent grid: forward-type bf16 epilogues without a fused BN or a
+  // split, when the tiles exceed one resident round (knob 12: -1 rule, 1 on)
+  const int pk = mmad_persist_override();
+  if (pk != 0 && S == 1 && !ep.bn_sync && persist_cfg(cfg)) {
+    const void* pfn = persist_kernel<T, TO, AK, BK_, EPI>(cfg);
+    const int cap = pfn ? persist_capacity(pfn, EPI, cfg) : 0;
+    if (cap > 0 && ntiles > cap) {
+      ep.persist_tiles = ntiles;
+      dim3 pg(cap), pb(CFG_NT[cfg]);
+      auto args_go = [&](auto kern) {
+        if (ep.done_ev)
+          hipExtLaunchKernelGGL(kern, pg, pb, 0u, s, nullptr, ep.done_ev, 0u, A, lda, B, ldb, K, ep);
+        else
+          kern<<<pg, pb, 0, s>>>(A, lda, B, ldb, K, ep);
+      };
+      if constexpr (sizeof(T) == 2 && (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_MSE || EPI == GEMM_EPI_SCORE)) {
+        switch (cfg) {
+          case 1: args_go(mmad_gemm_kernel_p<T, TO, AK, BK_, 1, EPI>); break;
+          case 2: args_go(mmad_gemm_kernel_p<T, TO, AK, BK_, 2, EPI>); break;
+          default: args_go(mmad_gemm_kernel_p<T, TO, AK, BK_, CFG_BIG, EPI>); break;
+        }
+        MMAD_LAUNCH_CHECK();
+        return MMAD_OK;
+      }
+    }
+  }
   dim3 grd(ntiles * S), blk(CFG_NT[cfg]);
   const size_t dyn = 0;
   // the caller's completion event rides on the launch itself (no marker packet)

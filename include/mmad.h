@@ -64,7 +64,9 @@ int mmad_pad_granule(void);
  *      128x128; -2 = 128x128 where its grid covers >= 200 CUs, else knob 5;
  *      -1 = knob 5);
  *      6 / 7 = tile of the bwd-data / forward GEMMs (-1 autotuned)
- *   12-15 retired (EINVAL)
+ *   12 persistent grid for the forward-type GEMMs without a fused BN or a
+ *      split (-1 rule: when the tiles exceed one resident round; 0 off; 1 on)
+ *   13-15 retired (EINVAL)
  *   16 train-mode BN schedule (-1 dtype default: bf16 fused, fp32 apply;
  *      0 apply kernels, 1 fold into the consumer, 2 fused into the GEMMs)
  *   17 backward BN schedule (-1 = the forward's, 2 = fused into bwd-data)
@@ -80,7 +82,8 @@ int mmad_pad_granule(void);
  *   27 executor events with the system-scope fence (0)
  *   28 data parallel: sharded weight buckets (reduce-scatter, Adam on 1/N,
  *      all-gather; 1) or all-reduce + full Adam (0)
- *   29 retired (EINVAL)
+ *   29 schedule study: every side-stream dW + Adam GEMM held until the main
+ *      stream has enqueued the whole bwd-data chain (0)
  *   30 data parallel: minimum exchange bucket in MiB of fp32 gradient;
  *      consecutive layers (backward order) share a bucket until it holds this
  *      much (8; 0 = one bucket per layer)

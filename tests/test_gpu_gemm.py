@@ -200,3 +200,53 @@ def test_splitk_timeout_is_reported_not_combined(ws):
     ref = x[:M, :K].double() @ w[:N, :K].double().t()
     err = (y[:M, :N].double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-2
+
+
+@pytest.mark.parametrize("kind", ["fwd", "score", "mse"])
+def test_persistent_grid_bit_identical(kind):
+    """Knob 12 (persistent grid: one block per resident slot walks the tiles)
+    gives the ordinary grid's bits for the forward-type bf16 epilogues, with
+    every large-row tile (256x128, 128x256, 256x256) forced, at a row count
+    whose tiles exceed one resident round (16,384 rows: 512-1024 tiles on 256
+    CUs); outputs, BN-statistic / score-row / loss partials compared."""
+    lib = _native.load()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    M, N, K = 16384, 2048, 1658
+    Mp, Np, Kp = pad(M), pad(N), pad(K)
+    x = torch.zeros(Mp, Kp, device=dev, dtype=torch.bfloat16)
+    x[:M, :K] = torch.randn(M, K, device=dev, generator=g).bfloat16()
+    w = torch.zeros(Np, Kp, device=dev, dtype=torch.bfloat16)
+    w[:N, :K] = (torch.randn(N, K, device=dev, generator=g) * 0.05).bfloat16()
+    b = torch.randn(Np, device=dev, generator=g) * 0.1
+    ref = torch.randn(Mp, Np, device=dev, generator=g).bfloat16()
+    tgt = torch.randn(M, N, device=dev, generator=g)
+    s = stream_ptr()
+
+    def run():
+        y = torch.zeros(Mp, Np, device=dev, dtype=torch.bfloat16)
+        part = torch.zeros(Mp // 32, 2, Np, device=dev)
+        rows = torch.zeros(Np // 128, Mp, device=dev)
+        if kind == "fwd":
+            call("mmad_fc_fwd", BF16, M, N, K, Mp, Np, Kp, ptr(x), ptr(w), ptr(b), 1, 0.2, None, None,
+                 ptr(y), ptr(part), s)
+            return y, part
+        if kind == "score":
+            call("mmad_fc_fwd_score", BF16, M, N, K, Mp, Np, Kp, ptr(x), ptr(w), ptr(b), 1, 0.2, None,
+                 None, ptr(y), ptr(ref), ptr(rows), None, 0, s)
+            return y, rows
+        call("mmad_fc_fwd_mse", BF16, M, N, K, Mp, Np, Kp, ptr(x), ptr(w), ptr(b), ptr(tgt), N, 2.0,
+             ptr(y), ptr(part), s)
+        return y, part
+    try:
+        for tile in (1, 2, 6):
+            lib.mmad_tune_set(0, tile)
+            lib.mmad_tune_set(12, 0)
+            a = run()
+            lib.mmad_tune_set(12, 1)
+            p = run()
+            torch.cuda.synchronize()
+            assert torch.equal(a[0], p[0]) and torch.equal(a[1], p[1]), (kind, tile)
+    finally:
+        lib.mmad_tune_set(0, -1)
+        lib.mmad_tune_set(12, 0)

@@ -82,10 +82,13 @@ for li in layers:
     for r in range(rounds):
         for t in tiles:
             tt, _, dbg = t.partition("d")
-            lib.mmad_tune_set(0, int(tt))
+            per = tt.endswith("p")              # "6p": the persistent grid (knob 12)
+            lib.mmad_tune_set(0, int(tt.rstrip("p")))
             lib.mmad_tune_set(3, int(dbg or 0))
+            lib.mmad_tune_set(12, 1 if per else 0)
             res[t].append(timeit(mine, iters))
             lib.mmad_tune_set(3, 0)
+            lib.mmad_tune_set(12, 0)
             if r == 0:
                 torch.cuda.synchronize()
                 outs[t] = ((dx if kind == "bwd_data" else y).clone(),
