@@ -88,13 +88,15 @@ __device__ __forceinline__ float apply_act_pw(float z, bool relu, float lo_slope
   return z > 0.f ? z : lo;
 }
 // derivative expressed through the activation OUTPUT a (all supported acts
-// are monotone so the output determines the branch / value); branch-free
-// (selects, no per-element branch tree in unrolled epilogues)
+// are monotone so the output determines the branch / value)
 __device__ __forceinline__ float act_grad_from_out(float a, int act, float slope) {
-  const float pw = a > 0.f ? 1.f : (act == MMAD_ACT_LEAKYRELU ? slope : (act == MMAD_ACT_RELU ? 0.f : 1.f));
-  const float sg = a * (1.f - a);
-  const float th = 1.f - a * a;
-  return act == MMAD_ACT_SIGMOID ? sg : (act == MMAD_ACT_TANH ? th : pw);
+  switch (act) {
+    case MMAD_ACT_LEAKYRELU: return a > 0.f ? 1.f : slope;
+    case MMAD_ACT_RELU: return a > 0.f ? 1.f : 0.f;
+    case MMAD_ACT_SIGMOID: return a * (1.f - a);
+    case MMAD_ACT_TANH: return 1.f - a * a;
+    default: return 1.f;
+  }
 }
 
 // torch.optim.Adam element update, as torch's _single_tensor_adam computes it

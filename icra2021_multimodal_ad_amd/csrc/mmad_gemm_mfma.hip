@@ -427,7 +427,7 @@ __device__ __forceinline__ bool col_wait(unsigned* ctr, unsigned gen0, unsigned*
 template <typename T, typename TO, bool AK, bool BK_, int CFG, int EPI>
 __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, const T* __restrict__ B,
                                           int ldb, int K, const GemmEpi& ep, const int bid,
-                                          const int nblk) {
+                                          const int nblk, const int tid_in) {
   using C = Cfg<CFG>;
   constexpr int BM = C::BM, BN = C::BN, WM = C::WM, WN = C::WN, NS = C::NS, NT = C::NT;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;   // 16x16 MFMA tiles per wave
@@ -455,13 +455,22 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   constexpr int XBYTES = BIG ? 0
                          : EPI == GEMM_EPI_FWD ? 12 * BN * 8 + 2 * BN * 4 + 64
                          : EPI == GEMM_EPI_BWD_DATA ? 6 * BN * 8 + 64 : 0;
-  constexpr int LDS_BYTES = (NS * SLOT > OBYTES + XBYTES) ? NS * SLOT : OBYTES + XBYTES;
+  // transposed epilogue staging (bf16 outputs of the forward-type epilogues
+  // without a fused BN): the tile goes to LDS column-major, 8 B per lane per
+  // MFMA fragment (ds_write_b64), and comes back row-major, 16 B per lane,
+  // through ds_read_b64_tr_b16 (tstage_* below); column stride CS, 8-byte
+  // granules XOR-swizzled by (col >> 1) & 7: conflict-free on both sides
+  constexpr bool TSTG = sizeof(TO) == 2 && (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_MSE ||
+                                            EPI == GEMM_EPI_SCORE);
+  constexpr int TCS = BM * 2 + 64;
+  constexpr int TBYTES = TSTG ? BN * TCS : 0;
+  constexpr int LDS_A = (NS * SLOT > OBYTES + XBYTES) ? NS * SLOT : OBYTES + XBYTES;
+  constexpr int LDS_BYTES = LDS_A > TBYTES ? LDS_A : TBYTES;
   static_assert((NS - 1) * NL <= 63, "vmcnt range");
   static_assert(LDS_BYTES <= 163840, "LDS budget");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
-  if (ep.dbg & 256) return;   // (launch-floor study: an empty block)
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = tid_in, lane = tid & 63, w = tid >> 6;
   const int wm = w / WN, wn = w % WN;
   // XCD-aware order (1-D grid).  Under round-robin dispatch, blocks with equal
   // bid % 8 share an XCD (speed only, never correctness); each such set gets a
@@ -1074,22 +1083,23 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         }
     }
   }
-  // the register phase, instantiated twice: PW = the piecewise-linear
-  // activations (branch-free, the hot path), else the general one (sigmoid /
-  // tanh; FWD / SCORE only -- the other epilogues apply no activation)
+  // activations: the piecewise-linear ones (LeakyReLU / ReLU / none, the hot
+  // path) are applied branch-free inside the register phase below; the
+  // others (sigmoid / tanh, FWD / SCORE only) by a pre-pass over the
+  // accumulators, acc = act(acc + bias) -- the same value the fused form
+  // computes -- after which the register phase applies no activation.  One
+  // instance of the register phase either way (two instances cost registers:
+  // spills in the 256-row tiles).
+  const bool pw_act = !FWDLIKE || EPI == GEMM_EPI_MSE || act_is_linear_piecewise(ep.act);
   const bool pw_relu = ep.act == MMAD_ACT_RELU;
   const float pw_lo = act_lo_slope(ep.act, ep.slope);
-  auto reg_phase = [&](auto pw_c) {
-    constexpr bool PW = decltype(pw_c)::value;
+  float ebias[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = cw + j * 16 + c;
-    const bool cvalid = col < ep.N;
-    float bias = 0.f, sc = 1.f, sh = 0.f;
+    float bias = 0.f;
     if constexpr (FWDLIKE) {
       bias = e_b[j];
-      sc = e_s[j];
-      sh = e_t[j];
       if (EPI != GEMM_EPI_SCORE && ep.bpart) {
         // + sum_k shift[k] W[n][k]: lane-group sums, then ((g0+g1)+(g2+g3))
         float t = 0.f;
@@ -1099,6 +1109,28 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         t = sum_lane_groups(t);
         bias += t;
       }
+    }
+    ebias[j] = bias;
+  }
+  if constexpr (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_SCORE) {
+    if (!pw_act) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = apply_act(acc[i][j][r] + ebias[j], ep.act, ep.slope);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = cw + j * 16 + c;
+    const bool cvalid = col < ep.N;
+    const float bias = ebias[j];
+    float sc = 1.f, sh = 0.f;
+    if constexpr (FWDLIKE) {
+      sc = e_s[j];
+      sh = e_t[j];
     }
     float s1[TM / 2], s2[TM / 2];
 #pragma unroll
@@ -1111,9 +1143,10 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         const bool valid = cvalid && row < ep.M;
         float v = acc[i][j][r];
         if (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_SCORE) {
-          // pinned: tile-independent
-          if constexpr (PW) v = fmaf(apply_act_pw(v + bias, pw_relu, pw_lo), sc, sh);
-          else v = fmaf(apply_act(v + bias, ep.act, ep.slope), sc, sh);
+          // pinned: tile-independent (act already applied by the pre-pass
+          // when it is not piecewise-linear)
+          const float a = apply_act_pw(v + bias, pw_relu, pw_lo);
+          v = fmaf(pw_act ? a : v, sc, sh);
           v = valid ? v : 0.f;
           s1[i >> 1] += v;
         } else if (EPI == GEMM_EPI_MSE) {
@@ -1136,7 +1169,14 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
 #pragma unroll
       for (int p = 0; p < TM / 2; ++p) {
         float a1 = s1[p];
-        a1 = sum_lane_groups(a1);
+        if constexpr (EPI == GEMM_EPI_BWD_DATA) {
+          // (the same value through ds_bpermute: the lane-swap form's two
+          // temporaries per reduction spill the fused-BN bwd-data tiles)
+          a1 += __shfl_xor(a1, 16);
+          a1 += __shfl_xor(a1, 32);
+        } else {
+          a1 = sum_lane_groups(a1);
+        }
         const int crow = rw + p * 32;
         const int chunk = crow / MMAD_PART_ROWS;
         float* part = ep.part + (size_t)chunk * 2 * ep.ldpart;
@@ -1175,9 +1215,6 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
     }
   }
 
-  };
-  if (!FWDLIKE || EPI == GEMM_EPI_MSE || act_is_linear_piecewise(ep.act)) reg_phase(std::true_type{});
-  else reg_phase(std::false_type{});
 
   // ===================== epilogue, LDS-staged coalesced store ===============
   // fused BN (forward): the Welford partials are out -- arrive at the column
@@ -1210,8 +1247,26 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       __syncthreads();
     }
   }
-  // (dbg 128, epilogue studies: no LDS staging writes)
-  if (!(ep.dbg & 128)) {
+  // transposed staging for this tile.  Only the non-256 FWD tiles can carry a
+  // fused BN (whose epilogue re-stages row-major): for every other forward-
+  // type tile the choice is a compile-time constant, so the row-major path is
+  // not instantiated beside it (registers).  dbg 512 (A/B): row-major b16.
+  constexpr bool TSTG_ONLY = TSTG && (EPI != GEMM_EPI_FWD || BIG);
+  const bool tstg = TSTG_ONLY ? true : (TSTG && !ep.bn_sync && !(ep.dbg & 512));
+  auto tsw = [](int col) { return ((col >> 1) & 7) << 3; };
+  if (TSTG && tstg) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int rl0 = wm * 16 * TM + i * 16 + 4 * g;
+        const int cl = wn * 16 * TN + j * 16 + c;
+        bf16x4 q;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) q[r] = (bf16)acc[i][j][r];
+        *(bf16x4*)(smem + cl * TCS + ((rl0 * 2) ^ tsw(cl))) = q;
+      }
+  } else {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1279,6 +1334,82 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         if (ep.ad_shadow) *(bf16x4*)((bf16*)ep.ad_shadow + off[u]) = sh;
       }
     }
+  } else if (TSTG && tstg) {
+    // read back row-major: iteration u covers a 16-row x 32-column block
+    // (row block rb = wave's, column block cb); lane (n = lane & 15, g = lane >> 4)
+    // gets row rbase + n, columns cbase + 8g .. + 7 (two tr-reads of 4), one
+    // 16-B store.  A wave walks its row blocks, and per row block the column
+    // blocks in order, so the 4 blocks of a 128-column score group are
+    // consecutive iterations of one lane.
+    constexpr int RB = BM / 16, CB = BN / 32, RBW = RB / NW, NB = RBW * CB;
+    static_assert(!TSTG || (RB % NW == 0 && NB == ITERS), "transposed staging geometry");
+    const int n16 = lane & 15, q4 = (lane >> 2) & 3, p4 = lane & 3;
+    const MMAD_LDS char* lds = (const MMAD_LDS char*)smem;
+    uint4v rvs[EPI == GEMM_EPI_SCORE ? NB : 1];
+    if constexpr (EPI == GEMM_EPI_SCORE) {
+      if (ep.ref) {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+          const int rbase = (w * RBW + u / CB) * 16, cbase = (u % CB) * 32;
+          rvs[u] = *(const uint4v*)((const TO*)ep.ref + (size_t)(m0 + rbase + n16) * ep.ldref + n0 +
+                                    cbase + 8 * g);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) rvs[u] = uint4v{0u, 0u, 0u, 0u};
+      }
+    }
+    float gpart[2] = {0.f, 0.f};   // SCORE: (T0 + T1), then T2 of one 128-column group
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int rbase = (w * RBW + u / CB) * 16, cbase = (u % CB) * 32;
+      const int k1 = cbase + 8 * g + q4, k2 = k1 + 4;
+      const int rb2 = (rbase + 4 * p4) * 2;
+      const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (MMAD_LDS short4v*)(lds + k1 * TCS + (rb2 ^ tsw(k1))));
+      const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (MMAD_LDS short4v*)(lds + k2 * TCS + (rb2 ^ tsw(k2))));
+      const bf16x4 l4 = __builtin_bit_cast(bf16x4, lo), h4 = __builtin_bit_cast(bf16x4, hi);
+      const bf16x8 v8 = __builtin_shufflevector(l4, h4, 0, 1, 2, 3, 4, 5, 6, 7);
+      const uint4v v = __builtin_bit_cast(uint4v, v8);
+      const int row = m0 + rbase + n16;
+      const int col = n0 + cbase + 8 * g;
+      if (out) *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
+      if constexpr (EPI == GEMM_EPI_SCORE) {
+        const uint4v rv = rvs[u];
+        const TO* pv = (const TO*)&v;
+        const TO* pr = (const TO*)&rv;
+        float wv[8];
+#pragma unroll
+        for (int e = 0; e < 8; e += 4) {
+          const floatx4 w4 = ep.colw ? *(const floatx4*)(ep.colw + col + e) : floatx4{1.f, 1.f, 1.f, 1.f};
+          wv[e] = w4[0]; wv[e + 1] = w4[1]; wv[e + 2] = w4[2]; wv[e + 3] = w4[3];
+        }
+        float sq = 0.f, dd[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          dd[e] = to_f32<TO>(pv[e]) - to_f32<TO>(pr[e]);
+          sq = fmaf(dd[e] * dd[e], wv[e], sq);
+        }
+        if (ep.diff && row < ep.M) {
+          float* dp = ep.diff + (size_t)row * ep.lddiff + col;
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (col + e < ep.N) dp[e] = dd[e];
+        }
+        // the 16 chunks k = 4 (cb % 4) + g of a 128-column group combine as
+        // the row-major path's butterfly (k ^ 1, k ^ 2, k ^ 4, k ^ 8):
+        // lanes g ^ 1 and g ^ 2 here, then the group's blocks in registers
+        sq = sum_lane_groups(sq);
+        const int qb = (u % CB) & 3;
+        if (qb == 0 || qb == 2) gpart[qb >> 1] = sq;
+        else if (qb == 1) gpart[0] = gpart[0] + sq;
+        else {
+          const float tot = gpart[0] + (gpart[1] + sq);
+          if (g == 0) ep.rowsq[(size_t)(col / 128) * ep.ldrow + row] = tot;
+        }
+      }
+    }
   } else {
     // SCORE: every reference chunk loaded before the loop's stores.  ref
     // null = 0 (NAP run: sum of squared outputs); colw: per-column weights
@@ -1320,7 +1451,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       const uint4v v = *(const uint4v*)(smem + rl * OSTRIDE + ch * 16);
       const int row = m0 + rl;
       const int col = n0 + ch * OEPC;
-      if (out && !(ep.dbg & 64)) {   // (dbg 64, epilogue studies: no output stores)
+      if (out) {
         *(uint4v*)(out + (size_t)row * ep.ldo + col) = v;
       }
       if constexpr (EPI == GEMM_EPI_SCORE) {
@@ -1705,7 +1836,7 @@ template <typename T, typename TO, bool AK, bool BK_, int CFG, int EPI>
 __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel(const T* __restrict__ A, int lda,
                                                            const T* __restrict__ B, int ldb, int K,
                                                            GemmEpi ep) {
-  gemm_body<T, TO, AK, BK_, CFG, EPI>(A, lda, B, ldb, K, ep, blockIdx.x, gridDim.x);
+  gemm_body<T, TO, AK, BK_, CFG, EPI>(A, lda, B, ldb, K, ep, blockIdx.x, gridDim.x, threadIdx.x);
 }
 
 // Persistent form (knob 12) of the forward-type bf16 GEMMs at large row
@@ -1724,7 +1855,12 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel_p(const T* _
                                                              GemmEpi ep) {
   const int nt = ep.persist_tiles;
   for (int v = blockIdx.x; v < nt; v += gridDim.x) {
-    gemm_body<T, TO, AK, BK_, CFG, EPI>(A, lda, B, ldb, K, ep, v, nt);
+    // the thread index passes through an opaque move every tile, so nothing
+    // derived from it is hoisted out of the tile loop (hoisted, those values
+    // stay live across the whole body and the 256-row tiles spill)
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    gemm_body<T, TO, AK, BK_, CFG, EPI>(A, lda, B, ldb, K, ep, v, nt, tid);
     __syncthreads();
   }
 }

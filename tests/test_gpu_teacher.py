@@ -161,7 +161,9 @@ def test_teacher_forced_step_within_reference_band(golden, fused):
             lim = 3 * t["band"] + FLOOR * t["scale"]
             worst.append((t["dev"] / lim if lim > 0 else 0.0, r["step"], t["t"]))
             assert t["dev"] <= lim, (r["step"], t)
-            if "ratio" in t:
+            # the step-size ratio where the deviation is above the ulp floor
+            # (an update of a few ulps makes a one-ulp difference a large ratio)
+            if "ratio" in t and t["dev"] > FLOOR * t["scale"]:
                 assert abs(t["ratio"]) <= 3 * t["ratio_band"] + 1e-6, (r["step"], t)
     worst.sort(reverse=True)
     print("worst dev / limit:", worst[:5])
@@ -177,9 +179,11 @@ def test_teacher_no_signed_bias(golden):
     ratios = np.array([t["ratio"] for r in rows for t in r["tensors"] if "ratio" in t and t["upd"] > 0])
     bands = np.array([t["ratio_band"] for r in rows for t in r["tensors"] if "ratio" in t and t["upd"] > 0])
     loss_devs = [r["loss_dev"] for r in rows]
-    pos = int((ratios > 0).sum())
-    n = len(ratios)
-    print(f"loss deviations {loss_devs}; step ratios: {pos} of {n} positive, "
-          f"mean {ratios.mean():+.3e} (band mean {bands.mean():.3e})")
-    # mean signed ratio inside the band's typical size: no consistent step-size bias
+    pos, neg = int((ratios > 0).sum()), int((ratios < 0).sum())
+    print(f"loss deviations {loss_devs}; step ratios: {pos} positive, {neg} negative, "
+          f"{len(ratios) - pos - neg} exact; mean {ratios.mean():+.3e} (band mean {bands.mean():.3e})")
+    # mean signed ratio inside the band's typical size (round 4's Adam, with
+    # 1 - beta formed in float, gave -7.7e-6 here: 16 of 156 positive), and
+    # the signs of the non-zero ratios not one-sided beyond 3 sigma of a fair coin
     assert abs(ratios.mean()) <= bands.mean() + 1e-7
+    assert abs(pos - neg) <= 3.0 * np.sqrt(pos + neg) + 1, (pos, neg)
