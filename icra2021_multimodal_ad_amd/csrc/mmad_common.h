@@ -12,6 +12,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short short4v __attribute__((ext_vector_type(4)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef unsigned int uint4v __attribute__((ext_vector_type(4)));
+typedef unsigned int uint2v __attribute__((ext_vector_type(2)));
 
 #define MMAD_LDS __attribute__((address_space(3)))
 
@@ -77,7 +78,7 @@ __device__ __forceinline__ float apply_act(float z, int act, float slope) {
 // scalar branch tree per element -- ~17k instructions of epilogue code, most
 // of a 256x256 tile's epilogue time in instruction fetch.  Same values as
 // apply_act for these three (z * 1 == z exactly; ReLU's 0 is +0).
-__device__ __forceinline__ bool act_is_linear_piecewise(int act) {
+__host__ __device__ __forceinline__ bool act_is_linear_piecewise(int act) {
   return act == MMAD_ACT_LEAKYRELU || act == MMAD_ACT_RELU || act == MMAD_ACT_NONE;
 }
 __device__ __forceinline__ float act_lo_slope(int act, float slope) {

@@ -68,19 +68,22 @@ template <> struct Cfg<5> { static constexpr int BM = 128, BN = 128, WM = 2, WN 
 // 16384 x 2048 x 1664 vs 0.33 for 256x128); its epilogue staging fills LDS
 constexpr int CFG_BIG = 6;
 template <> struct Cfg<6> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NS = 2, NT = 512; };
-// 7: 256x256, 8 waves (2 x 4, wave tile 128x64), STAGGERED: waves 4-7 run one
-// workgroup barrier behind waves 0-3, so on every SIMD one wave computes
-// (16 MFMAs) while its partner reads its next fragments and issues its share
-// of the LDS-DMA; 32-deep K-tiles in a 4-slot ring (32 KB each), 3 K-tiles in
-// flight (tile7_loop below; CFG 6's loop is the 2-slot, one-barrier-per-stage
-// form it replaces where it measures faster)
-constexpr int CFG_P8 = 7;
+// 7: 256x256, CFG 6's loop with the MFMA operands swapped (W first): each
+// lane's accumulator quad is then 4 consecutive COLUMNS of one output row, so
+// the forward / score epilogue stores from registers -- one v_permlane16_swap
+// pair turns two column tiles' quads into a 16-byte chunk per lane, 64 B per
+// row per store instruction -- with no LDS staging round trip (the score row
+// sums meet across the two waves of a 128-column group in 4 KB of LDS).
+// Eval forward / score only (no column partials: the BN statistics need the
+// row-quad layout); the dispatcher runs CFG 6 in its place otherwise (same
+// tile, same bits).
+constexpr int CFG_XST = 7;
 template <> struct Cfg<7> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NS = 2, NT = 512; };
 constexpr int NCFG = 8;
 constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256, 256};
 constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256, 256};
 constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512, 512};
-inline bool is_big(int cfg) { return cfg == CFG_BIG || cfg == CFG_P8; }
+inline bool is_big(int cfg) { return cfg == CFG_BIG || cfg == CFG_XST; }
 // the 256x256 tiles: bf16 operands, forward-type epilogues, no fused BN
 template <typename T, int EPI>
 constexpr bool big_ok() {
@@ -88,6 +91,16 @@ constexpr bool big_ok() {
 }
 inline bool big_ok_rt(int dtype, int epi) {
   return dtype == MMAD_BF16 && (epi == GEMM_EPI_FWD || epi == GEMM_EPI_MSE || epi == GEMM_EPI_SCORE);
+}
+// the register-direct 256x256 tile: eval forward / score, piecewise-linear
+// activations (act_is_linear_piecewise: declared in mmad_common.h)
+template <typename T, int EPI>
+constexpr bool xst_ok() {
+  return sizeof(T) == 2 && (EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_SCORE);
+}
+inline bool xst_ok_rt(int dtype, int epi, const GemmEpi& ep) {
+  return dtype == MMAD_BF16 && (epi == GEMM_EPI_FWD || epi == GEMM_EPI_SCORE) && !ep.part && !ep.bpart &&
+         act_is_linear_piecewise(ep.act);
 }
 
 template <typename T, bool KMAJ, int ROWS, int NT>
@@ -226,32 +239,6 @@ __device__ __forceinline__ floatx4 frag_f32(const char* img, int rbase, int kc, 
     }
     return r;
   }
-}
-
-// ---- CFG 7 image: [256 rows][64 B] per operand and K-tile (32 bf16 of K) --
-// 16-byte chunk j of row r stored at j ^ sw64(r).  A ds_read_b128 of 16 rows
-// (lane & 15) x chunk g (lane >> 4) is served in four 16-lane groups, e.g.
-// {0-3, 12-15, 20-27} = rows 0-3 and 12-15 at g, rows 4-11 at g^1; with
-// sw64 = (4 - ((r >> 2) & 3)) & 3 each group's 16 (row, chunk) pairs land on
-// 16 distinct 16-B bank slots of the 256-B bank row (conflict-free).  The
-// DMA writes the image lane-linearly; the swizzle is applied to the per-lane
-// global source address (an involution, undone on the read).
-__device__ __forceinline__ int sw64(int r) { return (4 - ((r >> 2) & 3)) & 3; }
-
-// chunk c (0..1) of one 256-row x 32-k operand image (16 KB = 1024 pieces of
-// 16 B; 512 threads x 2)
-__device__ __forceinline__ void stage64(char* img, const bf16* __restrict__ G, int ld, int r0, int k0,
-                                        int tid, int c) {
-  const int p = c * 512 + tid;
-  const int row = p >> 2;
-  const int j = (p & 3) ^ sw64(row);
-  dma16(G + (size_t)(r0 + row) * ld + k0 + j * 8, img + (c * 512 + (tid & ~63)) * 16);
-}
-
-// 16x16x32 operand fragment: rows rbase + (lane & 15), k = 8g..8g+7 (g = lane >> 4)
-__device__ __forceinline__ bf16x8 frag64(const char* img, int rbase, int lane) {
-  const int m = rbase + (lane & 15);
-  return *(const bf16x8*)(img + m * 64 + (((lane >> 4) ^ sw64(m)) << 4));
 }
 
 // every phase of the main loop pinned in issue order
@@ -441,8 +428,10 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   constexpr int SLOT = IA::BYTES + IB::BYTES;
   constexpr int NL = IA::CHUNKS + IB::CHUNKS;          // vm ops per thread per stage
   constexpr bool FWDLIKE = EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_MSE || EPI == GEMM_EPI_SCORE;
-  constexpr bool BIG = CFG == CFG_BIG || CFG == CFG_P8;
+  constexpr bool BIG = CFG == CFG_BIG || CFG == CFG_XST;
+  constexpr bool XST = CFG == CFG_XST;
   static_assert(!BIG || big_ok<T, EPI>(), "256x256 tile: bf16 forward-type epilogues only");
+  static_assert(!XST || xst_ok<T, EPI>(), "CFG 7: bf16 eval forward / score only");
   // prefetched bias partials per lane (none for the 256x256 tile: its
   // 128 accumulator registers leave no room to hold them across the loop)
   constexpr int QB = BIG ? 0 : 8;
@@ -674,116 +663,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       for (int r = 0; r < 16; ++r)
         pf_a[u][r] = an[(size_t)(m0 + (grp + u * B_NG) * 16 + r) * ep.ldo + n0 + cc];
   };
-  if constexpr (CFG == CFG_P8) {
-    // ---- staggered 256x256 loop ------------------------------------------
-    // K-tile t (32 deep) lives in ring slot t % 4: A image | B image, 16 KB
-    // each.  Per K-tile every wave runs two load segments (L) and two compute
-    // segments (C), each closed by a workgroup barrier:
-    //   L(2t):   B fragments (4 n-tiles) + A top (4 m-tiles); DMA chunk 0 of
-    //            both operands of K-tile t+3 (2 issues)
-    //   C(2t):   16 MFMAs, rows 0..63 of the wave tile
-    //   L(2t+1): A bottom; vmcnt retires K-tile t+1; DMA chunk 1 of t+3
-    //   C(2t+1): 16 MFMAs, rows 64..127
-    // Waves 4-7 (the SIMD partners of waves 0-3) pass one extra barrier first,
-    // so every barrier closes one group's load segment and the other group's
-    // compute segment: each SIMD's matrix pipe is fed by one wave while its
-    // partner loads.  Every load segment ends with lgkmcnt(0), so the reads
-    // of segment L(j) are complete at the barrier that closes it.
-    // Correctness by barrier count (group 0 closes L(j) at barrier 2j, group 1
-    // at 2j+1):
-    //  * WAR: K-tile t+3 overwrites slot (t-1) % 4, last read in L(2t-1) and
-    //    closed by barrier 4t-1 (group 1); its first DMA issue is in L(2t),
-    //    which opens after barrier 4t-1 (group 0) / 4t (group 1).
-    //  * RAW: K-tile u is first read in L(2u), after barrier 4u-1 (group 0) /
-    //    4u (group 1); every wave retires its own DMAs of u with the counted
-    //    vmcnt in L(2u-1), which closes at barrier <= 4u-1, and the DMA data
-    //    is ordered for other waves by that barrier.
-    // The K accumulation order per output element is the same as every other
-    // tile's (32-deep MFMA steps in k order): results are bit-identical.
-    static_assert(sizeof(T) == 2 && AK && BK_ && BM == 256 && BN == 256 && TM == 8 && TN == 4,
-                  "CFG 7: bf16, K-major operands");
-    constexpr int SL = 32768, HB = 16384;
-    const int grp = w >> 2;
-    const int ntk = (ep.dbg & 1) ? 0 : Ks / 32;
-    auto slot = [&](int t) -> char* { return smem + (t & 3) * SL; };
-    // diagnostics (dbg bits, loop studies only): 16 = no DMA inside the loop
-    // (the MFMAs read stale slots), 32 = no MFMAs (accumulators stay live)
-    const bool d_nodma = ep.dbg & 16, d_nomfma = ep.dbg & 32;
-    auto dma = [&](int t, int c) {
-      if (t >= 3 && d_nodma) return;
-      stage64(slot(t), A, lda, m0, kbase + t * 32, tid, c);
-      stage64(slot(t) + HB, B, ldb, n0, kbase + t * 32, tid, c);
-    };
-    if (ntk > 0) {
-      bf16x8 fa[4], fb[4];
-#pragma unroll
-      for (int u = 0; u < 3; ++u)
-        if (u < ntk) { dma(u, 0); dma(u, 1); }
-      // K-tile 0 landed (1 and 2 may stay in flight)
-      if (ntk >= 3) wait_vmcnt<8>();
-      else if (ntk == 2) wait_vmcnt<4>();
-      else wait_vmcnt<0>();
-      block_barrier();
-      if (grp) block_barrier();            // the stagger
-      for (int t = 0; t < ntk; ++t) {
-        const char* sa = slot(t);
-        const char* sb = sa + HB;
-        // ---- L(2t)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) fb[j] = frag64(sb, rb + j * 16, lane);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = frag64(sa, ra + i * 16, lane);
-        if (t + 3 < ntk) dma(t + 3, 0);
-        wait_lgkm0();
-        MMAD_SB();
-        block_barrier();
-        // ---- C(2t)
-        __builtin_amdgcn_s_setprio(1);
-        if (!d_nomfma) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-        } else {
-          asm volatile("" ::"v"(fa[0]), "v"(fa[1]), "v"(fa[2]), "v"(fa[3]), "v"(fb[0]), "v"(fb[1]),
-                       "v"(fb[2]), "v"(fb[3]));
-        }
-        __builtin_amdgcn_s_setprio(0);
-        MMAD_SB();
-        block_barrier();
-        // ---- L(2t+1)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = frag64(sa, ra + (4 + i) * 16, lane);
-        if (t + 1 < ntk) {
-          // retire K-tile t+1: newer in flight are K-tile t+2 (4 issues) and
-          // chunk 0 of t+3 (2), where they exist
-          if (t + 3 < ntk) wait_vmcnt<6>();
-          else if (t + 2 < ntk) wait_vmcnt<4>();
-          else wait_vmcnt<0>();
-        }
-        if (t + 3 < ntk) dma(t + 3, 1);
-        wait_lgkm0();
-        MMAD_SB();
-        block_barrier();
-        // ---- C(2t+1)
-        __builtin_amdgcn_s_setprio(1);
-        if (!d_nomfma) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[4 + i][j], 0, 0, 0);
-        } else {
-          asm volatile("" ::"v"(fa[0]), "v"(fa[1]), "v"(fa[2]), "v"(fa[3]));
-        }
-        __builtin_amdgcn_s_setprio(0);
-        MMAD_SB();
-        block_barrier();
-      }
-      if (!grp) block_barrier();           // both groups: 4 * ntk + 2 barriers
-    }
-  } else if constexpr (BIG) {
+  if constexpr (BIG) {
     // 256x256 tile (bf16, both operands K-major): a 2-slot ring, one barrier
     // per stage after both 32-deep sub-steps; the fragment registers of a
     // sub-step are re-read row by row under the MFMAs that free them (their
@@ -800,6 +680,9 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         for (int j = 0; j < TN; ++j) fb[sl][j] = frag_bf16<true, true, BN>(base + IA::BYTES, rb + j * 16, kk, lane);
       };
       int pend = -1;
+      // diagnostics (dbg bit 16, loop studies only): no DMA after the
+      // prologue (the MFMAs read stale slots)
+      const bool d_nodma = ep.dbg & 16;
       issue(0);
       if (nt > 1) issue(1);
       if (nt > 1) wait_vmcnt<NL>();
@@ -812,8 +695,9 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         for (int i = 0; i < TM; ++i) {
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
-          if (pend >= 0) {
+            acc[i][j] = XST ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[0][j], fa[0][i], acc[i][j], 0, 0, 0)
+                            : __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0][i], fb[0][j], acc[i][j], 0, 0, 0);
+          if (pend >= 0 && !d_nodma) {
 #pragma unroll
             for (int q = 0; q < NL; ++q)
               if (q * TM / NL == i) issue_q(pend, q);
@@ -830,7 +714,8 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1][i], fb[1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = XST ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[1][j], fa[1][i], acc[i][j], 0, 0, 0)
+                            : __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1][i], fb[1][j], acc[i][j], 0, 0, 0);
         if (t + 1 < nt) {
           wait_vmcnt<0>();                   // stage t+1 landed (the only one in flight)
           wait_lgkm0();
@@ -1046,6 +931,115 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
 #pragma unroll
       for (int j = 0; j < TN; ++j) sum += acc[i][j][0];
     if (sum == 1.2345e-30f) ((float*)ep.out)[tid] = sum;
+    return;
+  }
+  if constexpr (XST) {
+    // ===================== CFG 7 epilogue (registers -> HBM) ================
+    // acc[i][j] of lane (c, g): output row rw + i*16 + c, columns
+    // cw + j*16 + 4g .. +3 (W was the MFMA's first operand).  Per element the
+    // same arithmetic as the row-quad epilogue below: act(acc + bias), then
+    // the BN-eval affine, masked outside M x N, rounded to bf16.  Column tiles
+    // 2h and 2h+1 are stored together: v_permlane16_swap of their quads gives
+    // lane g the 8 columns 8(g>>1) .. +7 of tile 2h + (g&1) (16 B).
+    // (piecewise-linear activations only: LeakyReLU / ReLU / none; sigmoid /
+    // tanh layers run on CFG 6, xst_ok_rt)
+    const bool pw_relu = ep.act == MMAD_ACT_RELU;
+    const float pw_lo = act_lo_slope(ep.act, ep.slope);
+    auto cvec = [&](const float* p, int col, float dflt) -> floatx4 {
+      return p ? *(const floatx4*)(p + col) : floatx4{dflt, dflt, dflt, dflt};
+    };
+    TO* out = (TO*)ep.out;
+    const int jl = g & 1, coff = 8 * (g >> 1);
+    float rsum[EPI == GEMM_EPI_SCORE ? TM : 1];   // this wave's 64-column row sums
+#pragma unroll
+    for (int h = 0; h < TN / 2; ++h) {
+      floatx4 cb[2], cs[2], ct[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int col = cw + (2 * h + u) * 16 + 4 * g;
+        cb[u] = cvec(ep.bias, col, 0.f);
+        cs[u] = cvec(ep.bn_scale, col, 1.f);
+        ct[u] = cvec(ep.bn_shift, col, 0.f);
+      }
+      const int col0 = cw + (2 * h + jl) * 16 + coff;   // this lane's chunk after the swap
+      uint4v rvs[EPI == GEMM_EPI_SCORE ? TM : 1];
+      if constexpr (EPI == GEMM_EPI_SCORE) {
+        if (ep.ref) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            rvs[i] = *(const uint4v*)((const TO*)ep.ref + (size_t)(rw + i * 16 + c) * ep.ldref + col0);
+        } else {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) rvs[i] = uint4v{0u, 0u, 0u, 0u};
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = rw + i * 16 + c;
+        unsigned d[2][2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int j = 2 * h + u;
+          bf16x4 q;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int col = cw + j * 16 + 4 * g + r;
+            float v = acc[i][j][r];
+            v = fmaf(apply_act_pw(v + cb[u][r], pw_relu, pw_lo), cs[u][r], ct[u][r]);
+            v = (row < ep.M && col < ep.N) ? v : 0.f;
+            q[r] = (bf16)v;
+          }
+          const uint2v qq = __builtin_bit_cast(uint2v, q);
+          d[u][0] = qq[0];
+          d[u][1] = qq[1];
+        }
+        const auto s0 = __builtin_amdgcn_permlane16_swap(d[0][0], d[1][0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(d[0][1], d[1][1], false, false);
+        const uint4v v = uint4v{s0[0], s1[0], s0[1], s1[1]};
+        if (out) *(uint4v*)(out + (size_t)row * ep.ldo + col0) = v;
+        if constexpr (EPI == GEMM_EPI_SCORE) {
+          const TO* pv = (const TO*)&v;
+          const TO* pr = (const TO*)&rvs[i];
+          float wv[8];
+#pragma unroll
+          for (int e = 0; e < 8; e += 4) {
+            const floatx4 w4 = cvec(ep.colw, col0 + e, 1.f);
+            wv[e] = w4[0]; wv[e + 1] = w4[1]; wv[e + 2] = w4[2]; wv[e + 3] = w4[3];
+          }
+          float sq = 0.f, dd[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            dd[e] = to_f32<TO>(pv[e]) - to_f32<TO>(pr[e]);
+            sq = fmaf(dd[e] * dd[e], wv[e], sq);
+          }
+          if (ep.diff && row < ep.M) {
+            float* dp = ep.diff + (size_t)row * ep.lddiff + col0;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (col0 + e < ep.N) dp[e] = dd[e];
+          }
+          // chunks 4h + {0, 1, 2, 3} of the wave's 8 sit in lanes g = 0, 2,
+          // 1, 3: (k0 + k1) + (k2 + k3), the row-major butterfly's order
+          sq += lane_xor32(sq);
+          sq += lane_xor16(sq);
+          rsum[i] = h == 0 ? sq : rsum[i] + sq;
+        }
+      }
+    }
+    if constexpr (EPI == GEMM_EPI_SCORE) {
+      // the two waves of a 128-column group: (k0..k7) + (k8..k15)
+      float* srs = (float*)smem;                 // [WN][BM]
+      __syncthreads();                           // ring LDS no longer read
+      if (g == 0) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) srs[wn * BM + wm * 16 * TM + i * 16 + c] = rsum[i];
+      }
+      __syncthreads();
+      static_assert(NT == 2 * BM && WN == 4, "one row-sum per thread");
+      const int gi = tid / BM, rl = tid % BM;
+      const float tot = srs[(2 * gi) * BM + rl] + srs[(2 * gi + 1) * BM + rl];
+      ep.rowsq[(size_t)((n0 >> 7) + gi) * ep.ldrow + m0 + rl] = tot;
+    }
     return;
   }
   if constexpr (FWDLIKE && BIG) load_epi_consts();
@@ -1954,6 +1948,8 @@ static int persist_capacity(const void* fn, int epi, int cfg) {
 template <typename T, typename TO, bool AK, bool BK_, int EPI>
 static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np, int K,
                         const GemmEpi& ep_in, int cfg, hipStream_t s) {
+  // CFG 7 outside its epilogues (column partials, MSE): CFG 6, the same tile
+  if (cfg == CFG_XST && !xst_ok_rt(sizeof(T) == 2 ? MMAD_BF16 : MMAD_F32, EPI, ep_in)) cfg = CFG_BIG;
   const int BM = CFG_BM[cfg], BN = CFG_BN[cfg];
   const int tiles_m = Mp / BM, tiles_n = Np / BN, ntiles = tiles_m * tiles_n;
   GemmEpi ep = ep_in;
@@ -2005,8 +2001,13 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
     case 5: go(mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI>); break;
     default:
       if constexpr (big_ok<T, EPI>()) {
-        if (cfg == CFG_P8) go(mmad_gemm_kernel<T, TO, AK, BK_, CFG_P8, EPI>);
-        else go(mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI>);
+        if constexpr (xst_ok<T, EPI>()) {
+          if (cfg == CFG_XST) {
+            go(mmad_gemm_kernel<T, TO, AK, BK_, CFG_XST, EPI>);
+            break;
+          }
+        }
+        go(mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI>);
       } else {
         mmad_set_error("gemm: tile configuration %d does not support this dtype / epilogue", cfg);
         return MMAD_EUNSUPPORTED;
@@ -2028,9 +2029,9 @@ static const void* kernel_ptr(int cfg) {
     case 4: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI>;
     case 5: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI>;
     default:
-      if constexpr (big_ok<T, EPI>())
-        return cfg == CFG_P8 ? (const void*)mmad_gemm_kernel<T, TO, AK, BK_, CFG_P8, EPI>
-                             : (const void*)mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI>;
+      if constexpr (xst_ok<T, EPI>())
+        if (cfg == CFG_XST) return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, CFG_XST, EPI>;
+      if constexpr (big_ok<T, EPI>()) return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, CFG_BIG, EPI>;
       return nullptr;
   }
 }

@@ -250,3 +250,65 @@ def test_persistent_grid_bit_identical(kind):
     finally:
         lib.mmad_tune_set(0, -1)
         lib.mmad_tune_set(12, 0)
+
+
+@pytest.mark.parametrize("case", ["fwd_leaky_bn", "fwd_relu", "fwd_none", "score_ref_diff", "score_nodiff",
+                                  "nap_colw", "fwd_stats_fallback", "fwd_sigmoid_fallback"])
+def test_register_direct_tile_bit_identical(case):
+    """Tile 7 (256x256 with the MFMA operands swapped, the epilogue stored from
+    registers through v_permlane16_swap) against the row-quad tiles 6 / 1 / 2:
+    bit-identical outputs, score row sums and diffs, on a shape with masked
+    rows and columns (M = 4000 of 4096, N = 2000 of 2048).  The forward with
+    BN-statistic partials and the sigmoid forward run CFG 6 in its place
+    (same tile, same bits)."""
+    lib = _native.load()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    M, N, K = 4000, 2000, 1658
+    Mp, Np, Kp = pad(M), pad(N), pad(K)
+    x = torch.zeros(Mp, Kp, device=dev, dtype=torch.bfloat16)
+    x[:M, :K] = torch.randn(M, K, device=dev, generator=g).bfloat16()
+    w = torch.zeros(Np, Kp, device=dev, dtype=torch.bfloat16)
+    w[:N, :K] = (torch.randn(N, K, device=dev, generator=g) * 0.05).bfloat16()
+    b = torch.randn(Np, device=dev, generator=g) * 0.1
+    sc = 1.0 + 0.1 * torch.randn(Np, device=dev, generator=g)
+    sh = 0.1 * torch.randn(Np, device=dev, generator=g)
+    ref = torch.zeros(Mp, Np, device=dev, dtype=torch.bfloat16)
+    ref[:M, :N] = torch.randn(M, N, device=dev, generator=g).bfloat16()
+    colw = torch.zeros(Np, device=dev)
+    colw[:N] = torch.rand(N, device=dev, generator=g) + 0.5
+    s = stream_ptr()
+
+    def run():
+        y = torch.zeros(Mp, Np, device=dev, dtype=torch.bfloat16)
+        rows = torch.zeros(Np // 128, Mp, device=dev)
+        diff = torch.zeros(M, N, device=dev)
+        part = torch.zeros(Mp // 32, 2, Np, device=dev)
+        act = {"fwd_relu": 2, "fwd_none": 0, "fwd_sigmoid_fallback": 3}.get(case, 1)
+        if case.startswith("fwd"):
+            bn = case == "fwd_leaky_bn"
+            call("mmad_fc_fwd", BF16, M, N, K, Mp, Np, Kp, ptr(x), ptr(w), ptr(b), act, 0.2,
+                 ptr(sc) if bn else None, ptr(sh) if bn else None, ptr(y),
+                 ptr(part) if case == "fwd_stats_fallback" else None, s)
+            return y, part
+        if case == "nap_colw":
+            score = torch.zeros(Mp, device=dev)
+            call("mmad_nap_score", BF16, M, K, N, Mp, Kp, Np, ptr(x), ptr(w), ptr(b), ptr(colw),
+                 ptr(rows), ptr(score), s)
+            return rows, score
+        call("mmad_fc_fwd_score", BF16, M, N, K, Mp, Np, Kp, ptr(x), ptr(w), ptr(b), 1, 0.2, ptr(sc),
+             ptr(sh), ptr(y), ptr(ref), ptr(rows),
+             ptr(diff) if case == "score_ref_diff" else None, N, s)
+        return y, rows, diff
+    outs = {}
+    try:
+        for tile in (6, 7, 1, 2):
+            lib.mmad_tune_set(0, tile)
+            outs[tile] = run()
+        torch.cuda.synchronize()
+    finally:
+        lib.mmad_tune_set(0, -1)
+    assert float(outs[6][0].float().abs().sum()) > 0
+    for tile in (7, 1, 2):
+        for a, b2 in zip(outs[6], outs[tile]):
+            assert torch.equal(a, b2), (case, tile)
