@@ -79,11 +79,22 @@ template <> struct Cfg<6> { static constexpr int BM = 256, BN = 256, WM = 2, WN 
 // tile, same bits).
 constexpr int CFG_XST = 7;
 template <> struct Cfg<7> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NS = 2, NT = 512; };
-constexpr int NCFG = 8;
-constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256, 256};
-constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256, 256};
-constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512, 512};
-inline bool is_big(int cfg) { return cfg == CFG_BIG || cfg == CFG_XST; }
+// 8: 256x256, FOUR waves (2 x 2, wave tile 128x128: 256 accumulator
+// registers per lane, in AGPRs), otherwise CFG 7 (swapped operands,
+// register-direct epilogue).  One wave per SIMD: per 32-deep step a wave
+// issues 64 MFMAs against 16 fragment reads, a third fewer LDS reads per MFMA
+// than the 8-wave 128x64 wave tiles.  Compiled in its own translation unit
+// (this file with MMAD_GEMM_B4_TU, csrc/Makefile) WITHOUT the VGPR-form MFMA
+// flag the other tiles use: 256 + ~150 registers need the AGPR half of the
+// file; the host side reaches it through mmad_gemm_b4_launch.
+constexpr int CFG_B4 = 8;
+template <> struct Cfg<8> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 2, NS = 2, NT = 256; };
+constexpr int NCFG = 9;
+constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256, 256, 256};
+constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256, 256, 256};
+constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512, 512, 256};
+inline bool is_big(int cfg) { return cfg == CFG_BIG || cfg == CFG_XST || cfg == CFG_B4; }
+inline bool is_xst(int cfg) { return cfg == CFG_XST || cfg == CFG_B4; }
 // the 256x256 tiles: bf16 operands, forward-type epilogues, no fused BN
 template <typename T, int EPI>
 constexpr bool big_ok() {
@@ -428,10 +439,10 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   constexpr int SLOT = IA::BYTES + IB::BYTES;
   constexpr int NL = IA::CHUNKS + IB::CHUNKS;          // vm ops per thread per stage
   constexpr bool FWDLIKE = EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_MSE || EPI == GEMM_EPI_SCORE;
-  constexpr bool BIG = CFG == CFG_BIG || CFG == CFG_XST;
-  constexpr bool XST = CFG == CFG_XST;
+  constexpr bool BIG = CFG == CFG_BIG || CFG == CFG_XST || CFG == CFG_B4;
+  constexpr bool XST = CFG == CFG_XST || CFG == CFG_B4;
   static_assert(!BIG || big_ok<T, EPI>(), "256x256 tile: bf16 forward-type epilogues only");
-  static_assert(!XST || xst_ok<T, EPI>(), "CFG 7: bf16 eval forward / score only");
+  static_assert(!XST || xst_ok<T, EPI>(), "CFG 7 / 8: bf16 eval forward / score only");
   // prefetched bias partials per lane (none for the 256x256 tile: its
   // 128 accumulator registers leave no room to hold them across the loop)
   constexpr int QB = BIG ? 0 : 8;
@@ -950,7 +961,8 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
     };
     TO* out = (TO*)ep.out;
     const int jl = g & 1, coff = 8 * (g >> 1);
-    float rsum[EPI == GEMM_EPI_SCORE ? TM : 1];   // this wave's 64-column row sums
+    float rsum[EPI == GEMM_EPI_SCORE ? TM : 1];   // this wave's 64-column row sums (WN = 4)
+    float rsum2[EPI == GEMM_EPI_SCORE ? TM : 1][2];   // (WN = 2) the two 64-column halves
 #pragma unroll
     for (int h = 0; h < TN / 2; ++h) {
       floatx4 cb[2], cs[2], ct[2];
@@ -1022,11 +1034,20 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
           // 1, 3: (k0 + k1) + (k2 + k3), the row-major butterfly's order
           sq += lane_xor32(sq);
           sq += lane_xor16(sq);
-          rsum[i] = h == 0 ? sq : rsum[i] + sq;
+          if constexpr (WN == 4) {
+            rsum[i] = h == 0 ? sq : rsum[i] + sq;
+          } else {
+            // 128 columns per wave: ((Q0 + Q1) + (Q2 + Q3)), written here
+            static_assert(TN == 8, "one 128-column group per wave");
+            if (h == 0 || h == 2) rsum2[i][h >> 1] = sq;
+            else rsum2[i][h >> 1] = rsum2[i][h >> 1] + sq;
+            if (h == 3 && g == 0)
+              ep.rowsq[(size_t)(cw >> 7) * ep.ldrow + row] = rsum2[i][0] + rsum2[i][1];
+          }
         }
       }
     }
-    if constexpr (EPI == GEMM_EPI_SCORE) {
+    if constexpr (EPI == GEMM_EPI_SCORE && WN == 4) {
       // the two waves of a 128-column group: (k0..k7) + (k8..k15)
       float* srs = (float*)smem;                 // [WN][BM]
       __syncthreads();                           // ring LDS no longer read
@@ -1859,6 +1880,31 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel_p(const T* _
   }
 }
 
+#ifdef MMAD_GEMM_B4_TU
+// ---- the 4-wave 256x256 translation unit: its launcher only --------------
+int mmad_gemm_b4_launch(int epi, const void* A, int lda, const void* B, int ldb, int Mp, int Np, int K,
+                        const GemmEpi& ep, hipStream_t s) {
+  dim3 grd((Mp / 256) * (Np / 256)), blk(256);
+  auto go = [&](auto kern) {
+    if (ep.done_ev)
+      hipExtLaunchKernelGGL(kern, grd, blk, 0u, s, nullptr, ep.done_ev, 0u, (const bf16*)A, lda,
+                            (const bf16*)B, ldb, K, ep);
+    else
+      kern<<<grd, blk, 0, s>>>((const bf16*)A, lda, (const bf16*)B, ldb, K, ep);
+  };
+  if (epi == GEMM_EPI_FWD) go(mmad_gemm_kernel<bf16, bf16, true, true, CFG_B4, GEMM_EPI_FWD>);
+  else if (epi == GEMM_EPI_SCORE) go(mmad_gemm_kernel<bf16, bf16, true, true, CFG_B4, GEMM_EPI_SCORE>);
+  else {
+    mmad_set_error("gemm: tile 8 runs the eval forward / score epilogues only");
+    return MMAD_EUNSUPPORTED;
+  }
+  MMAD_LAUNCH_CHECK();
+  return MMAD_OK;
+}
+#else
+int mmad_gemm_b4_launch(int epi, const void* A, int lda, const void* B, int ldb, int Mp, int Np, int K,
+                        const GemmEpi& ep, hipStream_t s);
+
 // -------------------------------------------------------------------------
 // host-side planning and launch
 // -------------------------------------------------------------------------
@@ -1948,8 +1994,9 @@ static int persist_capacity(const void* fn, int epi, int cfg) {
 template <typename T, typename TO, bool AK, bool BK_, int EPI>
 static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np, int K,
                         const GemmEpi& ep_in, int cfg, hipStream_t s) {
-  // CFG 7 outside its epilogues (column partials, MSE): CFG 6, the same tile
-  if (cfg == CFG_XST && !xst_ok_rt(sizeof(T) == 2 ? MMAD_BF16 : MMAD_F32, EPI, ep_in)) cfg = CFG_BIG;
+  // CFG 7 / 8 outside their epilogues (column partials, MSE, sigmoid / tanh):
+  // CFG 6, the same 256x256 tile
+  if (is_xst(cfg) && !xst_ok_rt(sizeof(T) == 2 ? MMAD_BF16 : MMAD_F32, EPI, ep_in)) cfg = CFG_BIG;
   const int BM = CFG_BM[cfg], BN = CFG_BN[cfg];
   const int tiles_m = Mp / BM, tiles_n = Np / BN, ntiles = tiles_m * tiles_n;
   GemmEpi ep = ep_in;
@@ -1981,6 +2028,9 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
         return MMAD_OK;
       }
     }
+  }
+  if (cfg == CFG_B4) {
+    if constexpr (xst_ok<T, EPI>()) return mmad_gemm_b4_launch(EPI, A, lda, B, ldb, Mp, Np, K, ep, s);
   }
   dim3 grd(ntiles * S), blk(CFG_NT[cfg]);
   const size_t dyn = 0;
@@ -2148,6 +2198,7 @@ static int tune_cfg(int dtype, int epi, const void* A, int lda, const void* B, i
   for (int c = 0; c < NCFG && rc == MMAD_OK; ++c) {
     if (!cfg_fits(c, Mp, Np, epi, dtype)) continue;
     if (is_big(c) && (ep.bn_sync || ep.splitk > 1)) continue;   // no fused BN / split on 256x256
+    if (c == CFG_B4) continue;   // the 4-wave tile: forced only (measured slower)
     if (ep.bn_sync && !coresident(dtype, epi, c, Mp, Np)) continue;
     rc = launch_cfg(dtype, epi, A, lda, B, ldb, Mp, Np, K, et, c, s);   // warm
     if (rc != MMAD_OK) break;
@@ -2313,3 +2364,4 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   if (cfg_used) *cfg_used = cfg;
   return launch_cfg(dtype, epi, A, lda, B, ldb, Mp, Np, K, ep, cfg, s);
 }
+#endif  // MMAD_GEMM_B4_TU

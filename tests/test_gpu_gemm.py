@@ -255,8 +255,9 @@ def test_persistent_grid_bit_identical(kind):
 @pytest.mark.parametrize("case", ["fwd_leaky_bn", "fwd_relu", "fwd_none", "score_ref_diff", "score_nodiff",
                                   "nap_colw", "fwd_stats_fallback", "fwd_sigmoid_fallback"])
 def test_register_direct_tile_bit_identical(case):
-    """Tile 7 (256x256 with the MFMA operands swapped, the epilogue stored from
-    registers through v_permlane16_swap) against the row-quad tiles 6 / 1 / 2:
+    """Tiles 7 and 8 (256x256 with the MFMA operands swapped, the epilogue
+    stored from registers through v_permlane16_swap; 8 waves / 4 waves with
+    AGPR accumulators) against the row-quad tiles 6 / 1 / 2:
     bit-identical outputs, score row sums and diffs, on a shape with masked
     rows and columns (M = 4000 of 4096, N = 2000 of 2048).  The forward with
     BN-statistic partials and the sigmoid forward run CFG 6 in its place
@@ -302,13 +303,13 @@ def test_register_direct_tile_bit_identical(case):
         return y, rows, diff
     outs = {}
     try:
-        for tile in (6, 7, 1, 2):
+        for tile in (6, 7, 8, 1, 2):
             lib.mmad_tune_set(0, tile)
             outs[tile] = run()
         torch.cuda.synchronize()
     finally:
         lib.mmad_tune_set(0, -1)
     assert float(outs[6][0].float().abs().sum()) > 0
-    for tile in (7, 1, 2):
+    for tile in (7, 8, 1, 2):
         for a, b2 in zip(outs[6], outs[tile]):
             assert torch.equal(a, b2), (case, tile)
