@@ -421,11 +421,43 @@ __device__ __forceinline__ bool col_wait(unsigned* ctr, unsigned gen0, unsigned*
 // dW GEMM contracts the raw activation and fixes up in the epilogue
 // (dW = scale[k] * acc + shift[k] * db[n]).  Every GEMM is a plain MFMA
 // contraction.
+// XCD-aware order (1-D grid).  Under round-robin dispatch, blocks with equal
+// bid % 8 share an XCD (speed only, never correctness); each such set gets a
+// contiguous range of logical blocks lt; the S split-K blocks of one output
+// tile are consecutive in lt (one XCD), and tiles are grouped group_m M-tiles
+// at a time so every XCD works on a compact rectangle whose A/B panels stay
+// in its L2.
+struct TileCoord {
+  int tm, tn, tile, sk;
+};
+__device__ __forceinline__ TileCoord tile_coord(const GemmEpi& ep, int bid, int nblk, int S) {
+  TileCoord tc;
+  const int ntl = nblk / S;
+  const int q = nblk >> 3, r = nblk & 7, xcd = bid & 7;
+  const int lt = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  tc.tile = lt / S;
+  tc.sk = lt - tc.tile * S;
+  const int tiles_m = ntl / ep.tiles_n;
+  const int per_group = ep.group_m * ep.tiles_n;
+  const int first_m = (tc.tile / per_group) * ep.group_m;
+  const int gsz = min(tiles_m - first_m, ep.group_m);
+  tc.tm = first_m + (tc.tile % per_group) % gsz;
+  tc.tn = (tc.tile % per_group) / gsz;
+  return tc;
+}
+
 // The body of one output tile; `bid` / `nblk` = the block index / block count.
-template <typename T, typename TO, bool AK, bool BK_, int CFG, int EPI>
+// Persistent CFG 7 (mmad_gemm_kernel_p): `pre` = this tile's first two K
+// stages were issued by the previous tile's epilogue; `next_bid` >= 0 = issue
+// that tile's first two stages at the start of this tile's epilogue (its
+// stores then drain under the next tile's prologue instead of before it).
+// (PST: the persistent kernel's own instantiation -- shared with the ordinary
+// kernel, the body's lambdas would have two callers and stay out of line)
+template <typename T, typename TO, bool AK, bool BK_, int CFG, int EPI, bool PST = false>
 __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, const T* __restrict__ B,
                                           int ldb, int K, const GemmEpi& ep, const int bid,
-                                          const int nblk, const int tid_in) {
+                                          const int nblk, const int tid_in, const bool pre = false,
+                                          const int next_bid = -1) {
   using C = Cfg<CFG>;
   constexpr int BM = C::BM, BN = C::BN, WM = C::WM, WN = C::WN, NS = C::NS, NT = C::NT;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;   // 16x16 MFMA tiles per wave
@@ -472,27 +504,10 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
 
   const int tid = tid_in, lane = tid & 63, w = tid >> 6;
   const int wm = w / WN, wn = w % WN;
-  // XCD-aware order (1-D grid).  Under round-robin dispatch, blocks with equal
-  // bid % 8 share an XCD (speed only, never correctness); each such set gets a
-  // contiguous range of logical blocks lt; the S split-K blocks of one output
-  // tile are consecutive in lt (one XCD), and tiles are grouped group_m M-tiles
-  // at a time so every XCD works on a compact rectangle whose A/B panels stay
-  // in its L2.
   const int S = ep.splitk > 1 ? ep.splitk : 1;
   const int ntl = nblk / S;                 // output tiles
-  int tm, tn, tile, sk;
-  {
-    const int q = nblk >> 3, r = nblk & 7, xcd = bid & 7;
-    const int lt = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-    tile = lt / S;
-    sk = lt - tile * S;
-    const int tiles_m = ntl / ep.tiles_n;
-    const int per_group = ep.group_m * ep.tiles_n;
-    const int first_m = (tile / per_group) * ep.group_m;
-    const int gsz = min(tiles_m - first_m, ep.group_m);
-    tm = first_m + (tile % per_group) % gsz;
-    tn = (tile % per_group) / gsz;
-  }
+  const TileCoord tc = tile_coord(ep, bid, nblk, S);
+  const int tm = tc.tm, tn = tc.tn, tile = tc.tile, sk = tc.sk;
   const int m0 = tm * BM, n0 = tn * BN;
   const int Ks = K / S, kbase = sk * Ks;
   const int nt = (ep.dbg & 1) ? 0 : Ks / IA::BK;
@@ -694,9 +709,13 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       // diagnostics (dbg bit 16, loop studies only): no DMA after the
       // prologue (the MFMAs read stale slots)
       const bool d_nodma = ep.dbg & 16;
-      issue(0);
-      if (nt > 1) issue(1);
-      if (nt > 1) wait_vmcnt<NL>();
+      if (!(PST && pre)) {
+        issue(0);
+        if (nt > 1) issue(1);
+      }
+      // (pre: the previous tile's epilogue stores are younger than these
+      // stages -- wait for everything)
+      if (nt > 1 && !(PST && pre)) wait_vmcnt<NL>();
       else wait_vmcnt<0>();
       block_barrier();
       rd(0, 0, 0);
@@ -945,6 +964,20 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
     return;
   }
   if constexpr (XST) {
+    if (PST && next_bid >= 0) {
+      // persistent: the next tile's first two K stages into the ring now (every
+      // wave has consumed its last fragments: the barrier orders the refill)
+      __syncthreads();
+      const TileCoord nc = tile_coord(ep, next_bid, nblk, 1);
+#pragma unroll
+      for (int st2 = 0; st2 < 2; ++st2) {
+        if (st2 < nt) {
+          char* base = smem + st2 * SLOT;
+          issue_stage<T, AK, BM, NT>(base, A, lda, nc.tm * BM, st2 * IA::BK, tid);
+          issue_stage<T, BK_, BN, NT>(base + IA::BYTES, B, ldb, nc.tn * BN, st2 * IA::BK, tid);
+        }
+      }
+    }
     // ===================== CFG 7 epilogue (registers -> HBM) ================
     // acc[i][j] of lane (c, g): output row rw + i*16 + c, columns
     // cw + j*16 + 4g .. +3 (W was the MFMA's first operand).  Per element the
@@ -1049,8 +1082,10 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
     }
     if constexpr (EPI == GEMM_EPI_SCORE && WN == 4) {
       // the two waves of a 128-column group: (k0..k7) + (k8..k15)
-      float* srs = (float*)smem;                 // [WN][BM]
-      __syncthreads();                           // ring LDS no longer read
+      // [WN][BM] behind the ring (a persistent block's next stages fill it)
+      static_assert(NS * SLOT + WN * BM * 4 <= LDS_BYTES, "row-sum exchange beside the ring");
+      float* srs = (float*)(smem + NS * SLOT);
+      __syncthreads();                           // every wave's row sums below
       if (g == 0) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) srs[wn * BM + wm * 16 * TM + i * 16 + c] = rsum[i];
@@ -1875,7 +1910,13 @@ __global__ __launch_bounds__(Cfg<CFG>::NT, 1) void mmad_gemm_kernel_p(const T* _
     // stay live across the whole body and the 256-row tiles spill)
     int tid = threadIdx.x;
     asm volatile("" : "+v"(tid));
-    gemm_body<T, TO, AK, BK_, CFG, EPI>(A, lda, B, ldb, K, ep, v, nt, tid);
+    if constexpr (CFG == CFG_XST) {
+      const int nx = v + (int)gridDim.x;
+      gemm_body<T, TO, AK, BK_, CFG, EPI, true>(A, lda, B, ldb, K, ep, v, nt, tid, v != (int)blockIdx.x,
+                                                nx < nt ? nx : -1);
+    } else {
+      gemm_body<T, TO, AK, BK_, CFG, EPI, true>(A, lda, B, ldb, K, ep, v, nt, tid);
+    }
     __syncthreads();
   }
 }
@@ -1950,7 +1991,7 @@ static int plan_group_m(int ntiles, int tiles_m, int BM, int BN) {
 }
 
 // the configurations that have a persistent instantiation (the large-row tiles)
-constexpr bool persist_cfg(int cfg) { return cfg == 1 || cfg == 2 || cfg == CFG_BIG; }
+constexpr bool persist_cfg(int cfg) { return cfg == 1 || cfg == 2 || cfg == CFG_BIG || cfg == CFG_XST; }
 
 template <typename T, typename TO, bool AK, bool BK_, int EPI>
 static const void* persist_kernel(int cfg) {
@@ -1959,6 +2000,9 @@ static const void* persist_kernel(int cfg) {
       case 1: return (const void*)mmad_gemm_kernel_p<T, TO, AK, BK_, 1, EPI>;
       case 2: return (const void*)mmad_gemm_kernel_p<T, TO, AK, BK_, 2, EPI>;
       case CFG_BIG: return (const void*)mmad_gemm_kernel_p<T, TO, AK, BK_, CFG_BIG, EPI>;
+      case CFG_XST:
+        if constexpr (xst_ok<T, EPI>()) return (const void*)mmad_gemm_kernel_p<T, TO, AK, BK_, CFG_XST, EPI>;
+        return nullptr;
       default: return nullptr;
     }
   }
@@ -2022,6 +2066,12 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
         switch (cfg) {
           case 1: args_go(mmad_gemm_kernel_p<T, TO, AK, BK_, 1, EPI>); break;
           case 2: args_go(mmad_gemm_kernel_p<T, TO, AK, BK_, 2, EPI>); break;
+          case CFG_XST:
+            if constexpr (xst_ok<T, EPI>()) {
+              args_go(mmad_gemm_kernel_p<T, TO, AK, BK_, CFG_XST, EPI>);
+              break;
+            }
+            [[fallthrough]];
           default: args_go(mmad_gemm_kernel_p<T, TO, AK, BK_, CFG_BIG, EPI>); break;
         }
         MMAD_LAUNCH_CHECK();

@@ -202,11 +202,12 @@ def test_splitk_timeout_is_reported_not_combined(ws):
     assert err < 1e-2
 
 
-@pytest.mark.parametrize("kind", ["fwd", "score", "mse"])
+@pytest.mark.parametrize("kind", ["fwd", "fwdns", "score", "mse"])
 def test_persistent_grid_bit_identical(kind):
     """Knob 12 (persistent grid: one block per resident slot walks the tiles)
     gives the ordinary grid's bits for the forward-type bf16 epilogues, with
-    every large-row tile (256x128, 128x256, 256x256) forced, at a row count
+    every large-row tile (256x128, 128x256, 256x256; tile 7 also issues the
+    next tile's first K stages from its epilogue) forced, at a row count
     whose tiles exceed one resident round (16,384 rows: 512-1024 tiles on 256
     CUs); outputs, BN-statistic / score-row / loss partials compared."""
     lib = _native.load()
@@ -227,9 +228,9 @@ def test_persistent_grid_bit_identical(kind):
         y = torch.zeros(Mp, Np, device=dev, dtype=torch.bfloat16)
         part = torch.zeros(Mp // 32, 2, Np, device=dev)
         rows = torch.zeros(Np // 128, Mp, device=dev)
-        if kind == "fwd":
+        if kind in ("fwd", "fwdns"):
             call("mmad_fc_fwd", BF16, M, N, K, Mp, Np, Kp, ptr(x), ptr(w), ptr(b), 1, 0.2, None, None,
-                 ptr(y), ptr(part), s)
+                 ptr(y), ptr(part) if kind == "fwd" else None, s)
             return y, part
         if kind == "score":
             call("mmad_fc_fwd_score", BF16, M, N, K, Mp, Np, Kp, ptr(x), ptr(w), ptr(b), 1, 0.2, None,
@@ -239,7 +240,7 @@ def test_persistent_grid_bit_identical(kind):
              ptr(y), ptr(part), s)
         return y, part
     try:
-        for tile in (1, 2, 6):
+        for tile in (1, 2, 6, 7):
             lib.mmad_tune_set(0, tile)
             lib.mmad_tune_set(12, 0)
             a = run()
