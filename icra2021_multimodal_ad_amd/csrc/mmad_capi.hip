@@ -49,7 +49,8 @@ int g_knob[MMAD_KNOB_COUNT] = {
     0,     // 10 dW split rule: target 64x64-tile blocks (0 = no split)
     8,     // 11 dW split rule: minimum K stages per slice
     0,     // 12 persistent grid for forward-type GEMMs (-1 rule, 0 off, 1 on)
-    0, 0, 0,      // 13-15 retired (measured-slower experiments, removed in round 3)
+    1,     // 13 BN-backward apply: 128-row slabs per block (1, 2, 4)
+    0, 0,         // 14-15 retired (measured-slower experiments, removed in round 3)
     -1,    // 16 train-mode BN schedule (-1 = dtype default: bf16 fused, fp32 apply; 0 apply, 1 fold, 2 fused)
     -1,    // 17 backward BN schedule (-1 = the forward's; 2 = fused into the bwd-data GEMMs)
     2048,  // 18 fused BN up to this many padded rows (fold above)
@@ -116,7 +117,7 @@ int mmad_tile_epi_override(int epi) {
 }
 
 static bool knob_valid(int knob) {
-  return knob >= 0 && knob < MMAD_KNOB_COUNT && !(knob >= 13 && knob <= 15);
+  return knob >= 0 && knob < MMAD_KNOB_COUNT && !(knob >= 14 && knob <= 15);
 }
 int mmad_tune_set(int knob, int value) {
   if (!knob_valid(knob)) {

@@ -5,6 +5,7 @@
 // block (grid = Np/64 x Mp/128, thousands of blocks at the bench shapes).
 #include "mmad_common.h"
 #include "mmad_ops.h"
+#include "mmad_gemm.h"
 
 #include <cmath>
 #include <cstdio>
@@ -345,11 +346,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(int M, int Np, const T* _
   }
 }
 
-// dz = act'(a) * gamma*rstd/M * (M*dy - sum(dy) - xhat*sum(dy*xhat)) over one
-// 64-column x 128-row slab; sums from the bwd-data GEMM epilogue partials.
-// Every global load (dy, a, the column constants, the partials) is issued
-// before the first use, so a block costs one memory round trip, not four.
-template <typename T, int PU>
+// dz = act'(a) * gamma*rstd/M * (M*dy - sum(dy) - xhat*sum(dy*xhat)) over RB
+// 64-column x 128-row slabs; sums from the bwd-data GEMM epilogue partials,
+// merged once per block.  The first slab's loads (dy, a, the column
+// constants, the partials) are issued before any use, so the block's first
+// slab costs one memory round trip; each later slab's dy / a are loaded
+// under the previous slab's arithmetic.  Per slab the same arithmetic and
+// the same db-partial order as RB = 1 (bit-identical for every RB).
+template <typename T, int PU, int RB>
 __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int M, int N, int Np,
                                                       int nparts, const T* __restrict__ dy,
                                                       const T* __restrict__ a,
@@ -362,21 +366,25 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
   constexpr int V = Vec<T>::N;
   constexpr int CPR = SLAB_COLS / V;      // threads per row
   constexpr int RG = 256 / CPR;           // row groups
-  constexpr int RPT = SLAB_ROWS / RG;     // rows per thread
+  constexpr int RPT = SLAB_ROWS / RG;     // rows per thread and slab
   // PU: partial chunks per group loaded at once (16 from 2048 rows: one round
   // trip for all of a 4096-row batch's 64 chunks; same summation order)
   __shared__ double s_red[RG][SLAB_COLS];
   __shared__ double s_p1[4][SLAB_COLS], s_p2[4][SLAB_COLS];
-  const int n0 = blockIdx.x * SLAB_COLS, r0 = blockIdx.y * SLAB_ROWS, tid = threadIdx.x;
+  const int n0 = blockIdx.x * SLAB_COLS, tid = threadIdx.x;
   const int ch = tid % CPR, rg = tid / CPR;
-  // (1) this thread's dy / a rows
+  // (1) this thread's dy / a rows of the first slab
   uint4v rd[RPT], ra[RPT];
+  auto load_slab = [&](int slab) {
+    const int r0 = slab * SLAB_ROWS;
 #pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    const size_t off = (size_t)(r0 + rg + i * RG) * Np + n0 + ch * V;
-    rd[i] = *(const uint4v*)(dy + off);
-    ra[i] = *(const uint4v*)(a + off);
-  }
+    for (int i = 0; i < RPT; ++i) {
+      const size_t off = (size_t)(r0 + rg + i * RG) * Np + n0 + ch * V;
+      rd[i] = *(const uint4v*)(dy + off);
+      ra[i] = *(const uint4v*)(a + off);
+    }
+  };
+  load_slab(blockIdx.y * RB);
   // (2) column constants
   float mu[V], rs[V], gm[V];
 #pragma unroll
@@ -420,42 +428,53 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
   // cancels, so it is evaluated in fp64 (as the reference's CPU BatchNorm
   // backward does its reductions); dz and its column sums follow in fp64 too
   const double invM = 1.0 / (double)M;
-  double cf[V], dbv[V], dgv[V], accb[V];
+  double cf[V], dbv[V], dgv[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) {
     const int col = n0 + ch * V + k;
     cf[k] = col < N ? (double)gm[k] * (double)rs[k] * invM : 0.0;
     dbv[k] = s_p1[0][ch * V + k];
     dgv[k] = s_p2[0][ch * V + k];
-    accb[k] = 0.0;
   }
+  for (int sb = 0; sb < RB; ++sb) {
+    const int slab = blockIdx.y * RB + sb;
+    const int r0 = slab * SLAB_ROWS;
+    uint4v ro[RPT];
+    double accb[V];
 #pragma unroll
-  for (int i = 0; i < RPT; ++i) {
-    const int row = r0 + rg + i * RG;
-    const T* pd = (const T*)&rd[i];
-    const T* pa = (const T*)&ra[i];
-    uint4v ro;
-    T* po = (T*)&ro;
+    for (int k = 0; k < V; ++k) accb[k] = 0.0;
 #pragma unroll
-    for (int k = 0; k < V; ++k) {
-      const float av = to_f32<T>(pa[k]);
-      const double xh = ((double)av - (double)mu[k]) * (double)rs[k];
-      const double da = cf[k] * ((double)M * (double)to_f32<T>(pd[k]) - dbv[k] - xh * dgv[k]);
-      float d = (float)(da * (double)act_grad_from_out(av, act, slope));
-      d = row < M ? d : 0.f;
-      const T dt = from_f32<T>(d);
-      po[k] = dt;
-      accb[k] += (double)to_f32<T>(dt);
+    for (int i = 0; i < RPT; ++i) {
+      const int row = r0 + rg + i * RG;
+      const T* pd = (const T*)&rd[i];
+      const T* pa = (const T*)&ra[i];
+      T* po = (T*)&ro[i];
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const float av = to_f32<T>(pa[k]);
+        const double xh = ((double)av - (double)mu[k]) * (double)rs[k];
+        const double da = cf[k] * ((double)M * (double)to_f32<T>(pd[k]) - dbv[k] - xh * dgv[k]);
+        float d = (float)(da * (double)act_grad_from_out(av, act, slope));
+        d = row < M ? d : 0.f;
+        const T dt = from_f32<T>(d);
+        po[k] = dt;
+        accb[k] += (double)to_f32<T>(dt);
+      }
     }
-    *(uint4v*)(dz + (size_t)row * Np + n0 + ch * V) = ro;
-  }
+    // the next slab's rows load under this slab's stores and reduction
+    if (sb + 1 < RB) load_slab(slab + 1);
 #pragma unroll
-  for (int k = 0; k < V; ++k) s_red[rg][ch * V + k] = accb[k];
-  __syncthreads();
-  if (tid < SLAB_COLS) {
-    double t = 0.0;
-    for (int g = 0; g < RG; ++g) t += s_red[g][tid];
-    dbpart[(size_t)blockIdx.y * Np + n0 + tid] = (float)t;
+    for (int i = 0; i < RPT; ++i)
+      *(uint4v*)(dz + (size_t)(r0 + rg + i * RG) * Np + n0 + ch * V) = ro[i];
+#pragma unroll
+    for (int k = 0; k < V; ++k) s_red[rg][ch * V + k] = accb[k];
+    __syncthreads();
+    if (tid < SLAB_COLS) {
+      double t = 0.0;
+      for (int g = 0; g < RG; ++g) t += s_red[g][tid];
+      dbpart[(size_t)slab * Np + n0 + tid] = (float)t;
+    }
+    if (sb + 1 < RB) __syncthreads();   // s_red reused by the next slab
   }
 }
 
@@ -963,23 +982,37 @@ int mmad_bn_act_bwd_apply(int dtype, int act, float slope, int M, int N, int Mp,
                           const float* save_rstd, const float* gamma, const double* part,
                           int nparts, void* dz, float* dgamma, float* dbeta, float* db_partials,
                           void* stream) {
-  dim3 grd(Np / SLAB_COLS, Mp / SLAB_ROWS);
+  // 128-row slabs per block (knob 13: 1, 2 or 4; 0 = rule): the column
+  // partials are merged once per block instead of once per 128-row slab
+  int rb = mmad_knob(13);
+  if (rb != 1 && rb != 2 && rb != 4) rb = 1;
+  while (rb > 1 && (Mp / SLAB_ROWS) % rb) rb >>= 1;
+  dim3 grd(Np / SLAB_COLS, Mp / (SLAB_ROWS * rb));
   hipStream_t s = (hipStream_t)stream;
   const bool wide = nparts > 4 * 8;   // 16 partial chunks per round trip (8 no faster, r02bj_*)
-#define MMAD_BNB(PU_)                                                                              \
-  if (dtype == MMAD_BF16)                                                                          \
-    bn_bwd_apply_k<bf16, PU_><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const bf16*)dy,   \
-                                                  (const bf16*)a, save_mean, save_rstd, gamma, part, \
-                                                  (bf16*)dz, dgamma, dbeta, db_partials);          \
-  else                                                                                             \
-    bn_bwd_apply_k<float, PU_><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const float*)dy, \
-                                                   (const float*)a, save_mean, save_rstd, gamma,   \
-                                                   part, (float*)dz, dgamma, dbeta, db_partials);
-  if (wide) {
-    MMAD_BNB(16)
-  } else {
-    MMAD_BNB(8)
+#define MMAD_BNB(PU_, RB_)                                                                             \
+  if (dtype == MMAD_BF16)                                                                              \
+    bn_bwd_apply_k<bf16, PU_, RB_><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const bf16*)dy,  \
+                                                       (const bf16*)a, save_mean, save_rstd, gamma,    \
+                                                       part, (bf16*)dz, dgamma, dbeta, db_partials);   \
+  else                                                                                                 \
+    bn_bwd_apply_k<float, PU_, RB_><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const float*)dy, \
+                                                        (const float*)a, save_mean, save_rstd, gamma,  \
+                                                        part, (float*)dz, dgamma, dbeta, db_partials);
+#define MMAD_BNB_RB(PU_)      \
+  if (rb == 4) {              \
+    MMAD_BNB(PU_, 4)          \
+  } else if (rb == 2) {       \
+    MMAD_BNB(PU_, 2)          \
+  } else {                    \
+    MMAD_BNB(PU_, 1)          \
   }
+  if (wide) {
+    MMAD_BNB_RB(16)
+  } else {
+    MMAD_BNB_RB(8)
+  }
+#undef MMAD_BNB_RB
 #undef MMAD_BNB
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
@@ -1000,13 +1033,13 @@ int mmad_bn_act_bwd(int dtype, int act, float slope, int M, int N, int Mp, int N
   if (dtype == MMAD_BF16) {
     bn_bwd_reduce_k<bf16><<<grd, 256, 0, s>>>(M, Np, (const bf16*)dy, (const bf16*)a, save_mean,
                                               save_rstd, part);
-    bn_bwd_apply_k<bf16, 8><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const bf16*)dy,
+    bn_bwd_apply_k<bf16, 8, 1><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const bf16*)dy,
                                              (const bf16*)a, save_mean, save_rstd, gamma, part,
                                              (bf16*)dz, dgamma, dbeta, db_partials);
   } else {
     bn_bwd_reduce_k<float><<<grd, 256, 0, s>>>(M, Np, (const float*)dy, (const float*)a, save_mean,
                                                save_rstd, part);
-    bn_bwd_apply_k<float, 8><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const float*)dy,
+    bn_bwd_apply_k<float, 8, 1><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const float*)dy,
                                               (const float*)a, save_mean, save_rstd, gamma, part,
                                               (float*)dz, dgamma, dbeta, db_partials);
   }

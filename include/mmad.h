@@ -66,7 +66,9 @@ int mmad_pad_granule(void);
  *      6 / 7 = tile of the bwd-data / forward GEMMs (-1 autotuned)
  *   12 persistent grid for the forward-type GEMMs without a fused BN or a
  *      split (-1 rule: when the tiles exceed one resident round; 0 off; 1 on)
- *   13-15 retired (EINVAL)
+ *   13 BN-backward apply kernel: 128-row slabs per block (1, 2 or 4; the
+ *      column partials are merged once per block)
+ *   14-15 retired (EINVAL)
  *   16 train-mode BN schedule (-1 dtype default: bf16 fused, fp32 apply;
  *      0 apply kernels, 1 fold into the consumer, 2 fused into the GEMMs)
  *   17 backward BN schedule (-1 = the forward's, 2 = fused into bwd-data)

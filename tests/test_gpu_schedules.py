@@ -75,3 +75,35 @@ def test_adam_fused_dw_tiles_match_default(tile):
     for name in ("params", "exp_avg", "exp_avg_sq", "running"):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
     assert torch.equal(a.shadow, b.shadow)
+
+
+@pytest.mark.parametrize("dtype,rows", [("bf16", 4096), ("f32", 1024)])
+@pytest.mark.parametrize("rb", [2, 4])
+def test_bn_apply_slabs_match_default(dtype, rows, rb):
+    """The BN-backward apply kernel with 2 / 4 row slabs per block (knob 13,
+    read at every launch: the column partials are merged once per block)
+    gives the one-slab kernel's bits: parameters, Adam moments, BN statistics
+    and losses.  bf16 at 4096 rows (fold forward, apply backward) and fp32 at
+    1024 rows (apply both ways)."""
+    import types
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    ms = []
+    for _ in range(2):
+        cfg = types.SimpleNamespace(input_size=2048, btl_size=100, n_layers=5, gpu_id=0, dtype=dtype,
+                                    models="ae")
+        torch.manual_seed(8)
+        ms.append(get_model(cfg))
+    ms[1].load_state_dict(ms[0].state_dict())
+    for m in ms:
+        m._native.sync_shadow(force=True)
+    for s in range(2):
+        x = torch.from_numpy(synth_windows(rows, 2048, seed=60 + s)).cuda()
+        la = float(ms[0]._native.train_step_fused(x))
+        with _native.tune(bn_apply_rb=rb):
+            lb = float(ms[1]._native.train_step_fused(x))
+            torch.cuda.synchronize()
+        assert la == lb, (s, la, lb)
+    torch.cuda.synchronize()
+    a, b = ms[0]._native, ms[1]._native
+    for name in ("params", "exp_avg", "exp_avg_sq", "running"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
