@@ -225,15 +225,21 @@ def gemm_roofline(model, batch, iters=50):
     def launch():
         call("mmad_fc_fwd", dt, batch, L["N"], L["K"], Mp, L["Np"], L["Kp"], ptr(xin), ptr(w), ptr(b),
              1, 0.2, None, None, ptr(out), ptr(stats), s)
+    import statistics
     for _ in range(5):
         launch()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(iters):
-        launch()
-    e1.record()
+    # 5 groups of iters/5 back-to-back launches, each between its own event
+    # pair; the median group (one slow group -- a clock dip -- does not move it)
+    groups, per = 5, max(iters // 5, 1)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(groups)]
+    for e0, e1 in ev:
+        e0.record()
+        for _ in range(per):
+            launch()
+        e1.record()
     torch.cuda.synchronize()
-    avg_s = e0.elapsed_time(e1) / 1e3 / iters
+    avg_s = statistics.median(e0.elapsed_time(e1) for e0, e1 in ev) / 1e3 / per
+    iters = groups * per
     flops = 2.0 * batch * L["K"] * L["N"]
     peak = BF16_PEAK_TFLOPS if dt == _native.BF16 else F32_PEAK_TFLOPS
     ach = flops / avg_s / 1e12
@@ -244,7 +250,8 @@ def gemm_roofline(model, batch, iters=50):
            "bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
            "frac": round(ach / peak, 4), **tf,
            "avg_us": round(avg_s * 1e6, 2), "flops_per_launch": flops,
-           "timing": f"{iters} back-to-back launches between one HIP event pair"}
+           "timing": f"{iters} launches: the median of 5 groups of back-to-back launches, each "
+                     f"group between one HIP event pair"}
     if pmc is not None and pmc.get("SQ_VALU_MFMA_BUSY_CYCLES"):
         # rocprofv3 counters of the same kernel and shape (tools/pmc_gemm.py)
         res["mfma_counters"] = {k: pmc.get(k) for k in (
@@ -308,6 +315,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-probe", action="store_true", help="skip the in-situ kernel probe")
+    ap.add_argument("--soak-s", type=float, default=2.0,
+                    help="untimed steps for about this many seconds after the warmup (0 = none)")
     ap.add_argument("--no-c2", action="store_true",
                     help="auto at N=1: skip the c2 sub-object (BASELINE configs[1]) in the same line")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
@@ -360,7 +369,7 @@ def run(args):
         del model
         torch.cuda.synchronize()
         sub, _ = train_workload(args, "c2", dict(CONFIGS["c2"]), rank, world, local, with_cpu=False)
-        keep = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "model_tflops",
+        keep = ("value", "unit", "ms_per_step", "steps", "warmup", "soak_steps", "config", "model_tflops",
                 "host_enqueue_ms_per_step", "final_loss", "step_spread", "train_step", "roofline",
                 "roofline_encoder_gemm")
         res["c2"] = {k: sub[k] for k in keep if k in sub}
@@ -405,6 +414,23 @@ def train_workload(args, cname, cfgd, rank, world, local, with_cpu):
     pool = [synth_windows_device(batch, dim, dev, seed=1000 * rank + i) for i in range(8)]
 
     for i in range(args.warmup):
+        model.train_step_async(pool[i % len(pool)], opt)
+    torch.cuda.synchronize()
+    tw = time.perf_counter()                     # step time for the soak's length
+    for i in range(10):
+        model.train_step_async(pool[i % len(pool)], opt)
+    torch.cuda.synchronize()
+    # untimed soak: about args.soak_s seconds of the same steps before the
+    # timed region, so it runs at the clock the chip holds under sustained
+    # load (MI355X_MICROARCH.md 'DVFS give-back') and a sampling observer sees
+    # the GPU busy; the same step count on every rank (DP steps exchange)
+    per = (time.perf_counter() - tw) / 10
+    soak = int(min(args.soak_s / max(per, 1e-5), 20000)) if args.soak_s > 0 else 0
+    if world > 1:
+        t = torch.tensor([soak], device=dev, dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        soak = int(t.item())
+    for i in range(soak):
         model.train_step_async(pool[i % len(pool)], opt)
     torch.cuda.synchronize()
     probe_layer = pick_dominant_layer(nat, batch)
@@ -454,6 +480,7 @@ def train_workload(args, cname, cfgd, rank, world, local, with_cpu):
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "soak_steps": soak,
         "ms_per_step": round(el / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
