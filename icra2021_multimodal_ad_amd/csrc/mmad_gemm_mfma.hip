@@ -89,12 +89,19 @@ template <> struct Cfg<7> { static constexpr int BM = 256, BN = 256, WM = 2, WN 
 // file; the host side reaches it through mmad_gemm_b4_launch.
 constexpr int CFG_B4 = 8;
 template <> struct Cfg<8> { static constexpr int BM = 256, BN = 256, WM = 2, WN = 2, NS = 2, NT = 256; };
-constexpr int NCFG = 9;
-constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256, 256, 256};
-constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256, 256, 256};
-constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512, 512, 256};
+// 9: CFG 1 (256x128, 8 waves of 64x64) with CFG 7's swapped operands and
+// register-direct epilogue: the large-row forward / score GEMMs whose output
+// width is not a multiple of 256 (C5: every layer but the 2048-wide ones)
+constexpr int CFG_XST1 = 9;
+template <> struct Cfg<9> { static constexpr int BM = 256, BN = 128, WM = 4, WN = 2, NS = 3, NT = 512; };
+constexpr int NCFG = 10;
+constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256, 256, 256, 256};
+constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256, 256, 256, 128};
+constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512, 512, 256, 512};
 inline bool is_big(int cfg) { return cfg == CFG_BIG || cfg == CFG_XST || cfg == CFG_B4; }
-inline bool is_xst(int cfg) { return cfg == CFG_XST || cfg == CFG_B4; }
+inline bool is_xst(int cfg) { return cfg == CFG_XST || cfg == CFG_B4 || cfg == CFG_XST1; }
+// the row-quad tile a register-direct one falls back to (same tile shape)
+inline int xst_base(int cfg) { return cfg == CFG_XST1 ? 1 : CFG_BIG; }
 // the 256x256 tiles: bf16 operands, forward-type epilogues, no fused BN
 template <typename T, int EPI>
 constexpr bool big_ok() {
@@ -291,7 +298,8 @@ __device__ __forceinline__ void read_sub(const char* sa, const char* sb, int ra,
 struct NoHook {
   __device__ __forceinline__ void operator()(int) const {}
 };
-template <typename T, int TM, int TN, int H, typename Hook = NoHook>
+// (SW: the operands swapped -- W first -- for the register-direct epilogue)
+template <typename T, int TM, int TN, int H, bool SW = false, typename Hook = NoHook>
 __device__ __forceinline__ void mma_half(floatx4 (&acc)[TM][TN], const typename SubFrag<T>::F (&fa)[TM],
                                          const typename SubFrag<T>::F (&fb)[TN], Hook row_hook = Hook{}) {
 #pragma unroll
@@ -300,7 +308,8 @@ __device__ __forceinline__ void mma_half(floatx4 (&acc)[TM][TN], const typename 
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       if constexpr (sizeof(T) == 2) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = SW ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0)
+                       : __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
       } else {
 #pragma unroll
         for (int s = 0; s < 4; ++s)
@@ -472,9 +481,9 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   constexpr int NL = IA::CHUNKS + IB::CHUNKS;          // vm ops per thread per stage
   constexpr bool FWDLIKE = EPI == GEMM_EPI_FWD || EPI == GEMM_EPI_MSE || EPI == GEMM_EPI_SCORE;
   constexpr bool BIG = CFG == CFG_BIG || CFG == CFG_XST || CFG == CFG_B4;
-  constexpr bool XST = CFG == CFG_XST || CFG == CFG_B4;
+  constexpr bool XST = CFG == CFG_XST || CFG == CFG_B4 || CFG == CFG_XST1;
   static_assert(!BIG || big_ok<T, EPI>(), "256x256 tile: bf16 forward-type epilogues only");
-  static_assert(!XST || xst_ok<T, EPI>(), "CFG 7 / 8: bf16 eval forward / score only");
+  static_assert(!XST || xst_ok<T, EPI>(), "CFG 7 / 8 / 9: bf16 eval forward / score only");
   // prefetched bias partials per lane (none for the 256x256 tile: its
   // 128 accumulator registers leave no room to hold them across the loop)
   constexpr int QB = BIG ? 0 : 8;
@@ -543,7 +552,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       }
     }
   };
-  if constexpr (FWDLIKE && !BIG) load_epi_consts();
+  if constexpr (FWDLIKE && !BIG && !XST) load_epi_consts();
 
   // fused BN: this column's barrier generation, read before this block can
   // arrive (its latency hides under the main loop)
@@ -769,11 +778,11 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       constexpr bool ISSUE = decltype(issue_c)::value, LAST = decltype(last_c)::value;
       constexpr bool PF = decltype(pf_c)::value;   // the Adam prefetch is in flight
       const char* sa = smem + (t % NS) * SLOT;
-      mma_half<T, TM, TN, 0>(acc, f0a, f0b);
+      mma_half<T, TM, TN, 0, XST>(acc, f0a, f0b);
       MMAD_SB();
       read_sub<T, AK, BK_, NAT, BM, BN, TM, TN>(sa, sa + IA::BYTES, ra, rb, 1, lane, f1a, f1b);
       MMAD_SB();
-      mma_half<T, TM, TN, 1>(acc, f0a, f0b);
+      mma_half<T, TM, TN, 1, XST>(acc, f0a, f0b);
       MMAD_SB();
       if constexpr (!LAST) {
         if constexpr (ISSUE) {
@@ -797,14 +806,14 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
             if (q * TM / NL == i) issue_q(t + NS, q);
         }
       };
-      mma_half<T, TM, TN, 0>(acc, f1a, f1b, dma_row);
+      mma_half<T, TM, TN, 0, XST>(acc, f1a, f1b, dma_row);
       MMAD_SB();
       if constexpr (!LAST) {
         const char* sn = smem + ((t + 1) % NS) * SLOT;
         read_sub<T, AK, BK_, NAT, BM, BN, TM, TN>(sn, sn + IA::BYTES, ra, rb, 0, lane, f0a, f0b);
       }
       MMAD_SB();
-      mma_half<T, TM, TN, 1>(acc, f1a, f1b, dma_row);
+      mma_half<T, TM, TN, 1, XST>(acc, f1a, f1b, dma_row);
       MMAD_SB();
     };
     using T_ = std::true_type;
@@ -994,6 +1003,28 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
     };
     TO* out = (TO*)ep.out;
     const int jl = g & 1, coff = 8 * (g >> 1);
+    // score: every reference chunk of the tile loaded in one round trip when
+    // they fit (TM x TN/2 <= 8 chunks: the 256x128 tile), per column pair
+    // otherwise
+    constexpr bool REF_ALL = EPI == GEMM_EPI_SCORE && TM * (TN / 2) <= 8;
+    uint4v rall[REF_ALL ? TN / 2 : 1][REF_ALL ? TM : 1];
+    if constexpr (REF_ALL) {
+      // (one branch around the whole group: a per-chunk "ref ? load : 0"
+      // becomes a branch and a wait per load)
+      if (ep.ref) {
+#pragma unroll
+        for (int h = 0; h < TN / 2; ++h)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            rall[h][i] = *(const uint4v*)((const TO*)ep.ref + (size_t)(rw + i * 16 + c) * ep.ldref + cw +
+                                          (2 * h + jl) * 16 + coff);
+      } else {
+#pragma unroll
+        for (int h = 0; h < TN / 2; ++h)
+#pragma unroll
+          for (int i = 0; i < TM; ++i) rall[h][i] = uint4v{0u, 0u, 0u, 0u};
+      }
+    }
     float rsum[EPI == GEMM_EPI_SCORE ? TM : 1];   // this wave's 64-column row sums (WN = 4)
     float rsum2[EPI == GEMM_EPI_SCORE ? TM : 1][2];   // (WN = 2) the two 64-column halves
 #pragma unroll
@@ -1009,7 +1040,10 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
       const int col0 = cw + (2 * h + jl) * 16 + coff;   // this lane's chunk after the swap
       uint4v rvs[EPI == GEMM_EPI_SCORE ? TM : 1];
       if constexpr (EPI == GEMM_EPI_SCORE) {
-        if (ep.ref) {
+        if constexpr (REF_ALL) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) rvs[i] = rall[h][i];
+        } else if (ep.ref) {
 #pragma unroll
           for (int i = 0; i < TM; ++i)
             rvs[i] = *(const uint4v*)((const TO*)ep.ref + (size_t)(rw + i * 16 + c) * ep.ldref + col0);
@@ -1067,7 +1101,7 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
           // 1, 3: (k0 + k1) + (k2 + k3), the row-major butterfly's order
           sq += lane_xor32(sq);
           sq += lane_xor16(sq);
-          if constexpr (WN == 4) {
+          if constexpr (TN == 4) {
             rsum[i] = h == 0 ? sq : rsum[i] + sq;
           } else {
             // 128 columns per wave: ((Q0 + Q1) + (Q2 + Q3)), written here
@@ -1080,21 +1114,25 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
         }
       }
     }
-    if constexpr (EPI == GEMM_EPI_SCORE && WN == 4) {
-      // the two waves of a 128-column group: (k0..k7) + (k8..k15)
-      // [WN][BM] behind the ring (a persistent block's next stages fill it)
-      static_assert(NS * SLOT + WN * BM * 4 <= LDS_BYTES, "row-sum exchange beside the ring");
-      float* srs = (float*)(smem + NS * SLOT);
-      __syncthreads();                           // every wave's row sums below
+    if constexpr (EPI == GEMM_EPI_SCORE && TN == 4) {
+      // the two waves of a 128-column group: (k0..k7) + (k8..k15), through
+      // [WN][BM] floats of LDS (a persistent block's: behind the ring, which
+      // its next tile's stages fill; otherwise at its start)
+      static_assert(!PST || NS * SLOT + WN * BM * 4 <= LDS_BYTES, "row-sum exchange beside the ring");
+      float* srs = (float*)(smem + (PST ? NS * SLOT : 0));
+      __syncthreads();                           // ring reads / every wave's row sums below
       if (g == 0) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) srs[wn * BM + wm * 16 * TM + i * 16 + c] = rsum[i];
       }
       __syncthreads();
-      static_assert(NT == 2 * BM && WN == 4, "one row-sum per thread");
-      const int gi = tid / BM, rl = tid % BM;
-      const float tot = srs[(2 * gi) * BM + rl] + srs[(2 * gi + 1) * BM + rl];
-      ep.rowsq[(size_t)((n0 >> 7) + gi) * ep.ldrow + m0 + rl] = tot;
+      constexpr int GROUPS = BN / 128;
+      static_assert(WN == 2 * GROUPS && NT >= GROUPS * BM, "two waves per 128-column group");
+      if (tid < GROUPS * BM) {
+        const int gi = tid / BM, rl = tid % BM;
+        const float tot = srs[(2 * gi) * BM + rl] + srs[(2 * gi + 1) * BM + rl];
+        ep.rowsq[(size_t)((n0 >> 7) + gi) * ep.ldrow + m0 + rl] = tot;
+      }
     }
     return;
   }
@@ -1952,6 +1990,7 @@ int mmad_gemm_b4_launch(int epi, const void* A, int lda, const void* B, int ldb,
 static bool cfg_fits(int cfg, int Mp, int Np, int epi, int dtype) {
   if (Mp % CFG_BM[cfg] || Np % CFG_BN[cfg]) return false;
   if (is_big(cfg) && !big_ok_rt(dtype, epi)) return false;
+  if (is_xst(cfg) && !(dtype == MMAD_BF16 && (epi == GEMM_EPI_FWD || epi == GEMM_EPI_SCORE))) return false;
   // the score epilogue reduces rows over 128-column groups inside one tile
   if (epi == GEMM_EPI_SCORE && CFG_BN[cfg] < 128) return false;
   return true;
@@ -2040,7 +2079,7 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
                         const GemmEpi& ep_in, int cfg, hipStream_t s) {
   // CFG 7 / 8 outside their epilogues (column partials, MSE, sigmoid / tanh):
   // CFG 6, the same 256x256 tile
-  if (is_xst(cfg) && !xst_ok_rt(sizeof(T) == 2 ? MMAD_BF16 : MMAD_F32, EPI, ep_in)) cfg = CFG_BIG;
+  if (is_xst(cfg) && !xst_ok_rt(sizeof(T) == 2 ? MMAD_BF16 : MMAD_F32, EPI, ep_in)) cfg = xst_base(cfg);
   const int BM = CFG_BM[cfg], BN = CFG_BN[cfg];
   const int tiles_m = Mp / BM, tiles_n = Np / BN, ntiles = tiles_m * tiles_n;
   GemmEpi ep = ep_in;
@@ -2099,6 +2138,10 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
     case 3: go(mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI>); break;
     case 4: go(mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI>); break;
     case 5: go(mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI>); break;
+    case CFG_XST1:
+      if constexpr (xst_ok<T, EPI>()) go(mmad_gemm_kernel<T, TO, AK, BK_, CFG_XST1, EPI>);
+      else go(mmad_gemm_kernel<T, TO, AK, BK_, 1, EPI>);
+      break;
     default:
       if constexpr (big_ok<T, EPI>()) {
         if constexpr (xst_ok<T, EPI>()) {
@@ -2128,6 +2171,9 @@ static const void* kernel_ptr(int cfg) {
     case 3: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 3, EPI>;
     case 4: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 4, EPI>;
     case 5: return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 5, EPI>;
+    case CFG_XST1:
+      if constexpr (xst_ok<T, EPI>()) return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, CFG_XST1, EPI>;
+      return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, 1, EPI>;
     default:
       if constexpr (xst_ok<T, EPI>())
         if (cfg == CFG_XST) return (const void*)mmad_gemm_kernel<T, TO, AK, BK_, CFG_XST, EPI>;
@@ -2188,7 +2234,8 @@ bool mmad_gemm_bn_fusable(int dtype, int epi, int Mp, int Np) {
   if (epi != GEMM_EPI_FWD && epi != GEMM_EPI_BWD_DATA) return false;
   if (Mp % 128 || Np % 128 || Np / 64 > MMAD_BN_EXIT) return false;
   for (int c = 0; c < NCFG; ++c)
-    if (cfg_fits(c, Mp, Np, epi, dtype) && !is_big(c) && coresident(dtype, epi, c, Mp, Np)) return true;
+    if (cfg_fits(c, Mp, Np, epi, dtype) && !is_big(c) && !is_xst(c) && coresident(dtype, epi, c, Mp, Np))
+      return true;
   return false;
 }
 
@@ -2247,7 +2294,7 @@ static int tune_cfg(int dtype, int epi, const void* A, int lda, const void* B, i
   int rc = MMAD_OK;
   for (int c = 0; c < NCFG && rc == MMAD_OK; ++c) {
     if (!cfg_fits(c, Mp, Np, epi, dtype)) continue;
-    if (is_big(c) && (ep.bn_sync || ep.splitk > 1)) continue;   // no fused BN / split on 256x256
+    if ((is_big(c) || is_xst(c)) && (ep.bn_sync || ep.splitk > 1)) continue;   // no fused BN / split
     if (c == CFG_B4) continue;   // the 4-wave tile: forced only (measured slower)
     if (ep.bn_sync && !coresident(dtype, epi, c, Mp, Np)) continue;
     rc = launch_cfg(dtype, epi, A, lda, B, ldb, Mp, Np, K, et, c, s);   // warm
@@ -2370,8 +2417,8 @@ int mmad_gemm_dispatch(int dtype, int epi, const void* A, int lda, const void* B
   ep.splitk = (ep.sk_slab && ep.sk_ctl && !bnf) ? mmad_gemm_splitk(Mp, Np, K, dtype, epi) : 1;
   auto allowed = [&](int c) {
     return c >= 0 && c < NCFG && cfg_fits(c, Mp, Np, epi, dtype) &&
-           (!is_big(c) || ep.splitk <= 1) &&
-           (!bnf || (!is_big(c) && coresident(dtype, epi, c, Mp, Np)));
+           ((!is_big(c) && !is_xst(c)) || ep.splitk <= 1) &&
+           (!bnf || (!is_big(c) && !is_xst(c) && coresident(dtype, epi, c, Mp, Np)));
   };
   const int env = mmad_tile_override();
   const int env_epi = ep.ad_p ? mmad_tile_adam_for(Mp, Np, K) : mmad_tile_epi_override(epi);

@@ -253,20 +253,23 @@ def test_persistent_grid_bit_identical(kind):
         lib.mmad_tune_set(12, 0)
 
 
+@pytest.mark.parametrize("N", [2000, 1658])
 @pytest.mark.parametrize("case", ["fwd_leaky_bn", "fwd_relu", "fwd_none", "score_ref_diff", "score_nodiff",
                                   "nap_colw", "fwd_stats_fallback", "fwd_sigmoid_fallback"])
-def test_register_direct_tile_bit_identical(case):
-    """Tiles 7 and 8 (256x256 with the MFMA operands swapped, the epilogue
-    stored from registers through v_permlane16_swap; 8 waves / 4 waves with
-    AGPR accumulators) against the row-quad tiles 6 / 1 / 2:
-    bit-identical outputs, score row sums and diffs, on a shape with masked
-    rows and columns (M = 4000 of 4096, N = 2000 of 2048).  The forward with
+def test_register_direct_tile_bit_identical(case, N):
+    """Tiles 7, 8 and 9 (256x256 / 256x256 4-wave / 256x128 with the MFMA
+    operands swapped, the epilogue stored from registers through
+    v_permlane16_swap) against the row-quad tiles 6 / 1 / 2: bit-identical
+    outputs, score row sums and diffs, on shapes with masked rows and columns
+    (M = 4000 of 4096; N = 2000 of 2048, or 1658 of 1664, where only the
+    256x128 / 128x... tiles fit and a forced 256x256 falls back to the tuned
+    one).  The forward with
     BN-statistic partials and the sigmoid forward run CFG 6 in its place
     (same tile, same bits)."""
     lib = _native.load()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cuda").manual_seed(11)
-    M, N, K = 4000, 2000, 1658
+    M, K = 4000, 1658
     Mp, Np, Kp = pad(M), pad(N), pad(K)
     x = torch.zeros(Mp, Kp, device=dev, dtype=torch.bfloat16)
     x[:M, :K] = torch.randn(M, K, device=dev, generator=g).bfloat16()
@@ -304,13 +307,13 @@ def test_register_direct_tile_bit_identical(case):
         return y, rows, diff
     outs = {}
     try:
-        for tile in (6, 7, 8, 1, 2):
+        for tile in (6, 7, 8, 1, 2, 9):
             lib.mmad_tune_set(0, tile)
             outs[tile] = run()
         torch.cuda.synchronize()
     finally:
         lib.mmad_tune_set(0, -1)
     assert float(outs[6][0].float().abs().sum()) > 0
-    for tile in (7, 8, 1, 2):
+    for tile in (7, 8, 1, 2, 9):
         for a, b2 in zip(outs[6], outs[tile]):
             assert torch.equal(a, b2), (case, tile)

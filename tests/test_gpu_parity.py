@@ -329,7 +329,7 @@ def test_tile_configs_bit_identical(dtype):
     x = torch.from_numpy(synth_windows(512, 500, seed=18)).cuda()
     ref = None
     try:
-        for cfg in (-1, 0, 1, 2, 3, 4, 5, 6, 7, 8):
+        for cfg in (-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9):
             lib.mmad_tune_set(0, cfg)
             m, _ = _model(500, 40, 3, sd, dtype=dtype)
             loss = float(m._native.train_step(x))
