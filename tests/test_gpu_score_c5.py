@@ -3,7 +3,7 @@ batches (the scoring batch bench.py --config c5 and bench_score.py use), bf16.
 
 Checked through the C-ABI: a pass over 2 x 65,536 + 1,000 windows (ragged
 last batch) is finite; the captured hipGraph replay equals the eager pass bit
-for bit; nothing is written past N; and 256 windows (the first and the last
+for bit, and so does every batch scored alone; nothing is written past N; and 256 windows (the first and the last
 128) are within the bf16 band of the CPU oracle's get_diffs
 (reconstruction_aggregation.py:6-37) on the same weights and BN statistics,
 per layer: relative Frobenius error of the per-window squared-diff sums
@@ -50,6 +50,12 @@ def test_score_stream_c5_size_graph_eager_and_oracle():
     assert nat._lib.mmad_ae_graph_count(nat._h) >= 1
     assert torch.equal(first, eager) and torch.equal(replay, eager)
     assert torch.isnan(out[:, n:]).all()
+    # every batch scored alone (its own pass) gives the same bits: no state
+    # carries from one batch of a pass to the next
+    for s in range(0, n, BATCH):
+        k = min(BATCH, n - s)
+        alone = score_windows(x[s:s + k], model, batch_size=BATCH, graph=False)
+        assert torch.equal(alone, eager[:, s:s + k]), s
     # 256 windows against the oracle on the same weights / BN statistics
     om = model_from_state_dict({k: v.cpu().numpy() for k, v in model.state_dict().items()})
     rows = np.r_[0:128, n - 128:n]
