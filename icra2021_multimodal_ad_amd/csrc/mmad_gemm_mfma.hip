@@ -620,8 +620,14 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
   auto issue_q = [&](int s, int q) {
     char* base = smem + (s % NS) * SLOT;
     const int k0 = kbase + s * IA::BK;
-    if (q < IA::CHUNKS) issue_chunk<T, AK, BM, NT>(base, A, lda, m0, k0, tid, q);
-    else issue_chunk<T, BK_, BN, NT>(base + IA::BYTES, B, ldb, n0, k0, tid, q - IA::CHUNKS);
+    // persistent body: the chunk's source address is recomputed at every
+    // issue (an opaque thread index): hoisted out of the K loop, the 64-bit
+    // addresses of every chunk stay live across it and spill, and each
+    // scratch reload's vmcnt wait drains the DMA ring
+    int t = tid;
+    if constexpr (PST) asm volatile("" : "+v"(t));
+    if (q < IA::CHUNKS) issue_chunk<T, AK, BM, NT>(base, A, lda, m0, k0, t, q);
+    else issue_chunk<T, BK_, BN, NT>(base + IA::BYTES, B, ldb, n0, k0, t, q - IA::CHUNKS);
   };
 
   // ---- main loop: NS-slot LDS ring, all slots in flight; fragment registers
