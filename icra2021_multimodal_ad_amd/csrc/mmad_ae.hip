@@ -83,6 +83,10 @@ struct mmad_ae {
   // order) share one exchange bucket until it holds at least dp_bucket_mib
   // MiB of fp32 gradient (knob 30; 0 = one bucket per layer)
   int dp_bucket_mib = 8;
+  // data-parallel step: from this many padded rows each side-stream dW GEMM
+  // is issued as soon as its own dz is complete instead of with its bucket's
+  // closing layer (knob 14; 0 = one fork per bucket)
+  int dp_fork_rows = 1024;
   bool master_stale = false;
   int mse_tiles = 0;   // loss partials written by the last MSE GEMM
   // data parallelism: RCCL communicator (not owned), its stream and events
@@ -381,6 +385,7 @@ int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, i
     h->dp_shard = mmad_knob(28);
     h->side_hold = mmad_knob(29);
     h->dp_bucket_mib = mmad_knob(30) < 0 ? 0 : mmad_knob(30);
+    h->dp_fork_rows = mmad_knob(14);
     h->ev_flags_ = ev_flags(mmad_knob(27));
   }
   for (int side = 0; side < 2; ++side) {
@@ -836,7 +841,8 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     const bool dp = adam && h->comm;
     // the exchange bucket this layer closes (data parallel), if any
     const DpBucket* bk = nullptr;
-    if (dp && next_bucket < (int)plan.size() && plan[next_bucket].l_lo == l) bk = &plan[next_bucket++];
+    const DpBucket* cur = dp && next_bucket < (int)plan.size() ? &plan[next_bucket] : nullptr;
+    if (cur && cur->l_lo == l) bk = &plan[next_bucket++];
     // ping-pong shadows (bf16): the fused Adam of dW_l writes the other
     // shadow, so dW_l may start as soon as dz_l is complete
     const bool ping = adam && !dp && w.ping && l >= w.dw_main;
@@ -851,11 +857,25 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
                                         (l - w.dw_main) % h->ev_every == 0));
     bool ev_attached = false;   // ev_data[l] completed by the bwd-data launch (ev_on_kernel)
     if (dp) {
-      // data parallel: the dW GEMMs of a bucket's layers are issued together
-      // once the layer that closes it has its dz (one fork per bucket: the
-      // step is host-bound, every event call counts), then the bucket's event
-      pending.push_back(PendingDW{dz, in, a.Np, a.Kp, a.Np, a.Kp, Mp, dwe, l});
-      if (bk) {
+      // data parallel: below dp_fork_rows rows (host-bound steps, every event
+      // call counts) the dW GEMMs of a bucket's layers are issued together
+      // once the layer that closes it has its dz (one fork per bucket), then
+      // the bucket's event
+      // from dp_fork_rows rows the step is GPU-bound: a side-stream bucket's
+      // dW GEMMs then start at their own dz (one fork each) instead of
+      // queueing until the bucket's lowest layer
+      const bool each = h->dp_fork_rows > 0 && Mp >= h->dp_fork_rows && cur &&
+                        !(cur->l_hi < w.dw_main);
+      if (each) {
+        MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
+        MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
+        RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
+                       nullptr, PROBE_DW + l));
+        if (bk) MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l], side));
+      } else {
+        pending.push_back(PendingDW{dz, in, a.Np, a.Kp, a.Np, a.Kp, Mp, dwe, l});
+      }
+      if (bk && !each) {
         // a bucket made only of the last dw_main layers of the chain runs its
         // dW GEMMs on the main stream, idle by then, instead of behind the
         // side stream's backlog (the exchange tail waits for them)

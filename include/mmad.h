@@ -68,7 +68,10 @@ int mmad_pad_granule(void);
  *      split (-1 rule: when the tiles exceed one resident round; 0 off; 1 on)
  *   13 BN-backward apply kernel: 128-row slabs per block (1, 2 or 4; the
  *      column partials are merged once per block)
- *   14-15 retired (EINVAL)
+ *   14 data parallel: from this many padded rows, each side-stream dW GEMM
+ *      starts at its own dz instead of with its bucket's lowest layer (1024;
+ *      0 = one fork per bucket)
+ *   15 retired (EINVAL)
  *   16 train-mode BN schedule (-1 dtype default: bf16 fused, fp32 apply;
  *      0 apply kernels, 1 fold into the consumer, 2 fused into the GEMMs)
  *   17 backward BN schedule (-1 = the forward's, 2 = fused into bwd-data)

@@ -188,15 +188,18 @@ def test_native_comm_single_rank_step_matches_fused():
         lib.mmad_comm_destroy(h)
 
 
-@pytest.mark.parametrize("dtype,mib", [("f32", 8), ("bf16", 8), ("bf16", 0), ("f32", 1000)])
-def test_native_exchange_schedule_loopback(dtype, mib):
+@pytest.mark.parametrize("dtype,mib,fork", [("f32", 8, 0), ("bf16", 8, 0), ("bf16", 0, 0), ("f32", 1000, 0),
+                                            ("f32", 8, 1), ("bf16", 1000, 1), ("bf16", 8, 100000)])
+def test_native_exchange_schedule_loopback(dtype, mib, fork):
     """Exchange schedule of the native DP step on one GPU: a loopback
     communicator whose all-reduce doubles each bucket (= 2 identical shards)
     after a delay.  Must equal: plain fwd+bwd, grads *= 2, loss *= 2, flat Adam
     -- i.e. every bucket is reduced after its producer finished and before its
     Adam, and the small bucket + loss are reduced too -- whatever the bucket
     plan (knob dp_bucket_mib: 0 = one bucket per layer, 1000 = all weights in
-    one bucket closed by layer 0)."""
+    one bucket closed by layer 0), and whether each side-stream dW GEMM starts
+    at its own dz or with its bucket's lowest layer (knob dp_fork_rows: 1 =
+    per layer at every batch, 100000 = per bucket)."""
     import ctypes
     import types as _t
     from icra2021_multimodal_ad_amd import _native
@@ -215,7 +218,7 @@ def test_native_exchange_schedule_loopback(dtype, mib):
                            init_state_dict(700, 40, 5, seed=81).items()})
         return m
     try:
-        with _native.tune(dp_bucket_mib=mib):
+        with _native.tune(dp_bucket_mib=mib, dp_fork_rows=fork):
             ma = mk()
         mb = mk()
         ma._native.set_comm(comm)
@@ -341,11 +344,12 @@ def _dp_plan(layers, mib):
     return out
 
 
-@pytest.mark.parametrize("dtype,rank,mib,gbf", [("bf16", 0, 8, False), ("bf16", 1, 8, False),
-                                                ("f32", 1, 8, False), ("bf16", 1, 0, False),
-                                                ("f32", 0, 2, False), ("bf16", 1, 0, True),
-                                                ("bf16", 0, 8, True), ("f32", 1, 8, True)])
-def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank, mib, gbf):
+@pytest.mark.parametrize("dtype,rank,mib,gbf,fork", [("bf16", 0, 8, False, 0), ("bf16", 1, 8, False, 0),
+                                                     ("f32", 1, 8, False, 0), ("bf16", 1, 0, False, 0),
+                                                     ("f32", 0, 2, False, 0), ("bf16", 1, 0, True, 0),
+                                                     ("bf16", 0, 8, True, 0), ("f32", 1, 8, True, 0),
+                                                     ("bf16", 1, 8, False, 1), ("f32", 0, 0, True, 1)])
+def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank, mib, gbf, fork):
     """The sharded DP step (knob dp_shard: reduce-scatter, Adam on this rank's
     1/N of each weight bucket, all-gather of the updated weights) on one GPU,
     through a loopback communicator posing as rank `rank` of 2 (its
@@ -361,7 +365,8 @@ def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank, mib, gbf):
     exchange (mmad_ae_set_grad_bf16) -- this rank's shard then equals "bf16(g)
     x 2 widened to fp32, then Adam" bit for bit (the loopback's bf16 sum of
     two identical shards is exact, as RCCL's 2-rank bf16 sum of bf16 inputs
-    rounds once)."""
+    rounds once).  fork: knob dp_fork_rows (1 = each side-stream dW GEMM at
+    its own dz)."""
     import ctypes
     import types as _t
     from icra2021_multimodal_ad_amd import _native
@@ -381,7 +386,7 @@ def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank, mib, gbf):
         m._native.sync_shadow(force=True)
         return m
     try:
-        with _native.tune(dp_bucket_mib=mib):
+        with _native.tune(dp_bucket_mib=mib, dp_fork_rows=fork):
             ma = mk()
         mb = mk()
         a, b = ma._native, mb._native
