@@ -58,6 +58,14 @@ def main():
     print(f"{len(steps)} steps, wall (first start -> last end) median {statistics.median(walls) / 1e3:.1f} us")
     for name, sid, s, e in st:
         print(f"  +{(s - t0) / 1e3:8.1f} us  {(e - s) / 1e3:7.2f} us  stream {sid}  {short(name)}")
+    # the step boundary: pack-to-pack period and the previous step's last kernels
+    periods = [steps[i + 1][0][2] - steps[i][0][2] for i in range(len(steps) - 1)]
+    if periods:
+        print(f"pack-to-pack period median {statistics.median(periods) / 1e3:.1f} us")
+    if med > 0:
+        print("previous step's last kernels (offsets from this step's pack):")
+        for name, sid, s, e in sorted(steps[med - 1], key=lambda r: r[3])[-4:]:
+            print(f"  {(s - t0) / 1e3:+9.1f} .. {(e - t0) / 1e3:+9.1f} us  stream {sid}  {short(name)}")
     agg = collections.OrderedDict()
     for stp in steps:
         for name, sid, s, e in stp:
