@@ -869,6 +869,12 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       if (each) {
         MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
         MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
+        // (a bucket whose upper layers were below the row threshold: their
+        // dW GEMMs go first, so the bucket's event below covers them too)
+        for (const PendingDW& q : pending)
+          RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, q.dz, q.lda, q.in, q.ldb, q.M, q.N, q.K, q.ep,
+                         side, nullptr, PROBE_DW + q.layer));
+        pending.clear();
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
                        nullptr, PROBE_DW + l));
         if (bk) MMAD_HIP_CHECK(hipEventRecord(h->ev_dw[l], side));
