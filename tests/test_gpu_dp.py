@@ -237,6 +237,55 @@ def test_native_exchange_schedule_loopback(dtype, mib, fork):
         lib.mmad_comm_destroy(h)
 
 
+@pytest.mark.parametrize("dtype,fork", [("bf16", 1024), ("f32", 1024), ("bf16", 0)])
+def test_native_exchange_vib_mixed_rows_loopback(dtype, fork):
+    """The native DP step on a VIB-AE with k = 2 samples: the decoder runs
+    k * B = 1024 rows, the encoder B = 512, so at dp_fork_rows = 1024 the
+    decoder layers' dW GEMMs fork one by one while the encoder layers' wait
+    for their bucket's lowest layer, inside one bucket (dp_bucket_mib = 1000:
+    every weight in the bucket layer 0 closes).  With a loopback all-reduce
+    that doubles each bucket it must equal fwd+bwd, grads x 2, flat Adam,
+    on the same injected samples."""
+    import ctypes
+    import types as _t
+    from icra2021_multimodal_ad_amd import _native
+    from icra2021_multimodal_ad_amd.data import synth_windows
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    lib = _native.load()
+    h = ctypes.c_void_p()
+    assert lib.mmad_comm_create_loopback(ctypes.byref(h), 2.0) == 0
+    comm = _t.SimpleNamespace(handle=h)
+
+    def mk():
+        cfg = _t.SimpleNamespace(input_size=700, btl_size=40, n_layers=5, gpu_id=0, dtype=dtype,
+                                 models="vib_ae", vib_k=2, beta_kl=1.0)
+        torch.manual_seed(17)
+        m = get_model(cfg)
+        m._native.sync_shadow(force=True)
+        return m
+    try:
+        with _native.tune(dp_bucket_mib=1000, dp_fork_rows=fork):
+            ma = mk()
+        mb = mk()
+        assert torch.equal(ma._native.params, mb._native.params)
+        ma._native.set_comm(comm)
+        g = torch.Generator(device="cuda").manual_seed(3)
+        for s in range(2):
+            x = torch.from_numpy(synth_windows(512, 700, seed=40 + s)).cuda()
+            eps = torch.randn(2, 512, 40, device="cuda", generator=g)
+            la = float(ma._native.train_step_fused(x, k=2, eps=eps, beta_kl=1.0))
+            lb = mb._native.train_step(x, k=2, eps=eps, beta_kl=1.0)
+            mb._native.grads.mul_(2.0)
+            mb._native.adam()
+            assert abs(la - 2.0 * float(lb)) <= 1e-5 * abs(la), (la, float(lb))
+        torch.cuda.synchronize()
+        d = (ma._native.params - mb._native.params).abs().max().item()
+        assert d <= 1e-6, d
+        ma._native.set_comm(None)
+    finally:
+        lib.mmad_comm_destroy(h)
+
+
 def _nd_cfg():
     return types.SimpleNamespace(input_size=192, btl_size=16, n_layers=5, gpu_id=0, dtype="f32",
                                  models="ae", batch_size=64, n_epochs=2, n_normal=700, n_novelty=140,
