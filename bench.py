@@ -3,7 +3,8 @@ Adam) on synthetic 4-modal windows, 1..8 MI355X (BASELINE.json metric).
 
 Workloads (``--config``; ``auto`` = c3 on one GPU -- the largest single-GPU
 configuration, C4's per-GPU shard -- with c2 measured after it in the same line
-as the ``c2`` sub-object; c4 on several):
+as the ``c2`` sub-object and c3 on the exact-fp32 parity path as ``c3_f32``; c4
+on several):
   c2  BASELINE configs[1]: FC-AE, D=2048, 1024 windows, bf16, 1 GPU
   c3  BASELINE configs[2]: VIB-AE (k=1, beta_kl=1), D=2048, 4096 windows, bf16
   c4  BASELINE configs[3]: the c3 model, 4096 windows PER GPU (global 4096*N),
@@ -139,8 +140,9 @@ def cpu_baseline(d, batch, vib, budget_s=12.0):
 def dw_adam_bytes(N, K, B, es=2):
     """Algorithmic HBM bytes of one dW GEMM with the fused Adam epilogue:
     fp32 p/m/v read + written (24 B/param) + the bf16 weight shadow written
-    (2 B/param) + the two operands dz [B x N] and a [B x K] read once."""
-    return 26 * N * K + es * B * (N + K)
+    (2 B/param, bf16 models only) + the two operands dz [B x N] and a [B x K]
+    read once (es bytes per element)."""
+    return (26 if es == 2 else 24) * N * K + es * B * (N + K)
 
 
 def pick_dominant_layer(nat, batch):
@@ -278,12 +280,12 @@ def dw_roofline(nat, layer, durations_ms, batch, steps_timed, fused_adam=True, l
         flops += 2.0 * rows * L["N"] * L["K"]
     if fused_adam:
         what = "bwd-weight + fused Adam"
-        body = "p/m/v fp32 + bf16 shadow updated in the epilogue"
+        body = ("p/m/v fp32 + bf16 shadow updated in the epilogue" if es == 2 else
+                "p/m/v fp32 updated in the epilogue")
     else:
         what = "bwd-weight"
         body = "fp32 dW written for the all-reduce; Adam runs after the exchange"
     avg_s = statistics.fmean(durations_ms) / 1e3
-    ach = nbytes / avg_s / 1e9
     wl = {"dim": nat.enc_widths[0], "batch": batch, "dtype": nat.dtype_name,
           "model": "vib_ae" if nat.vib else "ae", "layer": layer}
     if len(layers) > 1:
@@ -291,10 +293,21 @@ def dw_roofline(nat, layer, durations_ms, batch, steps_timed, fused_adam=True, l
     tf, _ = pmc_fields("dw", wl)
     shapes = ", ".join(f"layer {l}: dW[{nat.layers[l]['N']}x{nat.layers[l]['K']}]" for l in layers)
     kern = "mmad_gemm"
+    # the bound is whichever resource the launch needs longer at its peak: HBM
+    # for the bf16 launch (26 B/param of Adam state against bf16 MFMA), the
+    # f32-input MFMA for the exact-fp32 one (1/16 of the bf16 rate)
+    mpeak = BF16_PEAK_TFLOPS if es == 2 else F32_PEAK_TFLOPS
+    hbm_bound = nbytes / (HBM_PEAK_GBS * 1e9) >= flops / (mpeak * 1e12)
+    if hbm_bound:
+        bound, ach, peak, unit = "hbm", nbytes / avg_s / 1e9, HBM_PEAK_GBS, "GB/s"
+        other = {"mfma_tflops": round(flops / avg_s / 1e12, 2), "mfma_frac": round(flops / avg_s / 1e12 / mpeak, 4)}
+    else:
+        bound, ach, peak, unit = "mfma", flops / avg_s / 1e12, mpeak, "TFLOP/s"
+        other = {"hbm_gbs": round(nbytes / avg_s / 1e9, 1), "hbm_frac": round(nbytes / avg_s / 1e9 / HBM_PEAK_GBS, 4)}
     return {"kernel": f"{kern} {what} ({shapes} = dz^T a over {rows} windows"
                       f"{'; both layers in one launch' if len(layers) > 1 else ''}; {body})",
-            "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), **tf,
+            "bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
+            "frac": round(ach / peak, 4), **tf, **other,
             "avg_us": round(avg_s * 1e6, 2), "launches_timed": len(durations_ms),
             "algorithmic_bytes_per_launch": nbytes,
             "flops_per_launch": flops,
@@ -319,6 +332,8 @@ def parse_args(argv=None):
                     help="untimed steps for about this many seconds after the warmup (0 = none)")
     ap.add_argument("--no-c2", action="store_true",
                     help="auto at N=1: skip the c2 sub-object (BASELINE configs[1]) in the same line")
+    ap.add_argument("--no-f32", action="store_true",
+                    help="auto at N=1: skip the c3_f32 sub-object (the exact-fp32 parity path at c3)")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
                     help="set a tune-table knob for the whole run (A/B of schedules; "
                          "icra2021_multimodal_ad_amd._native.KNOB names)")
@@ -367,12 +382,25 @@ def run(args):
         # the smaller BASELINE configs[1] in the same line, so the c2 series of
         # earlier rounds stays comparable (same steps / warmup, its own probes)
         del model
+        model = None
         torch.cuda.synchronize()
         sub, _ = train_workload(args, "c2", dict(CONFIGS["c2"]), rank, world, local, with_cpu=False)
         keep = ("value", "unit", "ms_per_step", "steps", "warmup", "soak_steps", "config", "model_tflops",
                 "host_enqueue_ms_per_step", "final_loss", "step_spread", "train_step", "roofline",
                 "roofline_encoder_gemm")
         res["c2"] = {k: sub[k] for k in keep if k in sub}
+        if not args.no_f32:
+            # the same c3 workload on the exact-fp32 path (fp32 storage, f32-input
+            # MFMA, apply-mode BatchNorm): the path the parity tests pin at 1e-4
+            # (tests/test_gpu_vib_full.py), with its own rooflines against the
+            # f32 MFMA peak
+            torch.cuda.synchronize()
+            a32 = argparse.Namespace(**vars(args))
+            a32.dtype = "f32"
+            sub, _ = train_workload(a32, "c3", dict(CONFIGS["c3"]), rank, world, local, with_cpu=False)
+            res["c3_f32"] = {k: sub[k] for k in keep + ("dtype",) if k in sub}
+            res["c3_f32"]["note"] = ("c3 on the exact-fp32 path (the one pinned within 1e-4 of the fp64 "
+                                     "oracle); value / ms_per_step measured like the headline's")
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

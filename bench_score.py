@@ -155,6 +155,17 @@ def run_c5(args):
     for _ in range(max(1, args.warmup)):        # the first call captures the graph
         one_pass()
     torch.cuda.synchronize()
+    diag = os.environ.get("MMAD_CRASH_DIAG")
+    if diag:
+        # crash diagnostics (round-5 SIGSEGV under rocprofv3): every Python
+        # thread's stack on a fatal signal, and this process's memory map
+        # once every library is loaded, so a native frame's address can be
+        # resolved to library + offset afterwards
+        import faulthandler
+        os.makedirs(diag, exist_ok=True)
+        faulthandler.enable(file=open(os.path.join(diag, "faulthandler.txt"), "w"), all_threads=True)
+        with open("/proc/self/maps") as f, open(os.path.join(diag, "maps.txt"), "w") as g:
+            g.write(f.read())
     t0 = time.perf_counter()
     for _ in range(args.steps):
         base, sap = one_pass()

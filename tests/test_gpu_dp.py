@@ -478,6 +478,155 @@ def test_sharded_exchange_shard_arithmetic_loopback(dtype, rank, mib, gbf, fork)
         lib.mmad_comm_destroy(h)
 
 
+def _c4_model(dtype):
+    """BASELINE configs[3]'s per-GPU model: VIB-AE, D=2048, btl 100, 5+5 layers
+    (bench.py CONFIGS['c4']), seeded init, shadow synced."""
+    import types as _t
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    cfg = _t.SimpleNamespace(input_size=2048, btl_size=100, n_layers=5, gpu_id=0, dtype=dtype,
+                             models="vib_ae", vib_k=1, beta_kl=1.0)
+    torch.manual_seed(29)
+    m = get_model(cfg)
+    m._native.sync_shadow(force=True)
+    return m
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("gbf", [False, True])
+@pytest.mark.parametrize("rank", [0, 3, 7])
+def test_c4_sharded_exchange_rank_of_8_loopback(dtype, gbf, rank):
+    """The C4 exchange at its own shape (BASELINE configs[3]: VIB-AE, D=2048,
+    4096 windows per GPU, 8 ranks), default knobs (dp_bucket_mib 8 ->
+    buckets {9}, {8}, {7..3}, {2,1}, {0}; dp_fork_rows default), on one GPU
+    through a loopback communicator posing as rank `rank` of 8: its
+    reduce-scatter multiplies this rank's 1/8 slice by 8 (= 8 identical
+    shards summed into the slice RCCL's in-place reduce-scatter writes), its
+    all-gather leaves the other 7 slices alone.  After one step, for every
+    weight bucket: this rank's slice of p / m / v (and the bf16 shadow) equals
+    "grads x 8, then Adam" of a single-process step on the same batch and
+    injected VIB noise, bit for bit; the other 7/8 keep their pre-step values;
+    the small bucket (bias / gamma / beta + loss) is all-reduced and fully
+    updated.  gbf: the bf16 gradient exchange (x 8 is exact in bf16, so the
+    slice equals "bf16(g) x 8 widened, then Adam").  Every bucket of the
+    padded layout is a multiple of 128 x 128 values, so n / 8 is an integer
+    multiple of 4 and every weight bucket takes the sharded form (the
+    all-reduce fallback for other rank counts: the test below)."""
+    import ctypes
+    import types as _t
+    from icra2021_multimodal_ad_amd import _native
+    from icra2021_multimodal_ad_amd.data import synth_windows
+    lib = _native.load()
+    world = 8
+    h = ctypes.c_void_p()
+    assert lib.mmad_comm_create_loopback_ranks(ctypes.byref(h), float(world), world, rank) == 0
+    comm = _t.SimpleNamespace(handle=h)
+    try:
+        ma, mb = _c4_model(dtype), _c4_model(dtype)
+        a, b = ma._native, mb._native
+        assert torch.equal(a.params, b.params)
+        a.set_comm(comm)
+        if gbf:
+            a.set_grad_bf16(True)
+        x = torch.from_numpy(synth_windows(4096, 2048, seed=400 + rank)).cuda()
+        eps = torch.randn(1, 4096, 100, device="cuda",
+                          generator=torch.Generator(device="cuda").manual_seed(rank))
+        p0, m0, v0 = a.params.clone(), a.exp_avg.clone(), a.exp_avg_sq.clone()
+        s0 = a.shadow.clone() if dtype == "bf16" else None
+        la = float(a.train_step_fused(x, k=1, eps=eps, beta_kl=1.0))
+        lb = b.train_step(x, k=1, eps=eps, beta_kl=1.0)
+        if gbf:
+            b.grads[:b.n_weight] = b.grads[:b.n_weight].bfloat16().float()
+        b.grads.mul_(float(world))
+        b.adam()
+        torch.cuda.synchronize()
+        a.check_status()
+        assert abs(la - world * float(lb)) <= 1e-5 * abs(la), (la, float(lb))
+        assert lib.mmad_ae_dp_master_stale(a._h) == 1
+        plan = _dp_plan(a.layers, 8)
+        assert [n for _, n in plan] == [n for _, n, _ in a.dw_plan()]
+        assert [lo for _, _, lo in a.dw_plan()] == [9, 8, 3, 1, 0]
+        covered = 0
+        for boff, n in plan:
+            assert n % world == 0 and (n // world) % 4 == 0, (boff, n)
+            cnt = n // world
+            own = slice(boff + rank * cnt, boff + (rank + 1) * cnt)
+            for name, ref0 in (("params", p0), ("exp_avg", m0), ("exp_avg_sq", v0)):
+                got, want = getattr(a, name), getattr(b, name)
+                assert torch.equal(got[own], want[own]), (name, boff)
+                assert not torch.equal(got[own], ref0[own]), (name, "own shard not updated", boff)
+                for r in range(world):
+                    if r != rank:
+                        oth = slice(boff + r * cnt, boff + (r + 1) * cnt)
+                        assert torch.equal(got[oth], ref0[oth]), (name, "other shard changed", boff, r)
+            if dtype == "bf16":
+                assert torch.equal(a.shadow[own], b.shadow[own])
+                assert torch.equal(a.shadow[boff:boff + rank * cnt], s0[boff:boff + rank * cnt])
+                assert torch.equal(a.shadow[boff + (rank + 1) * cnt:boff + n], s0[boff + (rank + 1) * cnt:boff + n])
+            covered += n
+        nw = a.n_weight
+        assert covered == nw
+        for name in ("params", "exp_avg", "exp_avg_sq"):      # the small bucket: all-reduced
+            assert torch.equal(getattr(a, name)[nw:], getattr(b, name)[nw:]), name
+        assert torch.equal(a.running, b.running)
+        a.sync_master()                                        # loopback all-gather: a no-op
+        a.set_comm(None)
+    finally:
+        lib.mmad_comm_destroy(h)
+
+
+@pytest.mark.parametrize("dtype,world,rank", [("f32", 6, 2), ("bf16", 3, 1), ("bf16", 7, 4)])
+def test_c4_exchange_indivisible_world_falls_back_to_all_reduce(dtype, world, rank):
+    """A rank count that does not divide a bucket takes the all-reduce form
+    for that bucket: the whole bucket summed, then Adam on all of it and the
+    shadow.  At the C4 model (buckets of 3407872, 2129920, 2490368, 3964928,
+    3670016 values) 3 and 6 ranks divide none of them; 7 divides only layer
+    0's bucket, which is sharded while the other four are all-reduced.  The
+    result is "grads x world, then Adam" on every all-reduced bucket and on
+    this rank's slice of a sharded one, bit for bit; the master weights are
+    stale only when some bucket was sharded."""
+    import ctypes
+    import types as _t
+    from icra2021_multimodal_ad_amd import _native
+    from icra2021_multimodal_ad_amd.data import synth_windows
+    lib = _native.load()
+    h = ctypes.c_void_p()
+    assert lib.mmad_comm_create_loopback_ranks(ctypes.byref(h), float(world), world, rank) == 0
+    comm = _t.SimpleNamespace(handle=h)
+    try:
+        ma, mb = _c4_model(dtype), _c4_model(dtype)
+        a, b = ma._native, mb._native
+        a.set_comm(comm)
+        x = torch.from_numpy(synth_windows(4096, 2048, seed=77)).cuda()
+        eps = torch.randn(1, 4096, 100, device="cuda", generator=torch.Generator(device="cuda").manual_seed(5))
+        la = float(a.train_step_fused(x, k=1, eps=eps, beta_kl=1.0))
+        lb = b.train_step(x, k=1, eps=eps, beta_kl=1.0)
+        b.grads.mul_(float(world))
+        b.adam()
+        torch.cuda.synchronize()
+        assert abs(la - world * float(lb)) <= 1e-5 * abs(la)
+        n_sharded = 0
+        for boff, n in _dp_plan(a.layers, 8):
+            if n % world == 0 and (n // world) % 4 == 0:
+                n_sharded += 1
+                cnt = n // world
+                rng = slice(boff + rank * cnt, boff + (rank + 1) * cnt)
+            else:
+                rng = slice(boff, boff + n)
+            for name in ("params", "exp_avg", "exp_avg_sq"):
+                assert torch.equal(getattr(a, name)[rng], getattr(b, name)[rng]), (name, boff)
+            if dtype == "bf16":
+                assert torch.equal(a.shadow[rng], b.shadow[rng]), boff
+        assert n_sharded == (1 if world == 7 else 0)
+        nw = a.n_weight
+        for name in ("params", "exp_avg", "exp_avg_sq"):
+            assert torch.equal(getattr(a, name)[nw:], getattr(b, name)[nw:]), name
+        assert lib.mmad_ae_dp_master_stale(a._h) == (1 if n_sharded else 0)
+        a.sync_master()
+        a.set_comm(None)
+    finally:
+        lib.mmad_comm_destroy(h)
+
+
 def test_rank_local_guard_follows_the_attached_communicator():
     """A step whose executor still holds a communicator enters collectives
     even when model.dist has been cleared (bench.py's rank-0 probe does
