@@ -334,6 +334,9 @@ def parse_args(argv=None):
                     help="auto at N=1: skip the c2 sub-object (BASELINE configs[1]) in the same line")
     ap.add_argument("--no-f32", action="store_true",
                     help="auto at N=1: skip the c3_f32 sub-object (the exact-fp32 parity path at c3)")
+    ap.add_argument("--stream", choices=["default", "own"], default="default",
+                    help="own: run every step on a created non-blocking stream instead of the "
+                         "caller's default stream (schedule studies, e.g. --tune side_cu_held=N)")
     ap.add_argument("--tune", action="append", default=[], metavar="KNOB=VALUE",
                     help="set a tune-table knob for the whole run (A/B of schedules; "
                          "icra2021_multimodal_ad_amd._native.KNOB names)")
@@ -366,6 +369,8 @@ def run(args):
     for kv in args.tune:
         k, v = kv.split("=", 1)
         _native.tune_set(k, int(v))
+    if args.stream == "own":
+        torch.cuda.set_stream(torch.cuda.Stream())
     if cname == "c5":
         import bench_score
         if world > 1:

@@ -120,10 +120,10 @@ SIGNATURES = {
 
 
 # the library's tune table (include/mmad.h, mmad_tune_set): GEMM knobs are read
-# per dispatch, the schedule knobs (14, 16-31) when a model handle is created
+# per dispatch, the schedule knobs (14-31) when a model handle is created
 KNOB = dict(tile=0, group_m=1, autotune=2, dbg=3, splitk=4, tile_adam=5, tile_bwd_data=6,
             tile_fwd=7, tile_adam_main=8, splitk_dw=9, splitk_dw_blocks=10, splitk_dw_min_stages=11,
-            persist=12, bn_apply_rb=13,
+            persist=12, bn_apply_rb=13, side_cu_held=15,
             bn_mode=16, bn_mode_bwd=17, bn_fused_rows=18, dw_main=19, pair_rows=20, dw_main_ping=21,
             ev_every=22, loss_side=23, dp_small_at=24, keep_grads=25, side_prio=26,
             event_sysfence=27, dp_shard=28, side_hold=29, dp_bucket_mib=30, ev_on_kernel=31, dp_fork_rows=14)

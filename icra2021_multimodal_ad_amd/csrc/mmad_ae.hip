@@ -71,6 +71,9 @@ struct mmad_ae {
   unsigned ev_flags_ = 0;
   int loss_side = 1;      // knob 23: reduce the loss on the side stream after the forward
   int side_prio_hi = 0;   // knob 26
+  // knob 15: > 0 = the side stream is created behind a CU mask that leaves
+  // this many CUs (evenly spaced over the mask) to the main stream alone
+  int side_cu_held = 0;
   // data-parallel step: the small bucket (bias / gamma / beta grads + loss)
   // goes on the comm stream right after the bwd-data GEMM of this layer
   // (ahead of this layer's and the lower layers' weight buckets); knob 24
@@ -254,6 +257,16 @@ struct AeWS {
 
 static size_t esz(int dtype) { return dtype == MMAD_BF16 ? 2 : 4; }
 
+// can the dispatcher choose a split-K factor > 1 for this handle's GEMMs?
+// (any dtype: a forced override, knob 4; bf16: the dW rule, when a dW
+// override or the dW split target is set -- by default nothing splits)
+static bool splitk_possible(int dtype) {
+  const int o = mmad_splitk_override();
+  if (o > 1) return true;
+  if (o == 1 || dtype != MMAD_BF16) return false;
+  return mmad_splitk_dw_override() > 1 || mmad_splitk_dw_blocks() > 0;
+}
+
 static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
   int64_t off = 0;
   auto take = [&](int64_t bytes) -> char* {
@@ -305,10 +318,15 @@ static void carve(const mmad_ae* h, int B, int k, char* base, AeWS& w) {
   w.dyn_dev = (MmadDyn*)take(sizeof(MmadDyn));
   w.dyn = nullptr;
   {
+    // the split-K partial slabs (54.5 MB per stream) only when the current
+    // knobs let the dispatcher split one of this handle's GEMMs; without a
+    // slab it never splits.  Sized per call from the knobs in force, so a
+    // later override grows the workspace the next size query reports (and a
+    // caller that skipped the query gets "workspace too small", not an overrun)
     size_t slab = 0, ctl = 0;
-    mmad_gemm_splitk_bytes(0, 0, &slab, &ctl);
-    w.sk_slab[0] = (float*)take((int64_t)slab);
-    w.sk_slab[1] = (float*)take((int64_t)slab);
+    if (splitk_possible(h->dtype)) mmad_gemm_splitk_bytes(0, 0, &slab, &ctl);
+    w.sk_slab[0] = slab ? (float*)take((int64_t)slab) : nullptr;
+    w.sk_slab[1] = slab ? (float*)take((int64_t)slab) : nullptr;
   }
   {
     const AeLayer& last = h->L[nL - 1];
@@ -382,6 +400,7 @@ int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, i
     h->dp_small_at = mmad_knob(24);
     h->keep_grads = mmad_knob(25);
     h->side_prio_hi = mmad_knob(26);
+    h->side_cu_held = mmad_knob(15);
     h->dp_shard = mmad_knob(28);
     h->side_hold = mmad_knob(29);
     h->dp_bucket_mib = mmad_knob(30) < 0 ? 0 : mmad_knob(30);
@@ -462,8 +481,27 @@ int mmad_ae_bind(mmad_ae* h, float* params, float* grads, float* adam_m, float* 
     int least = 0, greatest = 0;
     MMAD_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     // (knob 26: the highest priority instead, for schedule sweeps)
-    MMAD_HIP_CHECK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking,
-                                               h->side_prio_hi ? greatest : least));
+    if (h->side_cu_held > 0) {
+      // schedule study: the side stream's dW + Adam GEMMs kept off side_cu_held
+      // CUs so the bwd-data / BN-apply chain always has CUs of its own.  The
+      // masked stream is created blocking at the default priority (the API
+      // takes neither), so the caller's stream must be a created non-blocking
+      // one, not the legacy null stream, or every side launch serialises
+      int dev = 0, ncu = 0;
+      MMAD_HIP_CHECK(hipGetDevice(&dev));
+      MMAD_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+      const int held = std::min(h->side_cu_held, ncu - 1), stride = std::max(1, ncu / std::max(1, held));
+      std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+      for (int i = 0, n_held = 0; i < ncu; ++i) {
+        const bool hold = n_held < held && i % stride == stride - 1;
+        n_held += hold;
+        if (!hold) mask[i / 32] |= 1u << (i % 32);
+      }
+      MMAD_HIP_CHECK(hipExtStreamCreateWithCUMask(&h->side, (uint32_t)mask.size(), mask.data()));
+    } else {
+      MMAD_HIP_CHECK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking,
+                                                 h->side_prio_hi ? greatest : least));
+    }
     const size_t n = h->L.size();
     h->ev_fork.resize(n);
     h->ev_data.resize(n);
@@ -524,12 +562,6 @@ static const void* input_of(const mmad_ae* h, const AeWS& w, int l, bool train,
   return ps.out;
 }
 
-// can the dispatcher choose a split-K factor > 1 for this handle's GEMMs?
-// (bf16: the dW rule; any dtype: a forced override)
-static bool splitk_possible(int dtype) {
-  const int o = mmad_splitk_override();
-  return o > 1 || (dtype == MMAD_BF16 && o != 1);
-}
 
 static int prepare_ws(const mmad_ae* h, int B, int k, void* ws, int64_t ws_bytes, AeWS& w,
                       hipStream_t st) {

@@ -32,7 +32,7 @@ int mmad_pad_granule(void) { return MMAD_PAD; }
 // Tuning knobs: ONE table, set only through mmad_tune_set (the library reads
 // no environment variables, so every rank of a job runs the same schedule
 // unless its code says otherwise).  GEMM knobs (0-11) are read per dispatch;
-// the executor's schedule knobs (14, 16-31) are copied into a handle when it is
+// the executor's schedule knobs (14-31) are copied into a handle when it is
 // created (mmad_ae_create), so a handle keeps one schedule for its lifetime.
 namespace {
 int g_knob[MMAD_KNOB_COUNT] = {
@@ -48,10 +48,10 @@ int g_knob[MMAD_KNOB_COUNT] = {
     0,     // 9  split-K override of the dW GEMMs
     0,     // 10 dW split rule: target 64x64-tile blocks (0 = no split)
     8,     // 11 dW split rule: minimum K stages per slice
-    0,     // 12 persistent grid for forward-type GEMMs (-1 rule, 0 off, 1 on)
+    0,     // 12 persistent grid for forward-type GEMMs (0 off; else when the tiles exceed one round)
     1,     // 13 BN-backward apply: 128-row slabs per block (1, 2, 4)
     1024,  // 14 DP: per-layer dW fork from this many padded rows (0 = one fork per bucket)
-    0,     // 15 retired (a measured-slower experiment, removed in round 3)
+    0,     // 15 side stream behind a CU mask holding this many CUs for the main stream (0 = off)
     -1,    // 16 train-mode BN schedule (-1 = dtype default: bf16 fused, fp32 apply; 0 apply, 1 fold, 2 fused)
     -1,    // 17 backward BN schedule (-1 = the forward's; 2 = fused into the bwd-data GEMMs)
     2048,  // 18 fused BN up to this many padded rows (fold above)
@@ -118,7 +118,7 @@ int mmad_tile_epi_override(int epi) {
 }
 
 static bool knob_valid(int knob) {
-  return knob >= 0 && knob < MMAD_KNOB_COUNT && knob != 15;
+  return knob >= 0 && knob < MMAD_KNOB_COUNT;
 }
 int mmad_tune_set(int knob, int value) {
   if (!knob_valid(knob)) {

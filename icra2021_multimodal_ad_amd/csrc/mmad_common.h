@@ -101,8 +101,13 @@ __device__ __forceinline__ float act_grad_from_out(float a, int act, float slope
 }
 
 // torch.optim.Adam element update, as torch's _single_tensor_adam computes it
-// on the CPU (the reference's optimizer, novelty_detection.py:90) -- every
-// rounding step in torch's order (checked against torch 2.10 CPU kernels):
+// on the CPU (the reference's optimizer, novelty_detection.py:90, in the form
+// its golden vectors were generated in: torch-CPU) -- every rounding step in
+// torch's CPU order (checked against torch 2.10 CPU kernels).  The
+// reference's default device run (--gpu_id 0, model_builder.py:50-51) would
+// take torch's foreach CUDA path, whose addcdiv rounds p + s * (m / denom)
+// instead of p + (s * m) / denom: that form is not pinned here (no CUDA
+// reference run exists to pin it against):
 //   exp_avg.lerp_(g, 1 - b1)            m = fma(w1, g - m, m)   (w1 < 0.5)
 //   exp_avg_sq.mul_(b2).addcmul_(g, g, value=1 - b2)
 //                                       v = fma(w2 * g, g, v * b2)

@@ -95,6 +95,9 @@ template <> struct Cfg<8> { static constexpr int BM = 256, BN = 256, WM = 2, WN 
 constexpr int CFG_XST1 = 9;
 template <> struct Cfg<9> { static constexpr int BM = 256, BN = 128, WM = 4, WN = 2, NS = 3, NT = 512; };
 constexpr int NCFG = 10;
+// capacity-cache keys pack (device, dtype, epilogue, cfg) into one integer
+// with 8 slots per epilogue field and 16 per cfg field
+static_assert(NCFG <= 16, "widen the cfg field of the capacity-cache keys");
 constexpr int CFG_BM[NCFG] = {128, 256, 128, 64, 64, 128, 256, 256, 256, 256};
 constexpr int CFG_BN[NCFG] = {128, 128, 256, 64, 128, 128, 256, 256, 256, 128};
 constexpr int CFG_NT[NCFG] = {512, 512, 512, 256, 256, 256, 512, 512, 256, 512};
@@ -2062,7 +2065,7 @@ std::map<long, int> g_pcap;   // (device, epi, cfg) -> resident blocks of the pe
 static int persist_capacity(const void* fn, int epi, int cfg) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
-  const long key = ((long)dev * 8 + epi) * 8 + cfg;
+  const long key = ((long)dev * 8 + epi) * 16 + cfg;
   {
     std::lock_guard<std::mutex> lk(g_pcap_mu);
     auto it = g_pcap.find(key);
@@ -2093,7 +2096,8 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
   const int S = ep.splitk > 1 ? ep.splitk : 1;
   ep.group_m = plan_group_m(ntiles, tiles_m, BM, BN);
   // persistent grid: forward-type bf16 epilogues without a fused BN or a
-  // split, when the tiles exceed one resident round (knob 12: -1 rule, 1 on)
+  // split, when the tiles exceed one resident round (knob 12: any nonzero
+  // value; with fewer tiles the ordinary grid is the same launch)
   const int pk = mmad_persist_override();
   if (pk != 0 && S == 1 && !ep.bn_sync && persist_cfg(cfg)) {
     const void* pfn = persist_kernel<T, TO, AK, BK_, EPI>(cfg);
@@ -2207,7 +2211,7 @@ std::map<long, int> g_occ;   // (device, dtype, epi, cfg) -> resident grid capac
 static int grid_capacity(int dtype, int epi, int cfg) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
-  const long key = (((long)dev * 4 + dtype) * 8 + epi) * 8 + cfg;
+  const long key = (((long)dev * 4 + dtype) * 8 + epi) * 16 + cfg;
   {
     std::lock_guard<std::mutex> lk(g_occ_mu);
     auto it = g_occ.find(key);

@@ -7,9 +7,11 @@
 #include "mmad_ops.h"
 #include "mmad_gemm.h"
 
+#include <charconv>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <system_error>
 
 #define SLAB_COLS 64
 #define SLAB_ROWS 128
@@ -672,11 +674,13 @@ __global__ __launch_bounds__(256) void adam_k(int64_t n, float* __restrict__ p,
     *(floatx4*)(p + i4) = pp;
     *(floatx4*)(m + i4) = mm;
     *(floatx4*)(v + i4) = vv;
-    if (shadow && i4 < n_shadow) {
+    if (shadow && i4 + 4 <= n_shadow) {
       bf16x4 s;
 #pragma unroll
       for (int k = 0; k < 4; ++k) s[k] = (bf16)pp[k];
       *(bf16x4*)(shadow + i4) = s;
+    } else if (shadow) {   // a shadow shorter than the buffer, ending inside this quad
+      for (int k = 0; k < 4 && i4 + k < n_shadow; ++k) shadow[i4 + k] = (bf16)pp[k];
     }
   } else {
     for (int64_t i = i4; i < n; ++i) {
@@ -982,8 +986,9 @@ int mmad_bn_act_bwd_apply(int dtype, int act, float slope, int M, int N, int Mp,
                           const float* save_rstd, const float* gamma, const double* part,
                           int nparts, void* dz, float* dgamma, float* dbeta, float* db_partials,
                           void* stream) {
-  // 128-row slabs per block (knob 13: 1, 2 or 4; 0 = rule): the column
-  // partials are merged once per block instead of once per 128-row slab
+  // 128-row slabs per block (knob 13: 1, 2 or 4; any other value = 1; halved
+  // until it divides the row slabs): the column partials are merged once per
+  // block instead of once per 128-row slab
   int rb = mmad_knob(13);
   if (rb != 1 && rb != 2 && rb != 4) rb = 1;
   while (rb > 1 && (Mp / SLAB_ROWS) % rb) rb >>= 1;
@@ -1132,13 +1137,18 @@ int mmad_sse_partials(int dtype, int M, int N, int Np, const void* y, const floa
 
 double mmad_decimal_of(float f) {
   // the shortest decimal that rounds to f, as a double: the Python float a
-  // caller's optimizer holds (0.9, 0.999, 1e-3) when it reached us as float
-  char buf[32];
-  for (int prec = 1; prec <= 9; ++prec) {
-    snprintf(buf, sizeof buf, "%.*g", prec, (double)f);
-    if (strtof(buf, nullptr) == f) return strtod(buf, nullptr);
-  }
-  return (double)f;
+  // caller's optimizer holds (0.9, 0.999, 1e-3) when it reached us as float.
+  // std::to_chars / from_chars: shortest round-trip form, independent of the
+  // process locale (snprintf / strtod read LC_NUMERIC's decimal point).  A
+  // hyper-parameter that was not a short decimal (a scheduler's lr) comes
+  // back as the shortest decimal of its float, i.e. within the float's
+  // rounding of the caller's double -- the float ABI carries no more.
+  char buf[64];
+  const auto r = std::to_chars(buf, buf + sizeof buf, f);
+  if (r.ec != std::errc()) return (double)f;
+  double d = 0.0;
+  const auto q = std::from_chars(buf, r.ptr, d);
+  return q.ec == std::errc() && q.ptr == r.ptr ? d : (double)f;
 }
 
 MmadAdamConsts mmad_adam_consts(float lr, float beta1, float beta2, float eps, int step) {

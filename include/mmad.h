@@ -65,13 +65,18 @@ int mmad_pad_granule(void);
  *      -1 = knob 5);
  *      6 / 7 = tile of the bwd-data / forward GEMMs (-1 autotuned)
  *   12 persistent grid for the forward-type GEMMs without a fused BN or a
- *      split (-1 rule: when the tiles exceed one resident round; 0 off; 1 on)
- *   13 BN-backward apply kernel: 128-row slabs per block (1, 2 or 4; the
- *      column partials are merged once per block)
+ *      split (0 off; any other value: persistent whenever the tiles exceed
+ *      one resident round -- with fewer tiles the ordinary grid is the same
+ *      launch)
+ *   13 BN-backward apply kernel: 128-row slabs per block (1, 2 or 4; any other
+ *      value = 1; halved until it divides the row slabs; the column partials
+ *      are merged once per block)
  *   14 data parallel: from this many padded rows, each side-stream dW GEMM
  *      starts at its own dz instead of with its bucket's lowest layer (1024;
  *      0 = one fork per bucket)
- *   15 retired (EINVAL)
+ *   15 schedule study: the side stream created behind a CU mask that leaves
+ *      this many CUs to the main stream alone (0 = off; the masked stream is
+ *      blocking, so call the step on a created non-blocking stream)
  *   16 train-mode BN schedule (-1 dtype default: bf16 fused, fp32 apply;
  *      0 apply kernels, 1 fold into the consumer, 2 fused into the GEMMs)
  *   17 backward BN schedule (-1 = the forward's, 2 = fused into bwd-data)

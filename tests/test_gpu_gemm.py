@@ -204,8 +204,8 @@ def test_splitk_timeout_is_reported_not_combined(ws):
 
 @pytest.mark.parametrize("kind", ["fwd", "fwdns", "score", "mse"])
 def test_persistent_grid_bit_identical(kind):
-    """Knob 12 (persistent grid: one block per resident slot walks the tiles)
-    gives the ordinary grid's bits for the forward-type bf16 epilogues, with
+    """Knob 12 (persistent grid: one block per resident slot walks the tiles;
+    1 and -1 alike) gives the ordinary grid's bits for the forward-type bf16 epilogues, with
     every large-row tile (256x128, 128x256, 256x256; tile 7 also issues the
     next tile's first K stages from its epilogue) forced, at a row count
     whose tiles exceed one resident round (16,384 rows: 512-1024 tiles on 256
@@ -244,10 +244,11 @@ def test_persistent_grid_bit_identical(kind):
             lib.mmad_tune_set(0, tile)
             lib.mmad_tune_set(12, 0)
             a = run()
-            lib.mmad_tune_set(12, 1)
-            p = run()
-            torch.cuda.synchronize()
-            assert torch.equal(a[0], p[0]) and torch.equal(a[1], p[1]), (kind, tile)
+            for pk in (1, -1):                   # any nonzero value: persistent above one round
+                lib.mmad_tune_set(12, pk)
+                p = run()
+                torch.cuda.synchronize()
+                assert torch.equal(a[0], p[0]) and torch.equal(a[1], p[1]), (kind, tile, pk)
     finally:
         lib.mmad_tune_set(0, -1)
         lib.mmad_tune_set(12, 0)

@@ -196,3 +196,57 @@ def test_standalone_mse_loss_matches_torch(reduction, shape):
     (ref * 3.0).backward()
     for got, want in ((a.grad, ref_a.grad), (b.grad, ref_b.grad)):
         assert torch.allclose(got.cpu().double(), want, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("betas,step,lr", [((0.9, 0.999), 1, 1e-3), ((0.9, 0.999), 3, 1e-3),
+                                           ((0.8, 0.95), 2, 3e-4)])
+def test_public_adam_matches_torch_cpu_adam(betas, step, lr):
+    """The public flat optimizer entry mmad_adam (include/mmad.h; the
+    reference's optim.Adam step, novelty_detection.py:90) on an odd-length
+    buffer with a bf16 shadow: m / v equal torch.optim.Adam's CPU
+    single-tensor step from the same state bit for bit, p within one ulp (the
+    update order adam_elem restates; see below), all within 1e-6 of a float64
+    evaluation of the same formulas, and the shadow is bf16(p)."""
+    from icra2021_multimodal_ad_amd import _native
+    from icra2021_multimodal_ad_amd._native import call, ptr, stream_ptr
+    n = 4099
+    g_ = torch.Generator().manual_seed(step)
+    p0 = torch.randn(n, generator=g_) * 0.05
+    g = torch.randn(n, generator=g_) * 1e-2
+    m0 = torch.randn(n, generator=g_) * 1e-3 if step > 1 else torch.zeros(n)
+    v0 = torch.rand(n, generator=g_) * 1e-5 if step > 1 else torch.zeros(n)
+    # torch CPU, foreach=False (_single_tensor_adam), state after step - 1 steps
+    prm = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.Adam([prm], lr=lr, betas=betas, eps=1e-8, foreach=False)
+    opt.state[prm] = {"step": torch.tensor(float(step - 1)), "exp_avg": m0.clone(),
+                      "exp_avg_sq": v0.clone()}
+    prm.grad = g.clone()
+    opt.step()
+    st = opt.state[prm]
+    # the product: step size / bias correction as the executor forms them
+    b1, b2 = betas
+    step_size = lr / (1.0 - b1 ** step)
+    bc2_sqrt = (1.0 - b2 ** step) ** 0.5
+    dp, dg, dm, dv = (t.clone().cuda() for t in (p0, g, m0, v0))
+    shadow = torch.zeros(n, device="cuda", dtype=torch.bfloat16)
+    call("mmad_adam", n, ptr(dp), ptr(dg), ptr(dm), ptr(dv), b1, b2, 1e-8, step_size, bc2_sqrt,
+         ptr(shadow), n, stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dm.cpu(), st["exp_avg"])
+    assert torch.equal(dv.cpu(), st["exp_avg_sq"])
+    # p: the same formula and order; torch's vectorised CPU sqrt / division
+    # round a rare element (3 of 4099 at step 1) the other way from the
+    # correctly rounded ones here, so p may differ by one rounding of the
+    # update: within 2 ulp of the operands' scale max(|p0|, |p|)
+    pg, pt = dp.cpu().double(), prm.detach().double()
+    scale = torch.maximum(p0.double().abs(), pt.abs())
+    assert bool(((pg - pt).abs() <= scale * 2.0 ** -22).all())
+    assert float((pg == pt).double().mean()) >= 0.995
+    assert torch.equal(shadow, dp.bfloat16())
+    # float64 evaluation of the same update
+    pd, gd, md, vd = (t.double() for t in (p0, g, m0, v0))
+    md = b1 * md + (1 - b1) * gd
+    vd = b2 * vd + (1 - b2) * gd * gd
+    pd = pd - step_size * md / (vd.sqrt() / bc2_sqrt + 1e-8)
+    assert float((dp.cpu().double() - pd).abs().max()) <= 1e-6 * float(pd.abs().max())
+    assert float((dm.cpu().double() - md).abs().max()) <= 1e-6 * float(md.abs().max())

@@ -61,16 +61,16 @@ def test_abi_constants_and_errors(lib):
 
 
 def test_tune_table_names_and_defaults(lib):
-    """_native.KNOB names exactly the knobs include/mmad.h documents (the
-    retired slot 15 is refused), and the table starts at the documented
+    """_native.KNOB names exactly the knobs include/mmad.h documents (a slot
+    past the table is refused), and the table starts at the documented
     defaults the benches rely on."""
     import ctypes
     from icra2021_multimodal_ad_amd._native import KNOB
-    assert sorted(KNOB.values()) == [k for k in range(32) if k != 15]
-    assert lib.mmad_tune_set(15, 0) == -1
+    assert sorted(KNOB.values()) == list(range(32))
+    assert lib.mmad_tune_set(32, 0) == -1
     v = ctypes.c_int()
     for name, want in (("dp_fork_rows", 1024), ("dp_bucket_mib", 8), ("dp_shard", 1), ("persist", 0),
-                       ("bn_apply_rb", 1), ("ev_on_kernel", 1)):
+                       ("bn_apply_rb", 1), ("ev_on_kernel", 1), ("side_cu_held", 0)):
         assert lib.mmad_tune_get(KNOB[name], ctypes.byref(v)) == 0
         assert v.value == want, (name, v.value)
 

@@ -41,8 +41,13 @@ for step in "$@"; do
     bench)
       timeout -k 10 400 python -u bench.py ${arg//,/ } > "$log" 2>&1 ;;
     prof)
-      # keep the --stats CSVs and a per-grid summary; the trace database stays on the box
-      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/${T}_${i}_prof -o run -- \
+      # keep the --stats CSVs and a per-grid summary; the trace database stays on the box.
+      # c5 replays one captured hipGraph per pass: rocprofiler-sdk's kernel-trace
+      # intercept faults on HIP's batched graph packets after some hundred replays
+      # (profiles/r10/r10a_c5_rocprof_segv/ANALYSIS.txt), so those graphs dispatch
+      # kernel by kernel under the profiler
+      pc=1; [[ "$arg" == *c5* ]] && pc=0
+      DEBUG_CLR_GRAPH_PACKET_CAPTURE=$pc timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/${T}_${i}_prof -o run -- \
         python3 bench.py ${arg//,/ } > "$log" 2>&1 &&
         mkdir -p gpurun_out/${T}_${i}_prof &&
         { find /tmp/${T}_${i}_prof -name "*stats*.csv" -exec cp {} gpurun_out/${T}_${i}_prof/ \; ; true; } &&
