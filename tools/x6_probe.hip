@@ -20,6 +20,8 @@
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef short shortx4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short ushortx8 __attribute__((ext_vector_type(8)));
 
 #define CK(x)                                                                  \
   do {                                                                         \
@@ -102,6 +104,117 @@ __global__ void gemm_probe(const float* A, const float* B, float* C, int M, int 
   // C/D: col = lane & 15, row = 4 * (lane >> 4) + i
 #pragma unroll
   for (int i = 0; i < 4; ++i) C[(size_t)(tm * 16 + 4 * g + i) * N + tn * 16 + r] = acc[i];
+}
+
+// the same with v_mfma_f32_16x16x32_bf16 (8 bf16 per lane: k = 8g..8g+7)
+// V = 3: two-way split (3 MFMAs per 16x16x32), V = 4: three-way (6 MFMAs)
+template <int V>
+__global__ void gemm_probe32(const float* A, const float* B, float* C, int M, int N, int K) {
+  const int lane = threadIdx.x;
+  const int tm = blockIdx.x / (N / 16), tn = blockIdx.x % (N / 16);
+  const int r = lane % 16, g = lane / 16;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += 32) {
+    ushortx8 ah, am, al, bh, bm, bl;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float a = A[(size_t)(tm * 16 + r) * K + k0 + 8 * g + i];
+      const float b = B[(size_t)(k0 + 8 * g + i) * N + tn * 16 + r];
+      short h, m, l;
+      split3(a, h, m, l);
+      ah[i] = h; am[i] = m; al[i] = l;
+      split3(b, h, m, l);
+      bh[i] = h; bm[i] = m; bl[i] = l;
+    }
+    auto mf = [&](ushortx8 x, ushortx8 y) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x), __builtin_bit_cast(bf16x8, y),
+                                                    acc, 0, 0, 0);
+    };
+    if (V == 3) {
+      ushortx8 alo, blo;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        alo[i] = bf16_rne(bf16_f(am[i]) + bf16_f(al[i]));
+        blo[i] = bf16_rne(bf16_f(bm[i]) + bf16_f(bl[i]));
+      }
+      mf(ah, blo);
+      mf(alo, bh);
+      mf(ah, bh);
+    } else {
+      mf(ah, bl);
+      mf(al, bh);
+      mf(am, bm);
+      mf(ah, bm);
+      mf(am, bh);
+      mf(ah, bh);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) C[(size_t)(tm * 16 + 4 * g + i) * N + tn * 16 + r] = acc[i];
+}
+
+// a 64x64 wave tile's inner step as the GEMM runs it: 4 A + 4 B fragments of
+// one 32-deep K step read from LDS as fp32, then 16 output fragments.
+//   V = 0: 8 x v_mfma_f32_16x16x4_f32 per output fragment (exact-f32 path)
+//   V = 3 / 4: split the 8 fragments once, then 3 / 6 x 16x16x32 bf16 each
+template <int V>
+__global__ __launch_bounds__(256) void inner_loop(float* out, int iters) {
+  __shared__ float lds[8][64][8];
+  const int lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < 8 * 64 * 8; i += 256) (&lds[0][0][0])[i] = (float)(i % 97) * 1e-3f - 0.04f;
+  __syncthreads();
+  floatx4 acc[4][4] = {};
+  for (int it = 0; it < iters; ++it) {
+    float f[8][8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) f[q][t] = lds[q][lane][(t + it) & 7];
+    if (V == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int s = 0; s < 8; ++s)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f[i][s], f[4 + j][s], acc[i][j], 0, 0, 0);
+    } else {
+      ushortx8 h[8], m[8], l[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          short a, b, c;
+          split3(f[q][t], a, b, c);
+          h[q][t] = a; m[q][t] = b; l[q][t] = c;
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          auto mf = [&](ushortx8 x, ushortx8 y) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x),
+                                                                __builtin_bit_cast(bf16x8, y), acc[i][j], 0, 0, 0);
+          };
+          if (V == 3) {
+            mf(h[i], m[4 + j]);
+            mf(m[i], h[4 + j]);
+            mf(h[i], h[4 + j]);
+          } else {
+            mf(h[i], l[4 + j]);
+            mf(l[i], h[4 + j]);
+            mf(m[i], m[4 + j]);
+            mf(h[i], m[4 + j]);
+            mf(m[i], h[4 + j]);
+            mf(h[i], h[4 + j]);
+          }
+        }
+    }
+  }
+  float s = 0.f;
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
 // MFMA issue cost: the same instruction mix with operands in registers
@@ -195,6 +308,41 @@ int main() {
     printf("%-32s max err %.3e  rms err %.3e  (rel. to sum|ab|; max |diff vs f32 path| %.3e)  "
            "MFMA loop %.2f ms = %.1f fp32-equivalent TFLOP/s\n",
            names[v], mx, rms, mx_vs_f32, ms, fl / (ms * 1e-3) / 1e12);
+  }
+  const char* n32[2] = {"x3 via 16x16x32", "x6 via 16x16x32"};
+  for (int v = 0; v < 2; ++v) {
+    const int tiles = (M / 16) * (N / 16);
+    if (v == 0) gemm_probe32<3><<<tiles, 64>>>(dA, dB, dC, M, N, K);
+    else gemm_probe32<4><<<tiles, 64>>>(dA, dB, dC, M, N, K);
+    CK(hipGetLastError());
+    CK(hipMemcpy(C.data(), dC, C.size() * 4, hipMemcpyDeviceToHost));
+    double mx = 0, rms = 0;
+    for (size_t i = 0; i < C.size(); ++i) {
+      const double e = fabs((double)C[i] - ref[i]) / mag[i];
+      mx = e > mx ? e : mx;
+      rms += e * e;
+    }
+    printf("%-32s max err %.3e  rms err %.3e\n", n32[v], mx, sqrt(rms / C.size()));
+  }
+  // inner-loop timing: 1024 blocks x 4 waves, 64x64 wave tile, 32-deep K steps
+  const char* nl[3] = {"inner f32 (8 x 16x16x4 / frag)", "inner x3 (split + 3 x 16x16x32)", "inner x6 (split + 6 x 16x16x32)"};
+  for (int v = 0; v < 3; ++v) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int iters = 400;
+    float ms = 0;
+    for (int rep = 0; rep < 2; ++rep) {
+      CK(hipEventRecord(e0));
+      if (v == 0) inner_loop<0><<<1024, 256>>>(dO, iters);
+      if (v == 1) inner_loop<3><<<1024, 256>>>(dO, iters);
+      if (v == 2) inner_loop<4><<<1024, 256>>>(dO, iters);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&ms, e0, e1));
+    }
+    const double fl = 1024.0 * 4 * iters * 16 * (16 * 16 * 32 * 2.0);
+    printf("%-34s %.2f ms = %.1f fp32-equivalent TFLOP/s\n", nl[v], ms, fl / (ms * 1e-3) / 1e12);
   }
   return 0;
 }
