@@ -1219,6 +1219,31 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
           for (int r = 0; r < 4; ++r) acc[i][j][r] = apply_act(acc[i][j][r] + ebias[j], ep.act, ep.slope);
     }
   }
+  // MSE: every target value of this lane's accumulators loaded up front, all
+  // in flight together (issued inside the loop below they went out a column
+  // fragment at a time, one HBM round trip each); the fragment registers of
+  // the finished K loop hold them.  Same values, same arithmetic.  c3's MSE
+  // GEMM (4096 x 1658 -> 2048) 51.2 -> 39.9 us on its tile, c2's 18.9 -> 16.0
+  // (profiles/r10/r10h_mse_target_prefetch_ab.jsonl).  bf16 only: the fp32
+  // tiles would spill.
+  constexpr bool TPF = EPI == GEMM_EPI_MSE && sizeof(T) == 2 && TM * TN <= 16;
+  float tpf[TPF ? TN : 1][TPF ? TM : 1][4];
+  if constexpr (TPF) {
+    int trow[TM][4];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) trow[i][r] = (rw + i * 16 + 4 * g + r) % ep.tmod;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = cw + j * 16 + c;
+      const int cc = col < ep.N ? col : ep.N - 1;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tpf[j][i][r] = tgt[(size_t)trow[i][r] * ep.ldt + cc];
+    }
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = cw + j * 16 + c;
@@ -1250,7 +1275,8 @@ __device__ __forceinline__ void gemm_body(const T* __restrict__ A, int lda, cons
           // unconditional load at a clamped column (row % tmod is always a
           // target row): a load guarded per element makes hipcc branch around
           // each one and wait for it, one round trip per element
-          const float tv = tgt[(size_t)(row % ep.tmod) * ep.ldt + (col < ep.N ? col : ep.N - 1)];
+          const float tv = TPF ? tpf[TPF ? j : 0][TPF ? i : 0][r]
+                               : tgt[(size_t)(row % ep.tmod) * ep.ldt + (col < ep.N ? col : ep.N - 1)];
           const float d = valid ? v + bias - tv : 0.f;
           v = ep.gscale * d;
           s1[i >> 1] += v;
