@@ -179,9 +179,9 @@ __global__ __launch_bounds__(64) void bn_finalize_k(int M, int N, int Np, const 
 }
 
 // Finalize + fold.  Block (kb, nb): the 64 producer columns k0..k0+63 (its
-// Welford merge is recomputed per n-block: 16 KB of L2 reads) and the
+// statistics merge is recomputed per n-block: 16 KB of L2 reads) and the
 // 64 * FOLD_RPT consumer rows n0.. of W.  Merge order: 4 chunk groups
-// (g, g+4, ...) each sequential, then groups 0..3 in order.
+// (g, g+4, ...) each sequential, then ((g0 + g1) + g2) + g3.
 template <typename TW, int FOLD_RPT>
 __global__ __launch_bounds__(256) void bn_fold_k(int M, int N, int Np, const float* __restrict__ stats,
                                                  int nparts, const float* __restrict__ gamma,
@@ -206,8 +206,16 @@ __global__ __launch_bounds__(256) void bn_fold_k(int M, int N, int Np, const flo
     for (int u = 0; u < 4; ++u)
       wv[i][u] = *(const floatx4*)(W + (size_t)(n0 + r + 64 * i) * Np + k0 + cq + 4 * u);
   {
+    // shifted sums about chunk 0's mean K (no division in the chain: the
+    // pairwise Welford update it replaced held a dependent fp64 division per
+    // chunk, ~4.6 us of a 4096-row fold, tools/fold_probe.py):
+    //   S1 = sum n_i (mean_i - K),  S2 = sum [M2_i + n_i (mean_i - K)^2],
+    //   mean = K + S1 / n,  M2 = S2 - S1^2 / n
+    // (K is within ~std/sqrt(32) of the batch mean, so S1^2 / n stays a few
+    // per cent of S2: no cancellation to speak of in fp64)
     const int c = tid & 63, grp = tid >> 6;
-    double n = 0.0, mean = 0.0, m2 = 0.0;
+    const double K = stats[k0 + c];
+    double n = 0.0, s1 = 0.0, s2 = 0.0;
     for (int i0 = grp; i0 < nparts; i0 += 4 * U) {
       float mb[U], qb[U];
 #pragma unroll
@@ -222,28 +230,24 @@ __global__ __launch_bounds__(256) void bn_fold_k(int M, int N, int Np, const flo
         int cnt = M - i * MMAD_PART_ROWS;
         cnt = cnt < 0 ? 0 : (cnt > MMAD_PART_ROWS ? MMAD_PART_ROWS : cnt);
         if (i >= nparts || cnt == 0) continue;
-        const double nb = (double)cnt, nn = n + nb, d = (double)mb[u] - mean;
-        mean += d * (nb / nn);
-        m2 += (double)qb[u] + d * d * (n * nb / nn);
-        n = nn;
+        const double nb = (double)cnt, d = (double)mb[u] - K;
+        n += nb;
+        s1 = fma(nb, d, s1);
+        s2 += fma(nb * d, d, (double)qb[u]);
       }
     }
-    pm[grp][c] = mean;
-    pq[grp][c] = m2;
+    pm[grp][c] = s1;
+    pq[grp][c] = s2;
     pn[grp][c] = n;
   }
   __syncthreads();
   if (tid < 64) {
-    double n1 = 0.0, mud = 0.0, q = 0.0;
-#pragma unroll
-    for (int gq = 0; gq < 4; ++gq) {
-      const double nb = pn[gq][tid];
-      if (nb == 0.0) continue;
-      const double nn = n1 + nb, d = pm[gq][tid] - mud;
-      mud += d * (nb / nn);
-      q += pq[gq][tid] + d * d * (n1 * nb / nn);
-      n1 = nn;
-    }
+    const double n1 = ((pn[0][tid] + pn[1][tid]) + pn[2][tid]) + pn[3][tid];
+    const double t1 = ((pm[0][tid] + pm[1][tid]) + pm[2][tid]) + pm[3][tid];
+    const double t2 = ((pq[0][tid] + pq[1][tid]) + pq[2][tid]) + pq[3][tid];
+    const double K = stats[k0 + tid];
+    const double mud = n1 > 0.0 ? K + t1 / n1 : 0.0;
+    const double q = n1 > 0.0 ? fmax(t2 - t1 * (t1 / n1), 0.0) : 0.0;
     const float mu = (float)mud;
     const float var = n1 > 0.0 ? (float)(q / n1) : 0.f;
     const int col = k0 + tid;

@@ -161,3 +161,40 @@ def test_fold_forward_fused_backward_c3_vib(monkeypatch):
         assert abs(la - lb) <= 1e-2 * abs(lb), (s, la, lb)
     ma._native.check_status()
     mb._native.check_status()
+
+
+@pytest.mark.parametrize("rows", [4096, 4000])
+def test_fold_batch_statistics_match_fp64(rows):
+    """bn_fold_k's statistics merge (the bf16 schedule above 2048 rows: shifted
+    sums of the producer epilogue's per-32-row Welford partials): after one
+    train-mode forward, layer 0's running mean / var equal the momentum
+    update with the fp64 mean / unbiased variance of layer 0's activation,
+    recomputed in fp64 from the same bf16 operands (packed input, weight
+    shadow) -- the GEMM's fp32 accumulation aside: within 1e-5 of the
+    statistics' scale.  4000 rows: a ragged last 32-row chunk (padding rows
+    masked out of the partials)."""
+    import types
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    cfg = types.SimpleNamespace(input_size=2048, btl_size=100, n_layers=5, gpu_id=0, dtype="bf16",
+                                models="ae")
+    torch.manual_seed(21)
+    m = get_model(cfg)
+    nat = m._native
+    nat.sync_shadow(force=True)
+    x = torch.from_numpy(synth_windows(rows, 2048, seed=5)).cuda()
+    nat.forward(x, train_bn=True, want_xhat=False)
+    torch.cuda.synchronize()
+    nat.check_status()
+    L = nat.layers[0]
+    w = nat.shadow[L["w_off"]:L["w_off"] + L["Np"] * L["Kp"]].view(L["Np"], L["Kp"])[:L["N"], :L["K"]]
+    b = nat.params[L["b_off"]:L["b_off"] + L["N"]]
+    a = x.bfloat16().double() @ w.double().t() + b.double()
+    a = torch.where(a > 0, a, 0.2 * a)
+    mean = a.mean(0)
+    var_u = a.var(0, unbiased=True)
+    rm, rv = nat.running_views(0)
+    mom = nat.bn_momentum
+    want_m = mom * mean
+    want_v = (1 - mom) * 1.0 + mom * var_u
+    assert float((rm.double() - want_m).abs().max()) <= 1e-5 * float(want_m.abs().max())
+    assert float((rv.double() - want_v).abs().max()) <= 1e-5 * float(want_v.abs().max())

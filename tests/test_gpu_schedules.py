@@ -1,5 +1,5 @@
 """Fused-step schedule variants give the same bits as the default schedule:
-every schedule knob of the tune table (include/mmad.h knobs 19-26, read when
+every schedule knob of the tune table (include/mmad.h knobs 15, 19-31, read when
 a model handle is created) and the host-side shadow pair only reorder
 independent work across streams."""
 import pytest
@@ -14,12 +14,14 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("knobs", [
     {"ev_every": 1}, {"ev_every": 3}, {"loss_side": 0}, {"dw_main": 1}, {"dw_main": 3},
     {"pair_rows": 0}, {"pair_rows": 0, "dw_main_ping": 0}, {"shadow_pair": False},
-    {"side_prio": 1}, {"event_sysfence": 1}, {"keep_grads": 1}, {"ev_on_kernel": 0}])
+    {"side_prio": 1}, {"event_sysfence": 1}, {"keep_grads": 1}, {"ev_on_kernel": 0},
+    {"side_cu_held": 32}])
 def test_schedule_knobs_match_default(knobs):
     """Every schedule knob of the fused step only reorders independent work
     across streams (event coalescing, where the loss is reduced, how many dW
     GEMMs run on the main stream, ping-pong shadows, stream priority, event
-    fences, a materialised dW, hand-off events on the launch or behind it): parameters, Adam moments, BN statistics, the
+    fences, a materialised dW, hand-off events on the launch or behind it, a
+    CU-masked side stream): parameters, Adam moments, BN statistics, the
     current bf16 shadow and the losses equal the default schedule's bit for
     bit."""
     import types

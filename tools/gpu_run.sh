@@ -2,7 +2,7 @@
 # Usage on the box:  bash tools/gpu_run.sh <tag> <step> [<step> ...]
 # Steps (run in order; the first failure ends the call, no GPU step after it):
 #   tests            full `pytest -m gpu` suite
-#   tests:<expr>     `pytest -m gpu -k <expr>`
+#   tests:<expr>     `pytest -m gpu -k <expr>` ('+' -> ' ', e.g. tests:bn_fused+or+dp)
 #   smoke            __graft_entry__.smoke()
 #   bench[:<args>]   python bench.py <args, commas -> spaces>
 #   prof[:<args>]    rocprofv3 --kernel-trace --stats of bench.py <args>
@@ -32,7 +32,7 @@ for step in "$@"; do
   case "$kind" in
     tests)
       if [ -n "$arg" ]; then
-        timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf -k "$arg" --timeout 300 --timeout-method thread > "$log" 2>&1
+        timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf -k "${arg//+/ }" --timeout 300 --timeout-method thread > "$log" 2>&1
       else
         timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf --timeout 300 --timeout-method thread > "$log" 2>&1
       fi ;;
