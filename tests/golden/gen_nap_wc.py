@@ -55,21 +55,10 @@ import torch  # noqa: E402
 from icra2021_multimodal_ad_amd.common_utils import init_state_dict  # noqa: E402
 from icra2021_multimodal_ad_amd.data_loaders import get_loaders  # noqa: E402
 
-NAPWC = dict(input_size=256, btl_size=20, n_layers=5, batch_size=500, n_epochs=10,
-             n_normal=10000, n_novelty=1000, anomaly_strength=0.7, data="hsr_objectdrop",
-             target_class=1, unimodal_normal=False, novelty_ratio=0.0, start_layer_index=0,
-             end_layer_index=-1, sensor="All", verbose=0)
-SEEDS = (0, 1, 2)
+sys.path.insert(0, HERE)
+from napwc_config import NAPWC, SEEDS, config_for  # noqa: E402,F401  (the fixtures' configuration)
+
 MIN_VAR_RATIO = 1e-6
-
-
-def config_for(seed):
-    c = types.SimpleNamespace(**NAPWC)
-    c.gpu_id = -1
-    c.data_seed = 500 + seed
-    c.sampler_seed = 600 + seed
-    c.model_seed = 700 + seed
-    return c
 
 
 def ema_update(v, x, alpha=0.98):

@@ -45,7 +45,7 @@ sys.path.insert(2, HERE)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from gen_nap_wc import config_for  # noqa: E402
+from napwc_config import config_for  # noqa: E402
 from icra2021_multimodal_ad_amd.common_utils import init_state_dict  # noqa: E402
 from icra2021_multimodal_ad_amd.data_loaders import get_loaders  # noqa: E402
 

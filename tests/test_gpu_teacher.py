@@ -35,7 +35,7 @@ FLOOR = 2.0 ** -22
 def _cfg():
     import sys
     sys.path.insert(0, os.path.join(HERE, "golden"))
-    from gen_nap_wc import config_for    # the configuration only (no reference import)
+    from napwc_config import config_for    # plain configuration data (no reference import)
     return config_for(0)
 
 

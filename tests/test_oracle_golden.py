@@ -243,7 +243,7 @@ def test_teacher_forced_oracle_step_within_reference_band(golden):
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
-    from gen_nap_wc import config_for
+    from napwc_config import config_for
     from icra2021_multimodal_ad_amd.data_loaders import get_loaders
     g = golden("teacher")
     cfg = config_for(int(g["meta/seed"]))
