@@ -259,11 +259,13 @@ static size_t esz(int dtype) { return dtype == MMAD_BF16 ? 2 : 4; }
 
 // can the dispatcher choose a split-K factor > 1 for this handle's GEMMs?
 // (any dtype: a forced override, knob 4; bf16: the dW rule, when a dW
-// override or the dW split target is set -- by default nothing splits)
+// override or the dW split target is set; fp32: knob 32's dW rule -- by
+// default nothing splits)
 static bool splitk_possible(int dtype) {
   const int o = mmad_splitk_override();
   if (o > 1) return true;
-  if (o == 1 || dtype != MMAD_BF16) return false;
+  if (o == 1) return false;
+  if (dtype != MMAD_BF16) return mmad_splitk_dw_f32_blocks() > 0;
   return mmad_splitk_dw_override() > 1 || mmad_splitk_dw_blocks() > 0;
 }
 

@@ -68,6 +68,7 @@ int g_knob[MMAD_KNOB_COUNT] = {
     0,     // 29 schedule study: hold every side-stream dW + Adam until the bwd-data chain is enqueued
     8,     // 30 DP: minimum exchange bucket (MiB of fp32 gradient; consecutive layers merge)
     1,     // 31 bwd-data hand-off events completed by the GEMM launch (hipExtLaunchKernel)
+    1024,  // 32 fp32 dW split rule from 2048 rows: target 64x64-tile blocks (0 = no split)
 };
 }  // namespace
 int mmad_knob(int k) { return g_knob[k]; }
@@ -83,6 +84,7 @@ int mmad_splitk_dw_override() { return g_knob[9]; }
 // (VIB B=4096 0.991-0.996 vs 1.013 ms/step with the split tail off; r02ae_*)
 int mmad_splitk_dw_blocks() { return g_knob[10]; }
 int mmad_splitk_dw_min_stages() { return g_knob[11]; }
+int mmad_splitk_dw_f32_blocks() { return g_knob[32]; }
 // tile for the dW GEMMs with the fused Adam epilogue (the autotuner times
 // them without Adam, which under-weights the epilogue's HBM traffic: it picks
 // 128x128 for the large layers, 208 blocks for 256 CUs).  Default (-2) = a

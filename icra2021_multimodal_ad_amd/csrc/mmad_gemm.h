@@ -132,6 +132,7 @@ int mmad_splitk_override();   // 0 = shape rule; 1, 2, 4, 8, 16 = forced split f
 int mmad_splitk_dw_override();     // the same for the dW GEMMs only (knob 9)
 int mmad_splitk_dw_blocks();       // dW split rule: target 64x64-tile blocks (knob 10)
 int mmad_splitk_dw_min_stages();   // dW split rule: minimum K stages per slice (knob 11)
+int mmad_splitk_dw_f32_blocks();   // fp32 dW split rule from 2048 rows: target blocks (knob 32)
 int mmad_tile_adam_override();  // >= 0: tile of the Adam-fused dW GEMMs (-2: shape rule)
 int mmad_tile_adam_for(int Mp, int Np, int K);   // ... for a shape
 int mmad_tile_adam_main_override();  // >= 0: ... of those on the main stream

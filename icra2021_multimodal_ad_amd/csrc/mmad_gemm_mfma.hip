@@ -2379,8 +2379,18 @@ int mmad_gemm_splitk(int Mp, int Np, int K, int dtype, int epi) {
   // the exact-fp32 parity path keeps one sequential K order per output (the
   // order closest to the reference's; a different fp32 order can flip the
   // LeakyReLU branch of a pre-activation at rounding level, e.g. 5.6e-7 in
-  // tests/golden/mm192.npz); split-K is the bf16 performance path's
-  if (dtype != MMAD_BF16) return 1;
+  // tests/golden/mm192.npz); split-K is the bf16 performance path's -- except,
+  // behind knob 32, the fp32 dW GEMMs of large batches: a gradient feeds no
+  // branch, and contracting over >= 2048 rows the narrow layers' few 64x64
+  // tiles run one f32-MFMA K loop each at 1/16 of the bf16 rate
+  if (dtype != MMAD_BF16) {
+    const int target = mmad_splitk_dw_f32_blocks();
+    if (epi != GEMM_EPI_BWD_WEIGHT || target <= 0 || K < 2048) return 1;
+    int best = 1;
+    for (int S = 2; S <= 16; S *= 2)
+      if (ok(S) && t64 * S <= target && K / S >= 16 * bk) best = S;
+    return best;
+  }
   if (epi == GEMM_EPI_BWD_WEIGHT) {
     const int envw = mmad_splitk_dw_override();
     if (valid(envw)) return ok(envw) ? envw : 1;

@@ -99,8 +99,11 @@ int mmad_pad_granule(void);
  *      much (8; 0 = one bucket per layer)
  *   31 the bwd-data GEMM's hand-off event to the side stream completed by the
  *      launch itself (hipExtLaunchKernel stop event, 1) or recorded behind it
- *      (0: a marker packet that holds the main stream's next dispatch) */
-#define MMAD_KNOB_COUNT 32
+ *      (0: a marker packet that holds the main stream's next dispatch)
+ *   32 exact-fp32 dW GEMMs contracting over >= 2048 rows: split K until the
+ *      launch has about this many 64x64-tile blocks, >= 16 K stages per
+ *      slice (1024; 0 = never split an fp32 GEMM) */
+#define MMAD_KNOB_COUNT 33
 int mmad_tune_set(int knob, int value);
 int mmad_tune_get(int knob, int* value);
 /* The split-K factor the dispatcher picks for a padded GEMM shape (Mp x Np

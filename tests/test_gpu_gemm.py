@@ -318,3 +318,60 @@ def test_register_direct_tile_bit_identical(case, N):
     for tile in (7, 8, 1, 2, 9):
         for a, b2 in zip(outs[6], outs[tile]):
             assert torch.equal(a, b2), (case, tile)
+
+
+@pytest.mark.parametrize("blocks", [256, 512])
+def test_f32_dw_split_rule_fused_step(blocks):
+    """Knob 32 (the exact-fp32 path's dW split-K rule from 2048 rows) at the
+    C3 shape through the fused step (dW with the Adam epilogue run by the
+    last arriving slice): every split dW layer's slices combined in split
+    order -- repeat runs identical bit for bit -- and the step equal to the
+    unsplit one to fp32 accumulation order after the first step: loss within
+    1e-6, Adam moments within 1e-5 of their scale, parameters within 1e-6 but for
+    sign-of-zero gradient entries (<= 1e-4 of them); forward-type GEMMs and
+    batches below 2048 rows never split."""
+    import types
+    from icra2021_multimodal_ad_amd.model_builder import get_model
+    from icra2021_multimodal_ad_amd.data import synth_windows
+    lib = _native.load()
+    with _native.tune(splitk_dw_f32_blocks=0):
+        assert lib.mmad_gemm_splitk_for(512, 128, 4096, F32, 3) == 1      # knob off: no split
+    xs = [torch.from_numpy(synth_windows(4096, 2048, seed=30 + i)).cuda() for i in range(2)]
+    eps = torch.randn(1, 4096, 100, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1))
+    res = []
+    for knob in (0, blocks, blocks):
+        with _native.tune(splitk_dw_f32_blocks=knob):
+            if knob:
+                assert lib.mmad_gemm_splitk_for(512, 128, 4096, F32, 3) > 1   # L5's dW: [512 x 128], K 4096
+                assert lib.mmad_gemm_splitk_for(512, 128, 1024, F32, 3) == 1  # below 2048 rows
+                assert lib.mmad_gemm_splitk_for(4096, 128, 512, F32, 0) == 1  # forward
+            cfg = types.SimpleNamespace(input_size=2048, btl_size=100, n_layers=5, gpu_id=0, dtype="f32",
+                                        models="vib_ae", vib_k=1, beta_kl=1.0)
+            torch.manual_seed(33)
+            m = get_model(cfg)
+            nat = m._native
+            run = []
+            for x in xs:
+                loss = float(nat.train_step_fused(x, k=1, eps=eps, beta_kl=1.0))
+                torch.cuda.synchronize()
+                run.append((loss, nat.params.clone(), nat.exp_avg.clone(), nat.exp_avg_sq.clone()))
+            nat.check_status()
+            res.append(run)
+    # the split schedule is reproducible bit for bit over both steps
+    for (la, pa, ma, va), (lb, pb, mb, vb) in zip(res[1], res[2]):
+        assert la == lb and torch.equal(pa, pb) and torch.equal(ma, mb) and torch.equal(va, vb)
+    # against the unsplit step: the first step (the second one's inputs
+    # already differ by the first one's sign-of-zero entries, below)
+    (l0, p0, m0, v0), (l1, p1, m1, v1) = res[0][0], res[1][0]
+    assert abs(l0 - l1) <= 1e-6 * abs(l0), (l0, l1)
+    # Adam's moments carry the gradient: a dW entry is a 4096-row sum whose
+    # terms may cancel, so another fp32 order moves it by ~2^-24 of the terms'
+    # magnitude, not of its own (measured 1.7e-6 of max|m|); the parity bar
+    # for fp32 gradients is 1e-4 of their max (test_gpu_parity)
+    for a, b in ((m0, m1), (v0, v1)):
+        assert float((a - b).abs().max()) <= 1e-5 * float(a.abs().max())
+    # parameters: Adam's first steps move each weight by ~lr * sign(g), so an
+    # entry whose gradient is zero to rounding may step the other way; all but
+    # such entries agree to fp32 accumulation order
+    far = (p0 - p1).abs() > 1e-6 * float(p0.abs().max())
+    assert float(far.double().mean()) <= 1e-4, int(far.sum())
