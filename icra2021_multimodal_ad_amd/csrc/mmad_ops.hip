@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <system_error>
+#include <type_traits>
 
 #define SLAB_COLS 64
 #define SLAB_ROWS 128
@@ -431,47 +432,52 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
   }
   __syncthreads();
   // da = gamma rstd / M (M dy - sum dy - xhat sum dy xhat): the bracket nearly
-  // cancels, so it is evaluated in fp64 (as the reference's CPU BatchNorm
-  // backward does its reductions); dz and its column sums follow in fp64 too
-  const double invM = 1.0 / (double)M;
-  double cf[V], dbv[V], dgv[V];
+  // cancels, so on the exact-fp32 path it is evaluated in fp64 (as the
+  // reference's CPU BatchNorm backward does its reductions), dz and its column
+  // sums too.  The bf16 path (this kernel runs there from 2048 rows, c3 / c4)
+  // rounds dz to 8 bits: its bracket in fp32 (M * dy exact, M a power of two
+  // at the bench shapes; the column sums rounded once), which halves the
+  // kernel's registers and doubles its waves per SIMD -- a 4096-row apply ran
+  // at 2.2-2.5 TB/s with the fp64 bracket (tools/apply_probe.py)
+  using CT = std::conditional_t<sizeof(T) == 2, float, double>;
+  const CT invM = (CT)1 / (CT)M;
+  CT cf[V], dbv[V], dgv[V];
 #pragma unroll
   for (int k = 0; k < V; ++k) {
     const int col = n0 + ch * V + k;
-    cf[k] = col < N ? (double)gm[k] * (double)rs[k] * invM : 0.0;
-    dbv[k] = s_p1[0][ch * V + k];
-    dgv[k] = s_p2[0][ch * V + k];
+    cf[k] = col < N ? (CT)gm[k] * (CT)rs[k] * invM : (CT)0;
+    dbv[k] = (CT)s_p1[0][ch * V + k];
+    dgv[k] = (CT)s_p2[0][ch * V + k];
   }
   for (int sb = 0; sb < RB; ++sb) {
     const int slab = blockIdx.y * RB + sb;
     const int r0 = slab * SLAB_ROWS;
-    uint4v ro[RPT];
-    double accb[V];
+    CT accb[V];
 #pragma unroll
-    for (int k = 0; k < V; ++k) accb[k] = 0.0;
+    for (int k = 0; k < V; ++k) accb[k] = (CT)0;
 #pragma unroll
     for (int i = 0; i < RPT; ++i) {
       const int row = r0 + rg + i * RG;
       const T* pd = (const T*)&rd[i];
       const T* pa = (const T*)&ra[i];
-      T* po = (T*)&ro[i];
+      T* po = (T*)&rd[i];      // dz over dy in place: element k is read before it is written
 #pragma unroll
       for (int k = 0; k < V; ++k) {
         const float av = to_f32<T>(pa[k]);
-        const double xh = ((double)av - (double)mu[k]) * (double)rs[k];
-        const double da = cf[k] * ((double)M * (double)to_f32<T>(pd[k]) - dbv[k] - xh * dgv[k]);
-        float d = (float)(da * (double)act_grad_from_out(av, act, slope));
+        const CT xh = ((CT)av - (CT)mu[k]) * (CT)rs[k];
+        const CT da = cf[k] * ((CT)M * (CT)to_f32<T>(pd[k]) - dbv[k] - xh * dgv[k]);
+        float d = (float)(da * (CT)act_grad_from_out(av, act, slope));
         d = row < M ? d : 0.f;
         const T dt = from_f32<T>(d);
         po[k] = dt;
-        accb[k] += (double)to_f32<T>(dt);
+        accb[k] += (CT)to_f32<T>(dt);
       }
     }
-    // the next slab's rows load under this slab's stores and reduction
-    if (sb + 1 < RB) load_slab(slab + 1);
 #pragma unroll
     for (int i = 0; i < RPT; ++i)
-      *(uint4v*)(dz + (size_t)(r0 + rg + i * RG) * Np + n0 + ch * V) = ro[i];
+      *(uint4v*)(dz + (size_t)(r0 + rg + i * RG) * Np + n0 + ch * V) = rd[i];
+    // the next slab's rows load under this slab's reduction
+    if (sb + 1 < RB) load_slab(slab + 1);
 #pragma unroll
     for (int k = 0; k < V; ++k) s_red[rg][ch * V + k] = accb[k];
     __syncthreads();
