@@ -109,6 +109,10 @@ struct mmad_ae {
   // main stream has enqueued the whole bwd-data chain (ev_hold), to separate
   // the chain's in-step contention from its barrier costs
   int side_hold = 0;
+  // knob 33 (ping-pong steps): the side-stream dW + Adam GEMMs of the top
+  // dw_late layers fork behind the layer's bwd-data + BN apply instead of at
+  // its dz, so the largest dW does not share the CUs with the apply below it
+  int dw_late = 0;
   hipEvent_t ev_hold = nullptr;
   // fused step: dW GEMMs of layers < dw_main run on the caller's stream
   // (knob 19; tools/sched_sweep.py: 0.499 ms (2) vs 0.512 (1) vs 0.523 (3));
@@ -405,6 +409,7 @@ int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, i
     h->side_cu_held = mmad_knob(15);
     h->dp_shard = mmad_knob(28);
     h->side_hold = mmad_knob(29);
+    h->dw_late = mmad_knob(33);
     h->dp_bucket_mib = mmad_knob(30) < 0 ? 0 : mmad_knob(30);
     h->dp_fork_rows = mmad_knob(14);
     h->ev_flags_ = ev_flags(mmad_knob(27));
@@ -880,7 +885,8 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     // ping-pong shadows (bf16): the fused Adam of dW_l writes the other
     // shadow, so dW_l may start as soon as dz_l is complete
     const bool ping = adam && !dp && w.ping && l >= w.dw_main;
-    if (ping) {
+    const bool late = ping && l >= nL - h->dw_late;
+    if (ping && !late) {
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
     }
     // does the main stream record ev_data[l] (bwd-data of l done)?  Needed by
@@ -1075,6 +1081,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       } else if (h->side_hold) {
         pending.push_back(PendingDW{dz, in, a.Np, a.Kp, a.Np, a.Kp, Mp, dwe, l});
       } else if (ping) {
+        if (late) MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
         MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
                        nullptr, PROBE_DW + l));

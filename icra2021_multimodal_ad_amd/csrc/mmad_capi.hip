@@ -49,7 +49,7 @@ int g_knob[MMAD_KNOB_COUNT] = {
     0,     // 10 dW split rule: target 64x64-tile blocks (0 = no split)
     8,     // 11 dW split rule: minimum K stages per slice
     0,     // 12 persistent grid for forward-type GEMMs (0 off; else when the tiles exceed one round)
-    1,     // 13 BN-backward apply: 128-row slabs per block (1, 2, 4)
+    2,     // 13 BN-backward apply: 128-row slabs per block (1, 2, 4)
     1024,  // 14 DP: per-layer dW fork from this many padded rows (0 = one fork per bucket)
     0,     // 15 side stream behind a CU mask holding this many CUs for the main stream (0 = off)
     -1,    // 16 train-mode BN schedule (-1 = dtype default: bf16 fused, fp32 apply; 0 apply, 1 fold, 2 fused)
@@ -69,6 +69,7 @@ int g_knob[MMAD_KNOB_COUNT] = {
     8,     // 30 DP: minimum exchange bucket (MiB of fp32 gradient; consecutive layers merge)
     1,     // 31 bwd-data hand-off events completed by the GEMM launch (hipExtLaunchKernel)
     1024,  // 32 fp32 dW split rule from 2048 rows: target 64x64-tile blocks (0 = no split)
+    0,     // 33 ping-pong: the top n layers' side dW forks after their bwd-data + apply
 };
 }  // namespace
 int mmad_knob(int k) { return g_knob[k]; }

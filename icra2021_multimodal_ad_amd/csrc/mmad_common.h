@@ -90,14 +90,14 @@ __device__ __forceinline__ float apply_act_pw(float z, bool relu, float lo_slope
 }
 // derivative expressed through the activation OUTPUT a (all supported acts
 // are monotone so the output determines the branch / value)
+// (act is uniform: selects instead of a switch, so an unrolled per-element
+// loop stays one straight-line block instead of a branch chain per element)
 __device__ __forceinline__ float act_grad_from_out(float a, int act, float slope) {
-  switch (act) {
-    case MMAD_ACT_LEAKYRELU: return a > 0.f ? 1.f : slope;
-    case MMAD_ACT_RELU: return a > 0.f ? 1.f : 0.f;
-    case MMAD_ACT_SIGMOID: return a * (1.f - a);
-    case MMAD_ACT_TANH: return 1.f - a * a;
-    default: return 1.f;
-  }
+  const bool step = act == MMAD_ACT_LEAKYRELU || act == MMAD_ACT_RELU;
+  const float neg = act == MMAD_ACT_LEAKYRELU ? slope : 0.f;
+  float g = act == MMAD_ACT_SIGMOID ? a * (1.f - a) : 1.f;
+  g = act == MMAD_ACT_TANH ? 1.f - a * a : g;
+  return step ? (a > 0.f ? 1.f : neg) : g;
 }
 
 // torch.optim.Adam element update, as torch's _single_tensor_adam computes it

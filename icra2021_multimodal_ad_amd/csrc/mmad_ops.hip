@@ -359,9 +359,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_k(int M, int Np, const T* _
 // constants, the partials) are issued before any use, so the block's first
 // slab costs one memory round trip; each later slab's dy / a are loaded
 // under the previous slab's arithmetic.  Per slab the same arithmetic and
-// the same db-partial order as RB = 1 (bit-identical for every RB).
-template <typename T, int PU, int RB>
-__global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int M, int N, int Np,
+// the same db-partial order as RB = 1 (bit-identical for every RB).  LK: the
+// activation is LeakyReLU (the AE's), known at compile time -- with a run-time
+// act the per-element switch stays inside the unrolled loop, 32 branch chains
+// per row group and slab
+template <typename T, int PU, int RB, bool LK>
+__global__ __launch_bounds__(256) void bn_bwd_apply_k(int act_rt, float slope, int M, int N, int Np,
                                                       int nparts, const T* __restrict__ dy,
                                                       const T* __restrict__ a,
                                                       const float* __restrict__ mean,
@@ -374,6 +377,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
   constexpr int CPR = SLAB_COLS / V;      // threads per row
   constexpr int RG = 256 / CPR;           // row groups
   constexpr int RPT = SLAB_ROWS / RG;     // rows per thread and slab
+  const int act = LK ? (int)MMAD_ACT_LEAKYRELU : act_rt;
   // PU: partial chunks per group loaded at once (16 from 2048 rows: one round
   // trip for all of a 4096-row batch's 64 chunks; same summation order)
   __shared__ double s_red[RG][SLAB_COLS];
@@ -392,16 +396,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
     }
   };
   load_slab(blockIdx.y * RB);
-  // (2) column constants
-  float mu[V], rs[V], gm[V];
-#pragma unroll
-  for (int k = 0; k < V; k += 4) {
-    const int col = n0 + ch * V + k;
-    *(floatx4*)&mu[k] = *(const floatx4*)(mean + col);
-    *(floatx4*)&rs[k] = *(const floatx4*)(rstd + col);
-    *(floatx4*)&gm[k] = *(const floatx4*)(gamma + col);
-  }
-  // (3) partial sums: 4 groups of 64 columns, group g sums chunks g, g+4, ...
+  // (2) partial sums: 4 groups of 64 columns, group g sums chunks g, g+4, ...
   {
     const int c = tid & 63, grp = tid >> 6;
     double t1 = 0.0, t2 = 0.0;
@@ -431,6 +426,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_k(int act, float slope, int 
     if (blockIdx.y == 0) { dbeta[col] = (float)t1; dgamma[col] = (float)t2; }
   }
   __syncthreads();
+  // (3) column constants (loaded after the partials: their registers are free by then)
+  float mu[V], rs[V], gm[V];
+#pragma unroll
+  for (int k = 0; k < V; k += 4) {
+    const int col = n0 + ch * V + k;
+    *(floatx4*)&mu[k] = *(const floatx4*)(mean + col);
+    *(floatx4*)&rs[k] = *(const floatx4*)(rstd + col);
+    *(floatx4*)&gm[k] = *(const floatx4*)(gamma + col);
+  }
   // da = gamma rstd / M (M dy - sum dy - xhat sum dy xhat): the bracket nearly
   // cancels, so on the exact-fp32 path it is evaluated in fp64 (as the
   // reference's CPU BatchNorm backward does its reductions), dz and its column
@@ -1005,15 +1009,23 @@ int mmad_bn_act_bwd_apply(int dtype, int act, float slope, int M, int N, int Mp,
   dim3 grd(Np / SLAB_COLS, Mp / (SLAB_ROWS * rb));
   hipStream_t s = (hipStream_t)stream;
   const bool wide = nparts > 4 * 8;   // 16 partial chunks per round trip (8 no faster, r02bj_*)
-#define MMAD_BNB(PU_, RB_)                                                                             \
-  if (dtype == MMAD_BF16)                                                                              \
-    bn_bwd_apply_k<bf16, PU_, RB_><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const bf16*)dy,  \
-                                                       (const bf16*)a, save_mean, save_rstd, gamma,    \
-                                                       part, (bf16*)dz, dgamma, dbeta, db_partials);   \
-  else                                                                                                 \
-    bn_bwd_apply_k<float, PU_, RB_><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const float*)dy, \
-                                                        (const float*)a, save_mean, save_rstd, gamma,  \
-                                                        part, (float*)dz, dgamma, dbeta, db_partials);
+  const bool lk = act == MMAD_ACT_LEAKYRELU;
+#define MMAD_BNB_T(T, PU_, RB_, LK_)                                                                   \
+  bn_bwd_apply_k<T, PU_, RB_, LK_><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const T*)dy,     \
+                                                       (const T*)a, save_mean, save_rstd, gamma, part, \
+                                                       (T*)dz, dgamma, dbeta, db_partials);
+#define MMAD_BNB(PU_, RB_)                   \
+  if (dtype == MMAD_BF16) {                  \
+    if (lk) {                                \
+      MMAD_BNB_T(bf16, PU_, RB_, true)       \
+    } else {                                 \
+      MMAD_BNB_T(bf16, PU_, RB_, false)      \
+    }                                        \
+  } else if (lk) {                           \
+    MMAD_BNB_T(float, PU_, RB_, true)        \
+  } else {                                   \
+    MMAD_BNB_T(float, PU_, RB_, false)       \
+  }
 #define MMAD_BNB_RB(PU_)      \
   if (rb == 4) {              \
     MMAD_BNB(PU_, 4)          \
@@ -1029,6 +1041,7 @@ int mmad_bn_act_bwd_apply(int dtype, int act, float slope, int M, int N, int Mp,
   }
 #undef MMAD_BNB_RB
 #undef MMAD_BNB
+#undef MMAD_BNB_T
   MMAD_LAUNCH_CHECK();
   return MMAD_OK;
 }
@@ -1048,13 +1061,13 @@ int mmad_bn_act_bwd(int dtype, int act, float slope, int M, int N, int Mp, int N
   if (dtype == MMAD_BF16) {
     bn_bwd_reduce_k<bf16><<<grd, 256, 0, s>>>(M, Np, (const bf16*)dy, (const bf16*)a, save_mean,
                                               save_rstd, part);
-    bn_bwd_apply_k<bf16, 8, 1><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const bf16*)dy,
+    bn_bwd_apply_k<bf16, 8, 1, false><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const bf16*)dy,
                                              (const bf16*)a, save_mean, save_rstd, gamma, part,
                                              (bf16*)dz, dgamma, dbeta, db_partials);
   } else {
     bn_bwd_reduce_k<float><<<grd, 256, 0, s>>>(M, Np, (const float*)dy, (const float*)a, save_mean,
                                                save_rstd, part);
-    bn_bwd_apply_k<float, 8, 1><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const float*)dy,
+    bn_bwd_apply_k<float, 8, 1, false><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const float*)dy,
                                               (const float*)a, save_mean, save_rstd, gamma, part,
                                               (float*)dz, dgamma, dbeta, db_partials);
   }

@@ -70,7 +70,7 @@ int mmad_pad_granule(void);
  *      launch)
  *   13 BN-backward apply kernel: 128-row slabs per block (1, 2 or 4; any other
  *      value = 1; halved until it divides the row slabs; the column partials
- *      are merged once per block)
+ *      are merged once per block; default 2)
  *   14 data parallel: from this many padded rows, each side-stream dW GEMM
  *      starts at its own dz instead of with its bucket's lowest layer (1024;
  *      0 = one fork per bucket)
@@ -102,8 +102,11 @@ int mmad_pad_granule(void);
  *      (0: a marker packet that holds the main stream's next dispatch)
  *   32 exact-fp32 dW GEMMs contracting over >= 2048 rows: split K until the
  *      launch has about this many 64x64-tile blocks, >= 16 K stages per
- *      slice (1024; 0 = never split an fp32 GEMM) */
-#define MMAD_KNOB_COUNT 33
+ *      slice (1024; 0 = never split an fp32 GEMM)
+ *   33 ping-pong steps: the side-stream dW + Adam GEMMs of the top this many
+ *      layers start once the main stream has also finished the layer's
+ *      bwd-data GEMM and BN-backward apply, instead of at its dz (0) */
+#define MMAD_KNOB_COUNT 34
 int mmad_tune_set(int knob, int value);
 int mmad_tune_get(int knob, int* value);
 /* The split-K factor the dispatcher picks for a padded GEMM shape (Mp x Np

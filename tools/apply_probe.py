@@ -61,5 +61,5 @@ for N in (enc[1], dec[4], enc[3]):          # 1678, 1658, 939 columns
         row[f"rb{rb}_us"] = round(t64, 2)
         row[f"rb{rb}_2parts_us"] = round(t2, 2)
         row[f"rb{rb}_tb_s"] = round(row["bytes"] / (t64 * 1e-6) / 1e12, 2)
-    lib.mmad_tune_set(13, 1)
+    lib.mmad_tune_set(13, 2)
     print(json.dumps(row), flush=True)
