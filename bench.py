@@ -29,9 +29,12 @@ barrier + synchronize pairs, the max over ranks; rank 0 prints ONE JSON line:
 * ``roofline``: the kernel that dominates the step -- the dW GEMM with the
   fused Adam epilogue of the largest layer, HBM-bound (26 B of Adam state per
   parameter + its two bf16 operands).  Its duration comes from the executor's
-  probe (mmad_ae_probe: a HIP event pair around that one launch, on the stream
-  it runs on) over eager steps of the same state right after the timed region
-  (the same state and inputs);  ``traffic`` =
+  probe inside the timed steps (mmad_ae_probe kind 3: start / stop events
+  attached to that one launch by hipExtLaunchKernel, no marker packet, no
+  wait for the side stream -- the launch as it runs beside the side stream's
+  work, what rocprofv3's kernel records of the same command show);
+  ``avg_us_isolated`` = the same launch alone, in eager steps right after the
+  timed region (kind 1);  ``traffic`` =
   PMC HBM bytes per launch from the newest matching profiles/*_pmc_dw.json.
 * ``roofline_encoder_gemm``: the encoder's first forward GEMM (the north-star
   MFMA target), launched back to back between one event pair.
@@ -263,9 +266,12 @@ def gemm_roofline(model, batch, iters=50):
     return res
 
 
-def dw_roofline(nat, layer, durations_ms, batch, steps_timed, fused_adam=True, layers=None):
+def dw_roofline(nat, layer, durations_ms, batch, steps_timed, fused_adam=True, layers=None,
+                in_timed=False, isolated_ms=None):
     """roofline of the dominant dW GEMM launch from the in-situ probe durations.
-    layers: the layers that launch covered (mmad_ae_probe_layers)."""
+    layers: the layers that launch covered (mmad_ae_probe_layers).  in_timed:
+    the durations are the timed steps' own launches (kernel-attached events);
+    isolated_ms: the same launch timed alone after the timed region."""
     import statistics
     layers = sorted(layers or [layer], reverse=True)
     rows = batch                      # k = 1: decoder rows = encoder rows
@@ -311,8 +317,19 @@ def dw_roofline(nat, layer, durations_ms, batch, steps_timed, fused_adam=True, l
             "avg_us": round(avg_s * 1e6, 2), "launches_timed": len(durations_ms),
             "algorithmic_bytes_per_launch": nbytes,
             "flops_per_launch": flops,
-            "timing": f"executor probe: HIP event pair around this launch on its stream, in "
-                      f"{steps_timed} eager steps right after the timed region"}
+            **({"avg_us_isolated": round(statistics.fmean(isolated_ms) * 1e3, 2),
+                "frac_isolated": round((nbytes if hbm_bound else flops / 1e3) /
+                                       (statistics.fmean(isolated_ms) / 1e3) / 1e9 / peak, 4)}
+               if in_timed and isolated_ms else {}),
+            "timing": (f"executor probe inside the timed region: events attached to this launch "
+                       f"(hipExtLaunchKernel start / stop) in each of the {steps_timed} timed steps, as "
+                       f"it runs beside the side stream's work"
+                       + ("; avg_us_isolated: the same launch alone (started once the side stream's "
+                          "earlier work is done), in eager steps right after the timed region"
+                          if isolated_ms else "")
+                       if in_timed else
+                       f"executor probe: HIP event pair around this launch on its stream, in "
+                       f"{steps_timed} eager steps right after the timed region")}
 
 
 def parse_args(argv=None):
@@ -468,6 +485,13 @@ def train_workload(args, cname, cfgd, rank, world, local, with_cpu):
     torch.cuda.synchronize()
     probe_layer = pick_dominant_layer(nat, batch)
     lib = _native.load()
+    # the dominant dW launch timed inside the timed steps themselves: events
+    # attached to that one launch (hipExtLaunchKernel start / stop, no marker
+    # packet, no wait for the side stream; mmad_ae_probe kind 3), read after
+    # the timed region
+    probe_timed = not args.no_probe and rank == 0 and not nat.use_graph
+    if probe_timed:
+        _native.check(lib.mmad_ae_probe(nat._h, 3, probe_layer, args.steps), "mmad_ae_probe")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -496,6 +520,17 @@ def train_workload(args, cname, cfgd, rank, world, local, with_cpu):
     if bad:
         raise SystemExit("bench: a kernel barrier timed out in the timed steps; no valid measurement")
     loss_v = float(loss.item())
+    durs_timed, layers_timed = [], None
+    if probe_timed:
+        import ctypes
+        tbuf = (ctypes.c_float * args.steps)()
+        nt = lib.mmad_ae_probe_read(nat._h, tbuf, args.steps)
+        if nt < 0:
+            _native.check(nt, "mmad_ae_probe_read")
+        durs_timed = list(tbuf[:nt])
+        tmask = lib.mmad_ae_probe_layers(nat._h)
+        layers_timed = [l for l in range(len(nat.layers)) if tmask > 0 and (tmask >> l) & 1] or [probe_layer]
+        _native.check(lib.mmad_ae_probe(nat._h, 1, -1, 0), "mmad_ae_probe")
 
     fpw, _ = ae_flops_per_window(nat.enc_widths, nat.dec_widths)
     windows = args.steps * batch * world
@@ -570,10 +605,11 @@ def train_workload(args, cname, cfgd, rank, world, local, with_cpu):
         model.dist = mdl_dist
     durs, n_probe, probe_layers, fwd_in_step = [], 0, None, []
     if not args.no_probe and rank == 0:
-        # the dominant kernel is timed by the executor's probe on eager steps
-        # of the same state and inputs right after the timed region (a HIP
-        # event pair around that one launch, on the stream it is launched on;
-        # the probe's events stay out of the timed steps)
+        # the same launch once more, isolated: eager steps of the same state
+        # and inputs right after the timed region, each probed launch started
+        # only once the side stream's earlier work is done (a HIP event pair
+        # around it on its stream) -- the kernel alone, beside the in-step
+        # figure above
         import ctypes
         n_probe = max(20, args.steps // 4)
         graph_mode = nat.use_graph
@@ -616,10 +652,13 @@ def train_workload(args, cname, cfgd, rank, world, local, with_cpu):
                          if nat.use_graph and (model.dist is None or not model.dist.native)
                          else "eager executor step (mmad_ae_train_step)")
     if rank == 0:
-        if durs:
-            # the probe steps are single-process fused steps (Adam in the dW epilogue)
-            res["roofline"] = dw_roofline(nat, probe_layer, durs, batch, n_probe, fused_adam=True,
-                                          layers=probe_layers)
+        if durs_timed or durs:
+            # fused steps (Adam in the dW epilogue): the timed steps' own
+            # launches when they were probed, else the isolated probe steps
+            res["roofline"] = dw_roofline(nat, probe_layer, durs_timed or durs, batch,
+                                          len(durs_timed) or n_probe, fused_adam=True,
+                                          layers=(layers_timed if durs_timed else probe_layers),
+                                          in_timed=bool(durs_timed), isolated_ms=durs)
         res["roofline_encoder_gemm"] = gemm_roofline(model, batch)
         if fwd_in_step:
             import statistics

@@ -173,6 +173,11 @@ struct mmad_ae {
   mutable unsigned probe_mask = 0;    // layers the last probed launch covered (bit l)
   std::vector<hipEvent_t> probe_ev;   // [2 * capacity]: start, end pairs
   hipEvent_t probe_sync = nullptr;    // a main-stream probe's start waits for the side stream
+  // probe kinds 2 / 3: the events ride on the launch itself (hipExtLaunchKernel
+  // start / stop: the kernel's own start and end, as rocprofv3's kernel records)
+  // and nothing waits for the side stream -- the launch as it runs in the
+  // step's schedule, so the probe can stay on through a timed region
+  bool probe_kev = false;
   // hipGraph-captured fused train steps (mmad_ae_train_step_graph): one per
   // call signature, replayed after a host->device copy of the per-call values
   // (a ring of pinned host slots, each reused only once its copy has run)
@@ -639,7 +644,7 @@ static int ae_gemm(const mmad_ae* h, const AeWS& w, int dt, int epi, const void*
   ep.sk_ctl = w.sk_ctl[r];
   const bool rec = probe >= 0 && probe == h->probe_id && !h->capturing &&
                    2 * h->probe_n < (int)h->probe_ev.size();
-  if (rec && h->side && s != h->side && h->probe_sync) {
+  if (rec && !h->probe_kev && h->side && s != h->side && h->probe_sync) {
     // a probed main-stream launch starts its clock once the side stream's
     // earlier GEMMs are done: its blocks (a whole CU's LDS each on the tail
     // tiles) wait for those CUs anyway, and the event pair then brackets the
@@ -649,11 +654,18 @@ static int ae_gemm(const mmad_ae* h, const AeWS& w, int dt, int epi, const void*
     MMAD_HIP_CHECK(hipEventRecord(h->probe_sync, h->side));
     MMAD_HIP_CHECK(hipStreamWaitEvent(s, h->probe_sync, 0));
   }
-  if (rec) MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n], s));
+  // kernel-attached events only where the launch carries no hand-off event
+  const bool kev = rec && h->probe_kev && !ep.done_ev;
+  if (kev) {
+    ep.start_ev = h->probe_ev[2 * h->probe_n];
+    ep.done_ev = h->probe_ev[2 * h->probe_n + 1];
+  } else if (rec) {
+    MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n], s));
+  }
   const int rc = mmad_gemm_dispatch(dt, epi, A, lda, B, ldb, Mp, Np, K, ep, s, cfg);
   if (rc != MMAD_OK) return rc;
   if (rec) {
-    MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n + 1], s));
+    if (!kev) MMAD_HIP_CHECK(hipEventRecord(h->probe_ev[2 * h->probe_n + 1], s));
     ++h->probe_n;
     h->probe_mask = 1u << (probe % 64);
   }
@@ -1620,7 +1632,8 @@ int mmad_ae_status(mmad_ae* h, void* ws, int64_t ws_bytes, void* stream) {
 
 int mmad_ae_probe(mmad_ae* h, int kind, int layer, int capacity) {
   MMAD_CHECK_ARG(h, "ae_probe: null handle");
-  MMAD_CHECK_ARG(kind == 0 || kind == 1, "ae_probe: kind must be 0 (forward GEMM) or 1 (dW GEMM)");
+  MMAD_CHECK_ARG(kind >= 0 && kind <= 3,
+                 "ae_probe: kind must be 0 / 1 (forward / dW GEMM) or 2 / 3 (the same, kernel-attached events)");
   MMAD_CHECK_ARG(capacity >= 0 && capacity <= 4096, "ae_probe: capacity out of range");
   MMAD_CHECK_ARG(layer < 0 || layer < (int)h->L.size(), "ae_probe: bad layer %d", layer);
   for (auto e : h->probe_ev) (void)hipEventDestroy(e);
@@ -1628,11 +1641,12 @@ int mmad_ae_probe(mmad_ae* h, int kind, int layer, int capacity) {
   h->probe_n = 0;
   h->probe_id = -1;
   h->probe_mask = 0;
+  h->probe_kev = kind >= 2;
   if (layer < 0 || capacity == 0) return MMAD_OK;
   h->probe_ev.resize(2 * (size_t)capacity, nullptr);
   for (auto& e : h->probe_ev) MMAD_HIP_CHECK(hipEventCreate(&e));
   if (!h->probe_sync) MMAD_HIP_CHECK(hipEventCreateWithFlags(&h->probe_sync, hipEventDisableTiming));
-  h->probe_id = (kind == 0 ? PROBE_FWD : PROBE_DW) + layer;
+  h->probe_id = ((kind & 1) == 0 ? PROBE_FWD : PROBE_DW) + layer;
   return MMAD_OK;
 }
 

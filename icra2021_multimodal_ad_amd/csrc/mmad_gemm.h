@@ -119,6 +119,9 @@ struct GemmEpi {
   // (hipExtLaunchKernel's stop event) instead of a separate hipEventRecord
   // behind it, whose marker packet holds the stream's next dispatch
   hipEvent_t done_ev;
+  // host only (nullable): an event that takes the launch's start time
+  // (hipExtLaunchKernel's start event; the executor's in-step kernel probe)
+  hipEvent_t start_ev;
 };
 
 int mmad_knob(int k);          // the tune table (mmad_tune_set)

@@ -2000,8 +2000,8 @@ int mmad_gemm_b4_launch(int epi, const void* A, int lda, const void* B, int ldb,
                         const GemmEpi& ep, hipStream_t s) {
   dim3 grd((Mp / 256) * (Np / 256)), blk(256);
   auto go = [&](auto kern) {
-    if (ep.done_ev)
-      hipExtLaunchKernelGGL(kern, grd, blk, 0u, s, nullptr, ep.done_ev, 0u, (const bf16*)A, lda,
+    if (ep.done_ev || ep.start_ev)
+      hipExtLaunchKernelGGL(kern, grd, blk, 0u, s, ep.start_ev, ep.done_ev, 0u, (const bf16*)A, lda,
                             (const bf16*)B, ldb, K, ep);
     else
       kern<<<grd, blk, 0, s>>>((const bf16*)A, lda, (const bf16*)B, ldb, K, ep);
@@ -2132,8 +2132,8 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
       ep.persist_tiles = ntiles;
       dim3 pg(cap), pb(CFG_NT[cfg]);
       auto args_go = [&](auto kern) {
-        if (ep.done_ev)
-          hipExtLaunchKernelGGL(kern, pg, pb, 0u, s, nullptr, ep.done_ev, 0u, A, lda, B, ldb, K, ep);
+        if (ep.done_ev || ep.start_ev)
+          hipExtLaunchKernelGGL(kern, pg, pb, 0u, s, ep.start_ev, ep.done_ev, 0u, A, lda, B, ldb, K, ep);
         else
           kern<<<pg, pb, 0, s>>>(A, lda, B, ldb, K, ep);
       };
@@ -2161,8 +2161,8 @@ static int launch_tiled(const T* A, int lda, const T* B, int ldb, int Mp, int Np
   const size_t dyn = 0;
   // the caller's completion event rides on the launch itself (no marker packet)
   auto go = [&](auto kern) {
-    if (ep.done_ev)
-      hipExtLaunchKernelGGL(kern, grd, blk, (std::uint32_t)dyn, s, nullptr, ep.done_ev, 0u, A, lda, B, ldb,
+    if (ep.done_ev || ep.start_ev)
+      hipExtLaunchKernelGGL(kern, grd, blk, (std::uint32_t)dyn, s, ep.start_ev, ep.done_ev, 0u, A, lda, B, ldb,
                             K, ep);
     else
       kern<<<grd, blk, dyn, s>>>(A, lda, B, ldb, K, ep);
@@ -2318,6 +2318,7 @@ static int tune_cfg(int dtype, int epi, const void* A, int lda, const void* B, i
   // launch rewrites: no fused Adam while timing
   GemmEpi et = ep;
   et.done_ev = nullptr;   // the real launch below completes the caller's event
+  et.start_ev = nullptr;
   et.ad_p = nullptr;
   et.sm_p = nullptr;
   et.bn_rmean = nullptr;   // fused BN: no running-statistics update while timing

@@ -519,7 +519,12 @@ int mmad_ae_status(mmad_ae* h, void* ws, int64_t ws_bytes, void* stream);
  * the next `capacity` calls.  layer < 0 or capacity 0 turns it off.  A
  * probed launch on the main stream starts its clock only after the side
  * stream's earlier work (in probed calls only), so the pair brackets the
- * launch's own execution as a profiler's kernel record does.
+ * launch's own execution as a profiler's kernel record does.  Kinds 2 / 3:
+ * the same launches (forward / dW) timed by events attached to the launch
+ * itself (hipExtLaunchKernel start / stop: the kernel's own start and end) and
+ * no wait for the side stream -- the launch as it runs in the step's schedule,
+ * beside the side stream's work, cheap enough to stay on through a timed
+ * region (bench.py's roofline).
  * mmad_ae_probe_read synchronises on the recorded events and writes up to
  * max_n durations (ms) in call order; returns how many (or < 0). */
 int mmad_ae_probe(mmad_ae* h, int kind, int layer, int capacity);
