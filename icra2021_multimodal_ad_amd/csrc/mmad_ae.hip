@@ -113,6 +113,13 @@ struct mmad_ae {
   // dw_late layers fork behind the layer's bwd-data + BN apply instead of at
   // its dz, so the largest dW does not share the CUs with the apply below it
   int dw_late = 0;
+  // knob 34 (ping-pong steps): each side-stream dW's fork event (dz_l ready)
+  // completed by the launch that produces dz_l (the BN-backward apply or the
+  // bwd-data GEMM: hipExtLaunchKernel stop event) instead of a marker packet
+  // recorded on the main stream before the bwd-data GEMM of l -- each marker
+  // held the main stream's next dispatch ~5 us; the top layer's fork is the
+  // loss reduction's wait on the MSE launch, already on the side stream
+  int fork_on_kernel = 1;
   hipEvent_t ev_hold = nullptr;
   // fused step: dW GEMMs of layers < dw_main run on the caller's stream
   // (knob 19; tools/sched_sweep.py: 0.499 ms (2) vs 0.512 (1) vs 0.523 (3));
@@ -415,6 +422,7 @@ int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, i
     h->dp_shard = mmad_knob(28);
     h->side_hold = mmad_knob(29);
     h->dw_late = mmad_knob(33);
+    h->fork_on_kernel = mmad_knob(34);
     h->dp_bucket_mib = mmad_knob(30) < 0 ? 0 : mmad_knob(30);
     h->dp_fork_rows = mmad_knob(14);
     h->ev_flags_ = ev_flags(mmad_knob(27));
@@ -828,12 +836,20 @@ static int finish_reductions(mmad_ae* h, AeWS& w, bool biases, bool from_mse, fl
 // dp_loss (data-parallel fused step): the loss output; the bias / gamma / beta
 // bucket and the loss are reduced and exchanged as soon as the backward chain
 // has produced the last bias partials, ahead of layer 0's weight bucket
+// side_after_mse: the side stream already waits for the MSE launch (the fused
+// step's loss reduction), so the top layer's dW needs no fork of its own
 static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const AdamHyper* adam,
-                        hipStream_t st, float* dp_loss = nullptr) {
+                        hipStream_t st, float* dp_loss = nullptr, bool side_after_mse = false) {
   const int dt = h->dtype;
   const int nL = (int)h->L.size();
   hipStream_t side = h->side;
   std::vector<PendingDW> pending;   // side-stream dW GEMMs waiting for a recorded event
+  // ev_fork[l] completed by the launch that produced dz_l (knob 34)
+  std::vector<char> fork_done(nL, 0);
+  const bool fork_kev = h->fork_on_kernel && !h->capturing;
+  auto forks_at_dz = [&](int l) {   // does layer l's side-stream dW fork behind dz_l (ping, not late)?
+    return adam && !h->comm && w.ping && l >= w.dw_main && l < nL - h->dw_late;
+  };
   std::vector<DpBucket> plan;       // data parallel: the exchange buckets (dp_plan)
   int next_bucket = 0;
   if (adam && h->comm) dp_plan(h, plan);
@@ -898,7 +914,10 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     // shadow, so dW_l may start as soon as dz_l is complete
     const bool ping = adam && !dp && w.ping && l >= w.dw_main;
     const bool late = ping && l >= nL - h->dw_late;
-    if (ping && !late) {
+    // the top layer's dz is the MSE output, which the side stream has waited
+    // for already (the loss reduction): no fork
+    const bool fork_none = ping && !late && l == nL - 1 && from_mse && side_after_mse && fork_kev;
+    if (ping && !late && !fork_none && !fork_done[l]) {
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
     }
     // does the main stream record ev_data[l] (bwd-data of l done)?  Needed by
@@ -967,6 +986,8 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
       ep.N = a.K;
       ep.ldo = a.Kp;
       ep.ldpart = a.Kp;
+      // dz_{l-1} is produced below: its side-stream dW fork rides on that launch
+      const bool attach = fork_kev && forks_at_dz(l - 1);
       if (h->vib && l == h->n_enc) {
         ep.out = w.dzin;
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
@@ -997,20 +1018,30 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
           ep.done_ev = h->ev_data[l];
           ev_attached = true;
         }
+        if (attach && ps.bwd_fused && !ep.done_ev) {
+          ep.done_ev = h->ev_fork[l - 1];
+          fork_done[l - 1] = 1;
+        }
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
                                   a.Np, ep, st));
         if (rec && !ev_attached) MMAD_HIP_CHECK(hipEventRecord(h->ev_data[l], st));
-        if (!ps.bwd_fused)
-          RET_IF(mmad_bn_act_bwd_apply(dt, p.act, h->slope, rows_of(w, p), p.N, Mpp, p.Np, ps.dy,
-                                       ps.out, ps.mean, ps.rstd, h->params + p.g_off, ps.bnpart,
-                                       Mpp / 64, ps.dz, h->grads + p.g_off, h->grads + p.be_off,
-                                       ps.dbpart, st));
+        if (!ps.bwd_fused) {
+          RET_IF(mmad_bn_act_bwd_apply_ev(dt, p.act, h->slope, rows_of(w, p), p.N, Mpp, p.Np, ps.dy,
+                                          ps.out, ps.mean, ps.rstd, h->params + p.g_off, ps.bnpart,
+                                          Mpp / 64, ps.dz, h->grads + p.g_off, h->grads + p.be_off,
+                                          ps.dbpart, st, attach ? h->ev_fork[l - 1] : nullptr));
+          if (attach) fork_done[l - 1] = 1;
+        }
       } else {
         ep.out = ps.dy;
         ep.part = ps.stats;
         if (rec && h->ev_on_kernel && !h->capturing) {
           ep.done_ev = h->ev_data[l];
           ev_attached = true;
+        }
+        if (attach && !ep.done_ev) {
+          ep.done_ev = h->ev_fork[l - 1];
+          fork_done[l - 1] = 1;
         }
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_DATA, dz, a.Np, weights(h, a), a.Kp, Mp, a.Kp,
                                   a.Np, ep, st));
@@ -1094,7 +1125,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
         pending.push_back(PendingDW{dz, in, a.Np, a.Kp, a.Np, a.Kp, Mp, dwe, l});
       } else if (ping) {
         if (late) MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
-        MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
+        if (!fork_none) MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
                        nullptr, PROBE_DW + l));
       } else if (!rec) {
@@ -1216,7 +1247,7 @@ int mmad_ae_train_step(mmad_ae* h, const float* x, int ld_x, int B, int k, const
     if (!loss_ev_on_kernel) MMAD_HIP_CHECK(hipEventRecord(h->ev_loss, st));
     MMAD_HIP_CHECK(hipStreamWaitEvent(h->side, h->ev_loss, 0));
     RET_IF(finish_reductions(h, w, false, true, beta_kl, loss_out, h->side));
-    RET_IF(run_backward(h, w, true, beta_kl, &ah, st));
+    RET_IF(run_backward(h, w, true, beta_kl, &ah, st, nullptr, true));
     if (w.ping) std::swap(h->shadow, h->shadow_alt);
     return MMAD_OK;
   }

@@ -70,6 +70,7 @@ int g_knob[MMAD_KNOB_COUNT] = {
     1,     // 31 bwd-data hand-off events completed by the GEMM launch (hipExtLaunchKernel)
     1024,  // 32 fp32 dW split rule from 2048 rows: target 64x64-tile blocks (0 = no split)
     0,     // 33 ping-pong: the top n layers' side dW forks after their bwd-data + apply
+    1,     // 34 ping-pong: side dW fork events completed by the launch producing dz
 };
 }  // namespace
 int mmad_knob(int k) { return g_knob[k]; }

@@ -79,3 +79,10 @@ int mmad_bn_act_bwd_apply(int dtype, int act, float slope, int M, int N, int Mp,
                           const float* save_rstd, const float* gamma, const double* part,
                           int nparts, void* dz, float* dgamma, float* dbeta, float* db_partials,
                           void* stream);
+// the same, with `done` (nullable) completed by the launch itself
+// (hipExtLaunchKernel stop event: no marker packet behind it)
+int mmad_bn_act_bwd_apply_ev(int dtype, int act, float slope, int M, int N, int Mp, int Np,
+                             const void* dy, const void* a, const float* save_mean,
+                             const float* save_rstd, const float* gamma, const double* part,
+                             int nparts, void* dz, float* dgamma, float* dbeta, float* db_partials,
+                             void* stream, void* done);

@@ -7,6 +7,8 @@
 #include "mmad_ops.h"
 #include "mmad_gemm.h"
 
+#include <hip/hip_ext.h>
+
 #include <charconv>
 #include <cmath>
 #include <cstdio>
@@ -1000,6 +1002,15 @@ int mmad_bn_act_bwd_apply(int dtype, int act, float slope, int M, int N, int Mp,
                           const float* save_rstd, const float* gamma, const double* part,
                           int nparts, void* dz, float* dgamma, float* dbeta, float* db_partials,
                           void* stream) {
+  return mmad_bn_act_bwd_apply_ev(dtype, act, slope, M, N, Mp, Np, dy, a, save_mean, save_rstd, gamma,
+                                  part, nparts, dz, dgamma, dbeta, db_partials, stream, nullptr);
+}
+
+int mmad_bn_act_bwd_apply_ev(int dtype, int act, float slope, int M, int N, int Mp, int Np,
+                             const void* dy, const void* a, const float* save_mean,
+                             const float* save_rstd, const float* gamma, const double* part,
+                             int nparts, void* dz, float* dgamma, float* dbeta, float* db_partials,
+                             void* stream, void* done) {
   // 128-row slabs per block (knob 13: 1, 2 or 4; any other value = 1; halved
   // until it divides the row slabs): the column partials are merged once per
   // block instead of once per 128-row slab
@@ -1010,10 +1021,16 @@ int mmad_bn_act_bwd_apply(int dtype, int act, float slope, int M, int N, int Mp,
   hipStream_t s = (hipStream_t)stream;
   const bool wide = nparts > 4 * 8;   // 16 partial chunks per round trip (8 no faster, r02bj_*)
   const bool lk = act == MMAD_ACT_LEAKYRELU;
+  hipEvent_t dev = (hipEvent_t)done;
 #define MMAD_BNB_T(T, PU_, RB_, LK_)                                                                   \
-  bn_bwd_apply_k<T, PU_, RB_, LK_><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const T*)dy,     \
-                                                       (const T*)a, save_mean, save_rstd, gamma, part, \
-                                                       (T*)dz, dgamma, dbeta, db_partials);
+  if (dev)                                                                                             \
+    hipExtLaunchKernelGGL(bn_bwd_apply_k<T, PU_, RB_, LK_>, grd, dim3(256), 0u, s, nullptr, dev, 0u, act, \
+                          slope, M, N, Np, nparts, (const T*)dy, (const T*)a, save_mean, save_rstd,    \
+                          gamma, part, (T*)dz, dgamma, dbeta, db_partials);                           \
+  else                                                                                                 \
+    bn_bwd_apply_k<T, PU_, RB_, LK_><<<grd, 256, 0, s>>>(act, slope, M, N, Np, nparts, (const T*)dy,   \
+                                                         (const T*)a, save_mean, save_rstd, gamma,     \
+                                                         part, (T*)dz, dgamma, dbeta, db_partials);
 #define MMAD_BNB(PU_, RB_)                   \
   if (dtype == MMAD_BF16) {                  \
     if (lk) {                                \

@@ -105,8 +105,13 @@ int mmad_pad_granule(void);
  *      slice (1024; 0 = never split an fp32 GEMM)
  *   33 ping-pong steps: the side-stream dW + Adam GEMMs of the top this many
  *      layers start once the main stream has also finished the layer's
- *      bwd-data GEMM and BN-backward apply, instead of at its dz (0) */
-#define MMAD_KNOB_COUNT 34
+ *      bwd-data GEMM and BN-backward apply, instead of at its dz (0)
+ *   34 ping-pong steps: each side-stream dW's fork event completed by the
+ *      launch that produces the layer's dz (BN-backward apply or bwd-data
+ *      GEMM, hipExtLaunchKernel stop event) instead of a marker packet on the
+ *      main stream; the top layer forks through the loss reduction's wait on
+ *      the MSE launch (1; 0 = markers) */
+#define MMAD_KNOB_COUNT 35
 int mmad_tune_set(int knob, int value);
 int mmad_tune_get(int knob, int* value);
 /* The split-K factor the dispatcher picks for a padded GEMM shape (Mp x Np

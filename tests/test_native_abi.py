@@ -66,12 +66,12 @@ def test_tune_table_names_and_defaults(lib):
     defaults the benches rely on."""
     import ctypes
     from icra2021_multimodal_ad_amd._native import KNOB
-    assert sorted(KNOB.values()) == list(range(34))
-    assert lib.mmad_tune_set(34, 0) == -1
+    assert sorted(KNOB.values()) == list(range(35))
+    assert lib.mmad_tune_set(35, 0) == -1
     v = ctypes.c_int()
     for name, want in (("dp_fork_rows", 1024), ("dp_bucket_mib", 8), ("dp_shard", 1), ("persist", 0),
                        ("bn_apply_rb", 2), ("ev_on_kernel", 1), ("side_cu_held", 0),
-                       ("splitk_dw_f32_blocks", 1024), ("dw_late", 0)):
+                       ("splitk_dw_f32_blocks", 1024), ("dw_late", 0), ("fork_on_kernel", 1)):
         assert lib.mmad_tune_get(KNOB[name], ctypes.byref(v)) == 0
         assert v.value == want, (name, v.value)
 
