@@ -126,7 +126,7 @@ KNOB = dict(tile=0, group_m=1, autotune=2, dbg=3, splitk=4, tile_adam=5, tile_bw
             persist=12, bn_apply_rb=13, side_cu_held=15,
             bn_mode=16, bn_mode_bwd=17, bn_fused_rows=18, dw_main=19, pair_rows=20, dw_main_ping=21,
             ev_every=22, loss_side=23, dp_small_at=24, keep_grads=25, side_prio=26,
-            event_sysfence=27, dp_shard=28, side_hold=29, dp_bucket_mib=30, ev_on_kernel=31, dw_late=33, fork_on_kernel=34, dp_fork_rows=14,
+            event_sysfence=27, dp_shard=28, side_hold=29, dp_bucket_mib=30, ev_on_kernel=31, dw_late=33, fork_on_kernel=34, fork_pair_below=35, dp_fork_rows=14,
             splitk_dw_f32_blocks=32)
 # host-side schedule choices of the Python executor wrapper (engine.py), read
 # when a model is built: a second bf16 weight shadow (ping-pong), and whether

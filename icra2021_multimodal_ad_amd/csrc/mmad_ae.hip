@@ -120,6 +120,12 @@ struct mmad_ae {
   // held the main stream's next dispatch ~5 us; the top layer's fork is the
   // loss reduction's wait on the MSE launch, already on the side stream
   int fork_on_kernel = 1;
+  // knob 35 (ping-pong steps): from this layer down, side-stream dW GEMMs
+  // fork in pairs -- every other layer's dz gets no fork event and its dW is
+  // issued with the next lower layer's (where the side stream lags the chain
+  // by more than a layer anyway, each fork saved is a ~5-us hold on the
+  // main stream; 0 = every layer forks)
+  int fork_pair_below = 0;
   hipEvent_t ev_hold = nullptr;
   // fused step: dW GEMMs of layers < dw_main run on the caller's stream
   // (knob 19; tools/sched_sweep.py: 0.499 ms (2) vs 0.512 (1) vs 0.523 (3));
@@ -423,6 +429,7 @@ int mmad_ae_create(mmad_ae** out, int dtype, int n_enc, const int* enc_widths, i
     h->side_hold = mmad_knob(29);
     h->dw_late = mmad_knob(33);
     h->fork_on_kernel = mmad_knob(34);
+    h->fork_pair_below = mmad_knob(35);
     h->dp_bucket_mib = mmad_knob(30) < 0 ? 0 : mmad_knob(30);
     h->dp_fork_rows = mmad_knob(14);
     h->ev_flags_ = ev_flags(mmad_knob(27));
@@ -847,8 +854,14 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
   // ev_fork[l] completed by the launch that produced dz_l (knob 34)
   std::vector<char> fork_done(nL, 0);
   const bool fork_kev = h->fork_on_kernel && !h->capturing;
+  // does layer l's side-stream dW (ping) get a fork event of its own (knob 35)?
+  auto fork_ev = [&](int l) {
+    const int P = h->fork_pair_below;
+    if (P <= 0 || l > P || l == w.dw_main) return true;
+    return (P - l) % 2 == 1;
+  };
   auto forks_at_dz = [&](int l) {   // does layer l's side-stream dW fork behind dz_l (ping, not late)?
-    return adam && !h->comm && w.ping && l >= w.dw_main && l < nL - h->dw_late;
+    return adam && !h->comm && w.ping && l >= w.dw_main && l < nL - h->dw_late && fork_ev(l);
   };
   std::vector<DpBucket> plan;       // data parallel: the exchange buckets (dp_plan)
   int next_bucket = 0;
@@ -917,7 +930,7 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
     // the top layer's dz is the MSE output, which the side stream has waited
     // for already (the loss reduction): no fork
     const bool fork_none = ping && !late && l == nL - 1 && from_mse && side_after_mse && fork_kev;
-    if (ping && !late && !fork_none && !fork_done[l]) {
+    if (ping && !late && !fork_none && !fork_done[l] && fork_ev(l)) {
       MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
     }
     // does the main stream record ev_data[l] (bwd-data of l done)?  Needed by
@@ -1123,9 +1136,16 @@ static int run_backward(mmad_ae* h, AeWS& w, bool from_mse, float beta_kl, const
                        nullptr, PROBE_DW + l));
       } else if (h->side_hold) {
         pending.push_back(PendingDW{dz, in, a.Np, a.Kp, a.Np, a.Kp, Mp, dwe, l});
+      } else if (ping && !late && !fork_ev(l)) {
+        // no fork of its own: issued with the next lower layer's dW
+        pending.push_back(PendingDW{dz, in, a.Np, a.Kp, a.Np, a.Kp, Mp, dwe, l});
       } else if (ping) {
         if (late) MMAD_HIP_CHECK(hipEventRecord(h->ev_fork[l], st));
         if (!fork_none) MMAD_HIP_CHECK(hipStreamWaitEvent(side, h->ev_fork[l], 0));
+        for (const PendingDW& q : pending)
+          RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, q.dz, q.lda, q.in, q.ldb, q.M, q.N, q.K, q.ep,
+                         side, nullptr, PROBE_DW + q.layer));
+        pending.clear();
         RET_IF(ae_gemm(h, w, dt, GEMM_EPI_BWD_WEIGHT, dz, a.Np, in, a.Kp, a.Np, a.Kp, Mp, dwe, side,
                        nullptr, PROBE_DW + l));
       } else if (!rec) {

@@ -71,6 +71,7 @@ int g_knob[MMAD_KNOB_COUNT] = {
     1024,  // 32 fp32 dW split rule from 2048 rows: target 64x64-tile blocks (0 = no split)
     0,     // 33 ping-pong: the top n layers' side dW forks after their bwd-data + apply
     1,     // 34 ping-pong: side dW fork events completed by the launch producing dz
+    0,     // 35 ping-pong: side dW forks in pairs from this layer down (0 = every layer)
 };
 }  // namespace
 int mmad_knob(int k) { return g_knob[k]; }

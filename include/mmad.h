@@ -110,8 +110,11 @@ int mmad_pad_granule(void);
  *      launch that produces the layer's dz (BN-backward apply or bwd-data
  *      GEMM, hipExtLaunchKernel stop event) instead of a marker packet on the
  *      main stream; the top layer forks through the loss reduction's wait on
- *      the MSE launch (1; 0 = markers) */
-#define MMAD_KNOB_COUNT 35
+ *      the MSE launch (1; 0 = markers)
+ *   35 ping-pong steps: from this layer down the side-stream dW GEMMs fork in
+ *      pairs -- every other layer's dz gets no fork event and its dW is issued
+ *      with the next lower layer's (0 = every layer forks) */
+#define MMAD_KNOB_COUNT 36
 int mmad_tune_set(int knob, int value);
 int mmad_tune_get(int knob, int* value);
 /* The split-K factor the dispatcher picks for a padded GEMM shape (Mp x Np

@@ -1,5 +1,5 @@
 """Fused-step schedule variants give the same bits as the default schedule:
-every schedule knob of the tune table (include/mmad.h knobs 15, 19-31, 33, 34, read when
+every schedule knob of the tune table (include/mmad.h knobs 15, 19-31, 33-35, read when
 a model handle is created) and the host-side shadow pair only reorder
 independent work across streams."""
 import pytest
@@ -16,7 +16,9 @@ pytestmark = pytest.mark.gpu
     {"pair_rows": 0}, {"pair_rows": 0, "dw_main_ping": 0}, {"shadow_pair": False},
     {"side_prio": 1}, {"event_sysfence": 1}, {"keep_grads": 1}, {"ev_on_kernel": 0},
     {"side_cu_held": 32}, {"pair_rows": 0, "dw_late": 1}, {"pair_rows": 0, "dw_late": 99},
-    {"pair_rows": 0, "fork_on_kernel": 0}, {"pair_rows": 0, "fork_on_kernel": 0, "ev_on_kernel": 0}])
+    {"pair_rows": 0, "fork_on_kernel": 0}, {"pair_rows": 0, "fork_on_kernel": 0, "ev_on_kernel": 0},
+    {"pair_rows": 0, "fork_pair_below": 4}, {"pair_rows": 0, "fork_pair_below": 9},
+    {"pair_rows": 0, "fork_pair_below": 9, "fork_on_kernel": 0}])
 def test_schedule_knobs_match_default(knobs):
     """Every schedule knob of the fused step only reorders independent work
     across streams (event coalescing, where the loss is reduced, how many dW

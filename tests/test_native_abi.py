@@ -66,8 +66,8 @@ def test_tune_table_names_and_defaults(lib):
     defaults the benches rely on."""
     import ctypes
     from icra2021_multimodal_ad_amd._native import KNOB
-    assert sorted(KNOB.values()) == list(range(35))
-    assert lib.mmad_tune_set(35, 0) == -1
+    assert sorted(KNOB.values()) == list(range(36))
+    assert lib.mmad_tune_set(36, 0) == -1
     v = ctypes.c_int()
     for name, want in (("dp_fork_rows", 1024), ("dp_bucket_mib", 8), ("dp_shard", 1), ("persist", 0),
                        ("bn_apply_rb", 2), ("ev_on_kernel", 1), ("side_cu_held", 0),
