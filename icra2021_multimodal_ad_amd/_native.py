@@ -120,7 +120,7 @@ SIGNATURES = {
 
 
 # the library's tune table (include/mmad.h, mmad_tune_set): GEMM knobs are read
-# per dispatch, the schedule knobs (14-31) when a model handle is created
+# per dispatch, the schedule knobs (14-31, 33-35) when a model handle is created
 KNOB = dict(tile=0, group_m=1, autotune=2, dbg=3, splitk=4, tile_adam=5, tile_bwd_data=6,
             tile_fwd=7, tile_adam_main=8, splitk_dw=9, splitk_dw_blocks=10, splitk_dw_min_stages=11,
             persist=12, bn_apply_rb=13, side_cu_held=15,

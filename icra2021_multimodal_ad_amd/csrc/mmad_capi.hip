@@ -32,7 +32,7 @@ int mmad_pad_granule(void) { return MMAD_PAD; }
 // Tuning knobs: ONE table, set only through mmad_tune_set (the library reads
 // no environment variables, so every rank of a job runs the same schedule
 // unless its code says otherwise).  GEMM knobs (0-11) are read per dispatch;
-// the executor's schedule knobs (14-31) are copied into a handle when it is
+// the executor's schedule knobs (14-31, 33-35) are copied into a handle when it is
 // created (mmad_ae_create), so a handle keeps one schedule for its lifetime.
 namespace {
 int g_knob[MMAD_KNOB_COUNT] = {

@@ -45,7 +45,7 @@ int mmad_abi_version(void);
 int mmad_pad_granule(void);
 /* Tuning knobs (no reference counterpart).  One process-wide table, set only
  * through mmad_tune_set (the library reads no environment variables).  GEMM
- * knobs are read per dispatch; the executor's schedule knobs (16-30) are
+ * knobs are read per dispatch; the executor's schedule knobs (14-31, 33-35) are
  * copied into a handle by mmad_ae_create, so set them before creating it.
  *   0  GEMM tile override (-1 autotuned; 0 = 128x128/512 thr, 1 = 256x128,
  *      2 = 128x256, 3 = 64x64/256 thr, 4 = 64x128, 5 = 128x128/256 thr,
