@@ -489,9 +489,10 @@ def train_workload(args, cname, cfgd, rank, world, local, with_cpu):
     # attached to that one launch (hipExtLaunchKernel start / stop, no marker
     # packet, no wait for the side stream; mmad_ae_probe kind 3), read after
     # the timed region
-    probe_timed = not args.no_probe and rank == 0 and not nat.use_graph
+    probe_timed = not args.no_probe and rank == 0 and not nat.use_graph and args.steps > 0
+    n_cap = min(args.steps, 4096)              # the executor's probe capacity limit: the first 4096 steps
     if probe_timed:
-        _native.check(lib.mmad_ae_probe(nat._h, 3, probe_layer, args.steps), "mmad_ae_probe")
+        _native.check(lib.mmad_ae_probe(nat._h, 3, probe_layer, n_cap), "mmad_ae_probe")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -523,8 +524,8 @@ def train_workload(args, cname, cfgd, rank, world, local, with_cpu):
     durs_timed, layers_timed = [], None
     if probe_timed:
         import ctypes
-        tbuf = (ctypes.c_float * args.steps)()
-        nt = lib.mmad_ae_probe_read(nat._h, tbuf, args.steps)
+        tbuf = (ctypes.c_float * n_cap)()
+        nt = lib.mmad_ae_probe_read(nat._h, tbuf, n_cap)
         if nt < 0:
             _native.check(nt, "mmad_ae_probe_read")
         durs_timed = list(tbuf[:nt])
@@ -611,7 +612,7 @@ def train_workload(args, cname, cfgd, rank, world, local, with_cpu):
         # around it on its stream) -- the kernel alone, beside the in-step
         # figure above
         import ctypes
-        n_probe = max(20, args.steps // 4)
+        n_probe = min(4096, max(20, args.steps // 4))
         graph_mode = nat.use_graph
         nat.use_graph = False
         _native.check(lib.mmad_ae_probe(nat._h, 1, probe_layer, n_probe), "mmad_ae_probe")
